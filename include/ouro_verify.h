@@ -1,0 +1,160 @@
+/*
+ * ouro_verify.h -- C-ABI drop-in boundary of the MI355X (gfx950) batch verifier
+ * for the Ouroboros Praos/TPraos header-crypto hot path.
+ *
+ * The reference (dizgotti/ouroboros-network) reaches this arithmetic through
+ * cardano-crypto-class / cardano-crypto-praos, whose Haskell instances bind C
+ * symbols with `foreign import ccall`.  Each entry point below
+ * names the reference interface it replaces.  Plain pointers and sizes only;
+ * no HIP or torch types cross this boundary.
+ *
+ * Semantics shared by every call:
+ *   - Return 0 = valid / OURO_OK, -1 = invalid (single-item calls), or a
+ *     negative OURO_E* status for a call that could not run.  A device or
+ *     runtime failure NEVER reports "valid": batch verdicts are then left
+ *     untouched and the call returns OURO_EDEVICE.
+ *   - The caller owns every buffer; nothing is retained after return.
+ *   - All calls are thread-safe and reentrant: each calling thread gets its own
+ *     HIP stream and staging buffers on the current device.
+ *   - Byte layouts are the raw encodings of cardano-crypto-class:
+ *     VerKeyDSIGN/VerKeyVRF/VerKeyKES 32 B, SigDSIGN 64 B, CertVRF (proof) 80 B,
+ *     OutputVRF 64 B, SigKES (Sum6KES Ed25519DSIGN Blake2b_256) 448 B.
+ */
+#ifndef OURO_VERIFY_H
+#define OURO_VERIFY_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define OURO_OK 0
+#define OURO_INVALID (-1)
+#define OURO_EDEVICE (-2) /* HIP/runtime error; nothing was verified      */
+#define OURO_EINVAL (-3)  /* bad arguments (NULL with n > 0, sizes, ...)  */
+#define OURO_ENODEV (-4)  /* no usable gfx950 device                      */
+
+/* Per-header verdict bits (ouro_tpraos_verify_batch). */
+#define OURO_HDR_OCERT_OK 0x01u      /* Ed25519 over OCertSignable            */
+#define OURO_HDR_KES_OK 0x02u        /* Sum6KES over the header body          */
+#define OURO_HDR_VRF_ETA_OK 0x04u    /* nonce VRF proof                       */
+#define OURO_HDR_VRF_LEADER_OK 0x08u /* leader VRF proof                      */
+#define OURO_HDR_ALL_OK 0x0fu
+
+/* ------------------------------------------------------------------ setup */
+
+/* Select the HIP device used by the calling thread (default: current device).
+ * Returns OURO_OK or OURO_ENODEV. */
+int ouro_set_device(int device);
+
+/* Human-readable last error of the calling thread ("" if none). */
+const char *ouro_last_error(void);
+
+/* ----------------------------------------- single item (ABI-identical) --- */
+
+/* Replaces libsodium 1.0.18 crypto_sign_ed25519_verify_detached, the symbol
+ * cardano-crypto-class Ed25519DSIGN.verifyDSIGN binds (callers
+ * ouroboros-consensus-shelley/src/Ouroboros/Consensus/Shelley/Protocol.hs:435 via
+ * the OCERT rule, ouroboros-consensus-cardano/src/Ouroboros/Consensus/Cardano/
+ * CanHardFork.hs:360).  0 = valid, -1 = invalid, <= -2 = error. */
+int ouro_ed25519_verify(const unsigned char *sig, const unsigned char *m,
+                        unsigned long long mlen, const unsigned char *pk);
+
+/* Replaces crypto_vrf_ietfdraft03_verify (cardano-crypto-praos, bound by
+ * PraosVRF.verifyVRF / verifyCertified; caller: OVERLAY vrfChecks via
+ * Shelley/Protocol.hs:435).  On success writes the 64-byte output. */
+int ouro_vrf03_verify(unsigned char *output, const unsigned char *pk,
+                      const unsigned char *proof, const unsigned char *msg,
+                      unsigned long long msglen);
+
+/* Replaces crypto_vrf_ietfdraft03_proof_to_hash (VRF.certifiedOutput,
+ * Shelley/Ledger/TPraos.hs:40).  Does not verify the proof. */
+int ouro_vrf03_proof_to_hash(unsigned char *output, const unsigned char *proof);
+
+/* Replaces SumKES.verifyKES (Sum6KES Ed25519DSIGN Blake2b_256), called via
+ * SL.verifySignedKES at ouroboros-consensus-shelley/src/Ouroboros/Consensus/
+ * Shelley/Ledger/Integrity.hs:27.  t = KES period relative to the opcert. */
+int ouro_sum6kes_verify(const unsigned char *vk, unsigned int t, const unsigned char *m,
+                        unsigned long long mlen, const unsigned char *sig);
+
+/* --------------------------------------------- batch, host buffers ------ */
+/* H2D + kernel + D2H on the calling thread's stream; blocks until done.
+ * Messages are addressed by (offset, length) into one buffer.
+ * verdict[i] = 1 (valid) / 0 (invalid). */
+
+int ouro_ed25519_verify_batch(size_t n, const uint8_t *pk /* n x 32 */,
+                              const uint8_t *sig /* n x 64 */, const uint8_t *msg,
+                              const uint64_t *msg_off, const uint32_t *msg_len,
+                              uint8_t *verdict);
+
+/* beta[i] = 64-byte output on success, zeros otherwise */
+int ouro_vrf03_verify_batch(size_t n, const uint8_t *pk /* n x 32 */,
+                            const uint8_t *proof /* n x 80 */, const uint8_t *alpha,
+                            const uint64_t *alpha_off, const uint32_t *alpha_len,
+                            uint8_t *beta /* n x 64 */, uint8_t *verdict);
+
+int ouro_sum6kes_verify_batch(size_t n, const uint8_t *vk /* n x 32 */,
+                              const uint32_t *t, const uint8_t *msg, const uint64_t *msg_off,
+                              const uint32_t *msg_len, const uint8_t *sig /* n x 448 */,
+                              uint8_t *verdict);
+
+/* The crypto subset of SL.updateChainDepState for a batch of TPraos headers,
+ * reached in the reference via TPraos.updateChainDepState
+ * (ouroboros-consensus-shelley/src/Ouroboros/Consensus/Shelley/Protocol.hs:433-442):
+ * OCERT (Ed25519 over hotVk || BE64(counter) || BE64(kesPeriod), then Sum6KES
+ * over the raw header body) and OVERLAY (the eta and leader VRFs over the
+ * caller's mkSeed values).  Structure-of-arrays, one entry per header. */
+typedef struct ouro_tpraos_batch {
+  size_t n;
+  const uint8_t *issuer_vk;        /* n x 32  bheaderVk (cold key)            */
+  const uint8_t *vrf_vk;           /* n x 32  bheaderVrfVk                    */
+  const uint8_t *eta_proof;        /* n x 80  bheaderEta proof                */
+  const uint8_t *leader_proof;     /* n x 80  bheaderL proof                  */
+  const uint8_t *eta_alpha;        /* n x 32  mkSeed seedEta slot eta0        */
+  const uint8_t *leader_alpha;     /* n x 32  mkSeed seedL   slot eta0        */
+  const uint8_t *hot_vk;           /* n x 32  ocertVkHot (Sum6KES root)       */
+  const uint64_t *ocert_counter;   /* n       ocertN                          */
+  const uint64_t *ocert_kes_period;/* n       ocertKESPeriod (c0)             */
+  const uint8_t *ocert_sigma;      /* n x 64  ocertSigma                      */
+  const uint32_t *kes_t;           /* n       kesPeriod(slot) - c0, clamped   */
+  const uint8_t *kes_sig;          /* n x 448 header KES signature            */
+  const uint8_t *body;             /* concatenated raw header-body CBOR       */
+  const uint64_t *body_off;        /* n                                       */
+  const uint32_t *body_len;        /* n                                       */
+} ouro_tpraos_batch;
+
+/* verdict[i] = OURO_HDR_* bits; beta_eta / beta_leader (n x 64, may be NULL)
+ * receive the computed VRF outputs (zeros where a proof fails). */
+int ouro_tpraos_verify_batch(const ouro_tpraos_batch *b, uint8_t *verdict,
+                             uint8_t *beta_eta, uint8_t *beta_leader);
+
+/* ----------------------------------- batch, device-resident buffers ----- */
+/* Same kernels on caller-owned device memory, enqueued on `stream` (a
+ * hipStream_t, NULL = the thread's stream) and NOT synchronised: the caller
+ * orders its own copies/events around them.  `msg_off`/`msg_len` etc. are
+ * device pointers too.  Used by bench.py (inputs resident in HBM) and by
+ * pipelined callers that overlap H2D of the next window with this one. */
+
+int ouro_ed25519_verify_batch_device(void *stream, size_t n, const uint8_t *pk,
+                                     const uint8_t *sig, const uint8_t *msg,
+                                     const uint64_t *msg_off, const uint32_t *msg_len,
+                                     uint8_t *verdict);
+int ouro_vrf03_verify_batch_device(void *stream, size_t n, const uint8_t *pk,
+                                   const uint8_t *proof, const uint8_t *alpha,
+                                   const uint64_t *alpha_off, const uint32_t *alpha_len,
+                                   uint8_t *beta, uint8_t *verdict);
+int ouro_sum6kes_verify_batch_device(void *stream, size_t n, const uint8_t *vk,
+                                     const uint32_t *t, const uint8_t *msg,
+                                     const uint64_t *msg_off, const uint32_t *msg_len,
+                                     const uint8_t *sig, uint8_t *verdict);
+/* `b` is a host struct whose pointers are device pointers */
+int ouro_tpraos_verify_batch_device(void *stream, const ouro_tpraos_batch *b,
+                                    uint8_t *verdict, uint8_t *beta_eta,
+                                    uint8_t *beta_leader);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* OURO_VERIFY_H */

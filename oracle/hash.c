@@ -1,0 +1,190 @@
+/*
+ * hash.c -- SHA-512 (FIPS 180-4) and unkeyed Blake2b (RFC 7693).
+ * TEST INFRASTRUCTURE ONLY (see oracle.h).
+ *
+ * Restates libsodium 1.0.18 crypto_hash_sha512 and crypto_generichash_blake2b
+ * (key = NULL), which cardano-crypto-class binds for SHA-512 inside Ed25519/VRF
+ * and for Blake2b_256 (the KES Merkle hash, hashPairOfVKeys).  Call sites in
+ * the reference: Shelley/Ledger/Integrity.hs:27 (KES), Shelley/Protocol.hs:435
+ * (VRF/Ed25519 via ledger-specs).  Pinned by tests/test_oracle.py against the
+ * conda libsodium 1.0.18 build.
+ */
+#include "internal.h"
+#include <string.h>
+
+static inline uint64_t rotr64(uint64_t x, unsigned n) { return (x >> n) | (x << (64 - n)); }
+static inline uint64_t load_be64(const uint8_t *p) {
+  uint64_t v = 0;
+  for (int i = 0; i < 8; i++) v = (v << 8) | p[i];
+  return v;
+}
+static inline void store_be64(uint8_t *p, uint64_t v) {
+  for (int i = 7; i >= 0; i--) { p[i] = (uint8_t)v; v >>= 8; }
+}
+static inline uint64_t load_le64(const uint8_t *p) {
+  uint64_t v = 0;
+  for (int i = 7; i >= 0; i--) v = (v << 8) | p[i];
+  return v;
+}
+
+/* ------------------------------------------------------------ SHA-512 ---- */
+static const uint64_t K512[80] = {
+    0x428a2f98d728ae22ULL, 0x7137449123ef65cdULL, 0xb5c0fbcfec4d3b2fULL, 0xe9b5dba58189dbbcULL,
+    0x3956c25bf348b538ULL, 0x59f111f1b605d019ULL, 0x923f82a4af194f9bULL, 0xab1c5ed5da6d8118ULL,
+    0xd807aa98a3030242ULL, 0x12835b0145706fbeULL, 0x243185be4ee4b28cULL, 0x550c7dc3d5ffb4e2ULL,
+    0x72be5d74f27b896fULL, 0x80deb1fe3b1696b1ULL, 0x9bdc06a725c71235ULL, 0xc19bf174cf692694ULL,
+    0xe49b69c19ef14ad2ULL, 0xefbe4786384f25e3ULL, 0x0fc19dc68b8cd5b5ULL, 0x240ca1cc77ac9c65ULL,
+    0x2de92c6f592b0275ULL, 0x4a7484aa6ea6e483ULL, 0x5cb0a9dcbd41fbd4ULL, 0x76f988da831153b5ULL,
+    0x983e5152ee66dfabULL, 0xa831c66d2db43210ULL, 0xb00327c898fb213fULL, 0xbf597fc7beef0ee4ULL,
+    0xc6e00bf33da88fc2ULL, 0xd5a79147930aa725ULL, 0x06ca6351e003826fULL, 0x142929670a0e6e70ULL,
+    0x27b70a8546d22ffcULL, 0x2e1b21385c26c926ULL, 0x4d2c6dfc5ac42aedULL, 0x53380d139d95b3dfULL,
+    0x650a73548baf63deULL, 0x766a0abb3c77b2a8ULL, 0x81c2c92e47edaee6ULL, 0x92722c851482353bULL,
+    0xa2bfe8a14cf10364ULL, 0xa81a664bbc423001ULL, 0xc24b8b70d0f89791ULL, 0xc76c51a30654be30ULL,
+    0xd192e819d6ef5218ULL, 0xd69906245565a910ULL, 0xf40e35855771202aULL, 0x106aa07032bbd1b8ULL,
+    0x19a4c116b8d2d0c8ULL, 0x1e376c085141ab53ULL, 0x2748774cdf8eeb99ULL, 0x34b0bcb5e19b48a8ULL,
+    0x391c0cb3c5c95a63ULL, 0x4ed8aa4ae3418acbULL, 0x5b9cca4f7763e373ULL, 0x682e6ff3d6b2b8a3ULL,
+    0x748f82ee5defb2fcULL, 0x78a5636f43172f60ULL, 0x84c87814a1f0ab72ULL, 0x8cc702081a6439ecULL,
+    0x90befffa23631e28ULL, 0xa4506cebde82bde9ULL, 0xbef9a3f7b2c67915ULL, 0xc67178f2e372532bULL,
+    0xca273eceea26619cULL, 0xd186b8c721c0c207ULL, 0xeada7dd6cde0eb1eULL, 0xf57d4f7fee6ed178ULL,
+    0x06f067aa72176fbaULL, 0x0a637dc5a2c898a6ULL, 0x113f9804bef90daeULL, 0x1b710b35131c471bULL,
+    0x28db77f523047d84ULL, 0x32caab7b40c72493ULL, 0x3c9ebe0a15c9bebcULL, 0x431d67c49c100d4cULL,
+    0x4cc5d4becb3e42b6ULL, 0x597f299cfc657e2aULL, 0x5fcb6fab3ad6faecULL, 0x6c44198c4a475817ULL};
+
+static void sha512_compress(uint64_t H[8], const uint8_t blk[128]) {
+  uint64_t W[80];
+  for (int t = 0; t < 16; t++) W[t] = load_be64(blk + 8 * t);
+  for (int t = 16; t < 80; t++) {
+    uint64_t s0 = rotr64(W[t - 15], 1) ^ rotr64(W[t - 15], 8) ^ (W[t - 15] >> 7);
+    uint64_t s1 = rotr64(W[t - 2], 19) ^ rotr64(W[t - 2], 61) ^ (W[t - 2] >> 6);
+    W[t] = W[t - 16] + s0 + W[t - 7] + s1;
+  }
+  uint64_t a = H[0], b = H[1], c = H[2], d = H[3], e = H[4], f = H[5], g = H[6], h = H[7];
+  for (int t = 0; t < 80; t++) {
+    uint64_t S1 = rotr64(e, 14) ^ rotr64(e, 18) ^ rotr64(e, 41);
+    uint64_t ch = (e & f) ^ (~e & g);
+    uint64_t T1 = h + S1 + ch + K512[t] + W[t];
+    uint64_t S0 = rotr64(a, 28) ^ rotr64(a, 34) ^ rotr64(a, 39);
+    uint64_t mj = (a & b) ^ (a & c) ^ (b & c);
+    uint64_t T2 = S0 + mj;
+    h = g; g = f; f = e; e = d + T1; d = c; c = b; b = a; a = T1 + T2;
+  }
+  H[0] += a; H[1] += b; H[2] += c; H[3] += d; H[4] += e; H[5] += f; H[6] += g; H[7] += h;
+}
+
+void orc_sha512_init(orc_sha512_ctx *c) {
+  static const uint64_t IV[8] = {0x6a09e667f3bcc908ULL, 0xbb67ae8584caa73bULL,
+                                 0x3c6ef372fe94f82bULL, 0xa54ff53a5f1d36f1ULL,
+                                 0x510e527fade682d1ULL, 0x9b05688c2b3e6c1fULL,
+                                 0x1f83d9abfb41bd6bULL, 0x5be0cd19137e2179ULL};
+  memcpy(c->H, IV, sizeof IV);
+  c->buflen = 0;
+  c->total = 0;
+}
+
+void orc_sha512_update(orc_sha512_ctx *c, const uint8_t *in, size_t len) {
+  c->total += len;
+  if (c->buflen) {
+    size_t take = 128 - c->buflen;
+    if (take > len) take = len;
+    memcpy(c->buf + c->buflen, in, take);
+    c->buflen += take; in += take; len -= take;
+    if (c->buflen < 128) return;
+    sha512_compress(c->H, c->buf);
+    c->buflen = 0;
+  }
+  while (len >= 128) { sha512_compress(c->H, in); in += 128; len -= 128; }
+  memcpy(c->buf, in, len);
+  c->buflen = len;
+}
+
+void orc_sha512_final(orc_sha512_ctx *c, uint8_t out[64]) {
+  uint8_t blk[256];
+  memset(blk, 0, sizeof blk);
+  memcpy(blk, c->buf, c->buflen);
+  blk[c->buflen] = 0x80;
+  size_t tot = (c->buflen + 1 + 16 <= 128) ? 128 : 256;
+  /* 128-bit big-endian bit length */
+  store_be64(blk + tot - 8, c->total << 3);
+  store_be64(blk + tot - 16, c->total >> 61);
+  sha512_compress(c->H, blk);
+  if (tot == 256) sha512_compress(c->H, blk + 128);
+  for (int i = 0; i < 8; i++) store_be64(out + 8 * i, c->H[i]);
+}
+
+void orc_sha512(uint8_t out[64], const uint8_t *in, size_t len) {
+  orc_sha512_ctx c;
+  orc_sha512_init(&c);
+  orc_sha512_update(&c, in, len);
+  orc_sha512_final(&c, out);
+}
+
+/* ------------------------------------------------------------ Blake2b ---- */
+static const uint64_t B2B_IV[8] = {0x6a09e667f3bcc908ULL, 0xbb67ae8584caa73bULL,
+                                   0x3c6ef372fe94f82bULL, 0xa54ff53a5f1d36f1ULL,
+                                   0x510e527fade682d1ULL, 0x9b05688c2b3e6c1fULL,
+                                   0x1f83d9abfb41bd6bULL, 0x5be0cd19137e2179ULL};
+static const uint8_t B2B_SIGMA[12][16] = {
+    {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15},
+    {14, 10, 4, 8, 9, 15, 13, 6, 1, 12, 0, 2, 11, 7, 5, 3},
+    {11, 8, 12, 0, 5, 2, 15, 13, 10, 14, 3, 6, 7, 1, 9, 4},
+    {7, 9, 3, 1, 13, 12, 11, 14, 2, 6, 5, 10, 4, 0, 15, 8},
+    {9, 0, 5, 7, 2, 4, 10, 15, 14, 1, 11, 12, 6, 8, 3, 13},
+    {2, 12, 6, 10, 0, 11, 8, 3, 4, 13, 7, 5, 15, 14, 1, 9},
+    {12, 5, 1, 15, 14, 13, 4, 10, 0, 7, 6, 3, 9, 2, 8, 11},
+    {13, 11, 7, 14, 12, 1, 3, 9, 5, 0, 15, 4, 8, 6, 2, 10},
+    {6, 15, 14, 9, 11, 3, 0, 8, 12, 2, 13, 7, 1, 4, 10, 5},
+    {10, 2, 8, 4, 7, 6, 1, 5, 15, 11, 9, 14, 3, 12, 13, 0},
+    {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15},
+    {14, 10, 4, 8, 9, 15, 13, 6, 1, 12, 0, 2, 11, 7, 5, 3}};
+
+static void b2b_compress(uint64_t h[8], const uint8_t blk[128], uint64_t t, int last) {
+  uint64_t v[16], m[16];
+  for (int i = 0; i < 16; i++) m[i] = load_le64(blk + 8 * i);
+  for (int i = 0; i < 8; i++) { v[i] = h[i]; v[i + 8] = B2B_IV[i]; }
+  v[12] ^= t;        /* low word of the 128-bit counter */
+  if (last) v[14] = ~v[14];
+#define G(a, b, c, d, x, y)                      \
+  do {                                           \
+    v[a] = v[a] + v[b] + (x); v[d] = rotr64(v[d] ^ v[a], 32); \
+    v[c] = v[c] + v[d];       v[b] = rotr64(v[b] ^ v[c], 24); \
+    v[a] = v[a] + v[b] + (y); v[d] = rotr64(v[d] ^ v[a], 16); \
+    v[c] = v[c] + v[d];       v[b] = rotr64(v[b] ^ v[c], 63); \
+  } while (0)
+  for (int r = 0; r < 12; r++) {
+    const uint8_t *s = B2B_SIGMA[r];
+    G(0, 4, 8, 12, m[s[0]], m[s[1]]);
+    G(1, 5, 9, 13, m[s[2]], m[s[3]]);
+    G(2, 6, 10, 14, m[s[4]], m[s[5]]);
+    G(3, 7, 11, 15, m[s[6]], m[s[7]]);
+    G(0, 5, 10, 15, m[s[8]], m[s[9]]);
+    G(1, 6, 11, 12, m[s[10]], m[s[11]]);
+    G(2, 7, 8, 13, m[s[12]], m[s[13]]);
+    G(3, 4, 9, 14, m[s[14]], m[s[15]]);
+  }
+#undef G
+  for (int i = 0; i < 8; i++) h[i] ^= v[i] ^ v[i + 8];
+}
+
+void orc_blake2b(uint8_t *out, size_t outlen, const uint8_t *in, size_t len) {
+  uint64_t h[8];
+  for (int i = 0; i < 8; i++) h[i] = B2B_IV[i];
+  h[0] ^= 0x01010000ULL ^ (uint64_t)outlen; /* fanout=1, depth=1, keylen=0 */
+  uint8_t blk[128];
+  size_t off = 0;
+  /* every full block except the last one is compressed non-final */
+  while (len - off > 128) {
+    b2b_compress(h, in + off, (uint64_t)(off + 128), 0);
+    off += 128;
+  }
+  memset(blk, 0, sizeof blk);
+  memcpy(blk, in + off, len - off);
+  b2b_compress(h, blk, (uint64_t)len, 1);
+  uint8_t full[64];
+  for (int i = 0; i < 8; i++)
+    for (int j = 0; j < 8; j++) full[8 * i + j] = (uint8_t)(h[i] >> (8 * j));
+  memcpy(out, full, outlen);
+}
+
+void orc_blake2b_256(uint8_t out[32], const uint8_t *in, size_t len) {
+  orc_blake2b(out, 32, in, len);
+}

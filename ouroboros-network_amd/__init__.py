@@ -1,0 +1,29 @@
+"""ouroboros-network_amd -- MI355X-native batch verifier for the Ouroboros
+Praos/TPraos header-crypto hot path (Ed25519DSIGN, Sum6KES, PraosVRF draft-03).
+
+Importable as ``ouroboros_network_amd`` (repo-root symlink).  The compute path
+is the gfx950 library ``lib/libouro_verify.so`` behind the C ABI in
+``include/ouro_verify.h``; there is no CPU fallback.
+"""
+from . import _native
+from ._native import DeviceError, NativeUnavailable
+from .dsign import Ed25519DSIGN
+from .kes import Sum6KES, kes_period
+from .tpraos import HeaderBatch, first_invalid, verify_headers
+from .vrf import PraosVRF
+
+__all__ = [
+    "DeviceError",
+    "Ed25519DSIGN",
+    "HeaderBatch",
+    "NativeUnavailable",
+    "PraosVRF",
+    "Sum6KES",
+    "first_invalid",
+    "kes_period",
+    "verify_headers",
+]
+
+
+def library_path() -> str:
+    return _native.LIB_PATH

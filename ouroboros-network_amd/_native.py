@@ -1,0 +1,118 @@
+"""ctypes binding of the C-ABI product library ``lib/libouro_verify.so``.
+
+The library is the drop-in boundary (``include/ouro_verify.h``); this module is
+the Python host's view of it.  There is deliberately no fallback: if the HIP
+library is missing or cannot load, every call raises ``NativeUnavailable``.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libouro_verify.so")
+
+OURO_OK = 0
+OURO_INVALID = -1
+OURO_EDEVICE = -2
+OURO_EINVAL = -3
+OURO_ENODEV = -4
+
+HDR_OCERT_OK = 0x01
+HDR_KES_OK = 0x02
+HDR_VRF_ETA_OK = 0x04
+HDR_VRF_LEADER_OK = 0x08
+HDR_ALL_OK = 0x0F
+
+
+class NativeUnavailable(RuntimeError):
+    """The gfx950 library is not built or cannot be loaded."""
+
+
+class DeviceError(RuntimeError):
+    """A batch could not be verified (HIP/runtime failure).  Never 'valid'."""
+
+
+class TPraosBatch(ctypes.Structure):
+    """Mirror of ``ouro_tpraos_batch`` (include/ouro_verify.h)."""
+
+    _fields_ = [
+        ("n", ctypes.c_size_t),
+        ("issuer_vk", ctypes.c_void_p),
+        ("vrf_vk", ctypes.c_void_p),
+        ("eta_proof", ctypes.c_void_p),
+        ("leader_proof", ctypes.c_void_p),
+        ("eta_alpha", ctypes.c_void_p),
+        ("leader_alpha", ctypes.c_void_p),
+        ("hot_vk", ctypes.c_void_p),
+        ("ocert_counter", ctypes.c_void_p),
+        ("ocert_kes_period", ctypes.c_void_p),
+        ("ocert_sigma", ctypes.c_void_p),
+        ("kes_t", ctypes.c_void_p),
+        ("kes_sig", ctypes.c_void_p),
+        ("body", ctypes.c_void_p),
+        ("body_off", ctypes.c_void_p),
+        ("body_len", ctypes.c_void_p),
+    ]
+
+
+# every symbol include/ouro_verify.h declares, with its ctypes signature
+_P = ctypes.c_void_p
+_SZ = ctypes.c_size_t
+_I = ctypes.c_int
+_ULL = ctypes.c_ulonglong
+SIGNATURES = {
+    "ouro_set_device": (_I, [_I]),
+    "ouro_last_error": (ctypes.c_char_p, []),
+    "ouro_ed25519_verify": (_I, [_P, _P, _ULL, _P]),
+    "ouro_vrf03_verify": (_I, [_P, _P, _P, _P, _ULL]),
+    "ouro_vrf03_proof_to_hash": (_I, [_P, _P]),
+    "ouro_sum6kes_verify": (_I, [_P, ctypes.c_uint, _P, _ULL, _P]),
+    "ouro_ed25519_verify_batch": (_I, [_SZ, _P, _P, _P, _P, _P, _P]),
+    "ouro_vrf03_verify_batch": (_I, [_SZ, _P, _P, _P, _P, _P, _P, _P]),
+    "ouro_sum6kes_verify_batch": (_I, [_SZ, _P, _P, _P, _P, _P, _P, _P]),
+    "ouro_tpraos_verify_batch": (_I, [ctypes.POINTER(TPraosBatch), _P, _P, _P]),
+    "ouro_ed25519_verify_batch_device": (_I, [_P, _SZ, _P, _P, _P, _P, _P, _P]),
+    "ouro_vrf03_verify_batch_device": (_I, [_P, _SZ, _P, _P, _P, _P, _P, _P, _P]),
+    "ouro_sum6kes_verify_batch_device": (_I, [_P, _SZ, _P, _P, _P, _P, _P, _P, _P]),
+    "ouro_tpraos_verify_batch_device": (_I, [_P, ctypes.POINTER(TPraosBatch), _P, _P, _P]),
+}
+
+_lib = None
+_lock = threading.Lock()
+
+
+def load(path: str = LIB_PATH) -> ctypes.CDLL:
+    """Load (once) and type the product library; raise if unavailable."""
+    global _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(path):
+            raise NativeUnavailable(
+                f"{path} is not built; run `make -C ouroboros-network_amd` "
+                "(or __graft_entry__.build())")
+        try:
+            lib = ctypes.CDLL(path)
+        except OSError as e:  # pragma: no cover - depends on the image
+            raise NativeUnavailable(f"cannot load {path}: {e}") from e
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = lib
+        return lib
+
+
+def check(rc: int, what: str) -> int:
+    """Map a batch return code to an exception; 0 passes through."""
+    if rc == OURO_OK:
+        return rc
+    msg = load().ouro_last_error()
+    msg = msg.decode() if msg else ""
+    if rc == OURO_EINVAL:
+        raise ValueError(f"{what}: invalid arguments ({msg})")
+    if rc == OURO_ENODEV:
+        raise NativeUnavailable(f"{what}: no gfx950 device ({msg})")
+    raise DeviceError(f"{what}: device error {rc} ({msg})")

@@ -1,0 +1,116 @@
+// devhost_test.hip -- TEST-ONLY host build of the kernels' lane routines.
+//
+// hipcc compiles the __host__ __device__ bodies in verify.h for x86 too; this
+// library exports them so tests/test_devcode_host.py can check the exact
+// arithmetic the gfx950 kernels run against the oracle and libsodium in a
+// container with no GPU.  It is never linked into, or loaded by, the product
+// library (lib/libouro_verify.so) and launches nothing.
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+#include "verify.h"
+
+using namespace ouro;
+
+namespace {
+const int32_t* host_btab() {
+  static std::vector<int32_t> tab = [] {
+    std::vector<int32_t> t(kBTabWords);
+    build_btab(t.data());
+    return t;
+  }();
+  return tab.data();
+}
+struct Lane {
+  alignas(16) int32_t w[kLaneWords];
+};
+fe fe_from_bytes(const uint8_t* b) {
+  uint32_t w[8];
+  bytes_to_words8(w, b);
+  return fe_from_words(w);
+}
+void fe_to_bytes(uint8_t* out, const fe& f) {
+  uint32_t w[8];
+  fe_to_words(w, f);
+  memcpy(out, w, 32);
+}
+}  // namespace
+
+extern "C" {
+
+// field ops on canonical 32-byte encodings
+void dh_fe_mul(uint8_t* out, const uint8_t* a, const uint8_t* b) {
+  fe_to_bytes(out, fe_mul(fe_from_bytes(a), fe_from_bytes(b)));
+}
+void dh_fe_sq(uint8_t* out, const uint8_t* a) { fe_to_bytes(out, fe_sq(fe_from_bytes(a))); }
+void dh_fe_sub(uint8_t* out, const uint8_t* a, const uint8_t* b) {
+  fe_to_bytes(out, fe_sub(fe_from_bytes(a), fe_from_bytes(b)));
+}
+void dh_fe_invert(uint8_t* out, const uint8_t* a) {
+  fe_to_bytes(out, fe_invert(fe_from_bytes(a)));
+}
+// raw-limb round trip: limbs given as 10 int32, canonical encoding out
+void dh_fe_limbs_tobytes(uint8_t* out, const int32_t* limbs) {
+  fe f;
+  for (int i = 0; i < 10; i++) f.v[i] = limbs[i];
+  fe_to_bytes(out, f);
+}
+void dh_sc_reduce64(uint8_t* out, const uint8_t* in64) {
+  uint32_t w[16], r[8];
+  for (int i = 0; i < 16; i++) w[i] = ld_le32(in64 + 4 * i);
+  sc_reduce512(r, w);
+  memcpy(out, r, 32);
+}
+void dh_sha512_prefixed64(uint8_t* out, const uint8_t* prefix64, const uint8_t* msg,
+                          uint32_t mlen) {
+  uint32_t pre[16];
+  for (int i = 0; i < 16; i++) pre[i] = ld_le32(prefix64 + 4 * i);
+  uint64_t H[8];
+  sha512_prefixed<64>(H, pre, ShaGlobalTail{msg}, mlen);
+  uint32_t w[16];
+  sha512_digest_words(w, H);
+  memcpy(out, w, 64);
+}
+void dh_blake2b256_64(uint8_t* out, const uint8_t* in64) {
+  uint32_t w[16], h[8];
+  for (int i = 0; i < 16; i++) w[i] = ld_le32(in64 + 4 * i);
+  blake2b256_64(h, w);
+  memcpy(out, h, 32);
+}
+void dh_elligator2(uint8_t* out, const uint8_t* r32) {
+  uint32_t r[8];
+  bytes_to_words8(r, r32);
+  r[7] &= 0x7fffffffu;
+  ge_p3 H = elligator2_h(r);
+  uint32_t enc[8];
+  ge_encode_with_inv(enc, H.X, H.Y, fe_invert(H.Z));
+  memcpy(out, enc, 32);
+}
+int dh_ed25519_verify(const uint8_t* sig, const uint8_t* m, uint32_t mlen, const uint8_t* pk) {
+  uint32_t s[16], p[8];
+  for (int i = 0; i < 16; i++) s[i] = ld_le32(sig + 4 * i);
+  bytes_to_words8(p, pk);
+  Lane lane;
+  return ed25519_verify_lane(s, p, ShaGlobalTail{m}, mlen, lane.w, host_btab()) ? 0 : -1;
+}
+int dh_vrf03_verify(uint8_t* beta, const uint8_t* pk, const uint8_t* proof, const uint8_t* alpha,
+                    uint32_t alen) {
+  uint32_t p[8], pi[20], b[16];
+  bytes_to_words8(p, pk);
+  for (int i = 0; i < 20; i++) pi[i] = ld_le32(proof + 4 * i);
+  Lane lane;
+  bool ok = vrf03_verify_lane(b, p, pi, ShaGlobalTail{alpha}, alen, lane.w, host_btab());
+  memcpy(beta, b, 64);
+  return ok ? 0 : -1;
+}
+int dh_sum6kes_verify(const uint8_t* vk, uint32_t t, const uint8_t* m, uint32_t mlen,
+                      const uint8_t* sig) {
+  uint32_t v[8];
+  bytes_to_words8(v, vk);
+  alignas(16) uint32_t sw[112];
+  memcpy(sw, sig, 448);
+  Lane lane;
+  return sum6kes_verify_lane(v, t, sw, ShaGlobalTail{m}, mlen, lane.w, host_btab()) ? 0 : -1;
+}
+}

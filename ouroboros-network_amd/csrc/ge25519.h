@@ -1,0 +1,186 @@
+// ge25519.h -- edwards25519 group arithmetic for gfx950 (one point per lane).
+//
+// Coordinates follow the extended/"p1p1" scheme of the twisted-Edwards
+// formulas (Hisil-Wong-Carter-Dawson 2008, a = -1):
+//   p2     (X:Y:Z)           x = X/Z, y = Y/Z               -- doubling input
+//   p3     (X:Y:Z:T)         + T = XY/Z                     -- addition input
+//   p1p1   (X:Y:Z:T)         x = X/Z, y = Y/T               -- op output
+//   cached (Y+X, Y-X, Z, 2dT)                               -- per-lane tables
+//   niels  (y+x, y-x, 2dxy), Z = 1                          -- fixed B table
+// Only canonical encodings of results are ever compared, so equality with
+// libsodium's ref10 is a property of the group, not
+// of the formulas.  Decoding and the acceptance predicates below restate
+// libsodium 1.0.18 exactly.
+#pragma once
+#include "fe25519.h"
+
+namespace ouro {
+
+struct ge_p2 { fe X, Y, Z; };
+struct ge_p3 { fe X, Y, Z, T; };
+struct ge_p1p1 { fe X, Y, Z, T; };
+struct ge_cached { fe YplusX, YminusX, Z, T2d; };
+struct ge_niels { fe yplusx, yminusx, xy2d; };
+
+OURO_FI ge_p3 ge_p3_identity() { return ge_p3{fe_zero(), fe_one(), fe_one(), fe_zero()}; }
+OURO_FI ge_p2 ge_p2_identity() { return ge_p2{fe_zero(), fe_one(), fe_one()}; }
+OURO_FI ge_cached ge_cached_identity() {
+  return ge_cached{fe_one(), fe_one(), fe_one(), fe_zero()};
+}
+OURO_FI ge_niels ge_niels_identity() { return ge_niels{fe_one(), fe_one(), fe_zero()}; }
+
+OURO_FI ge_p2 ge_p1p1_to_p2(const ge_p1p1& p) {
+  return ge_p2{fe_mul(p.X, p.T), fe_mul(p.Y, p.Z), fe_mul(p.Z, p.T)};
+}
+OURO_FI ge_p3 ge_p1p1_to_p3(const ge_p1p1& p) {
+  return ge_p3{fe_mul(p.X, p.T), fe_mul(p.Y, p.Z), fe_mul(p.Z, p.T), fe_mul(p.X, p.Y)};
+}
+OURO_FI ge_p2 ge_p3_to_p2(const ge_p3& p) { return ge_p2{p.X, p.Y, p.Z}; }
+OURO_FI ge_cached ge_p3_to_cached(const ge_p3& p) {
+  return ge_cached{fe_add(p.Y, p.X), fe_sub(p.Y, p.X), p.Z, fe_mul(p.T, fe_d2())};
+}
+
+// 2P: A = X^2, B = Y^2, C = 2Z^2; x' = 2XY / (B - A), y' = (A + B) / (C - (B - A))
+OURO_FI ge_p1p1 ge_p2_dbl(const ge_p2& p) {
+  fe A = fe_sq(p.X);
+  fe B = fe_sq(p.Y);
+  fe C = fe_sq2(p.Z);
+  fe S = fe_sq(fe_add(p.X, p.Y));
+  ge_p1p1 r;
+  r.Y = fe_add(B, A);
+  r.Z = fe_sub(B, A);
+  r.X = fe_sub(S, r.Y);
+  r.T = fe_sub(C, r.Z);
+  return r;
+}
+OURO_FI ge_p1p1 ge_p3_dbl(const ge_p3& p) { return ge_p2_dbl(ge_p3_to_p2(p)); }
+
+// P + Q (neg = false) or P - Q (neg = true), Q cached.  The sign is a per-lane
+// select so a wave stays convergent whatever the digits are.
+OURO_FI ge_p1p1 ge_add_cached(const ge_p3& p, const ge_cached& q, bool neg) {
+  fe qa = fe_select(q.YminusX, q.YplusX, neg);
+  fe qb = fe_select(q.YplusX, q.YminusX, neg);
+  fe A = fe_mul(fe_add(p.Y, p.X), qa);
+  fe B = fe_mul(fe_sub(p.Y, p.X), qb);
+  fe C = fe_mul(q.T2d, p.T);
+  fe ZZ = fe_mul(p.Z, q.Z);
+  fe D = fe_add(ZZ, ZZ);
+  fe Dp = fe_add(D, C), Dm = fe_sub(D, C);
+  ge_p1p1 r;
+  r.X = fe_sub(A, B);
+  r.Y = fe_add(A, B);
+  r.Z = fe_select(Dm, Dp, neg);
+  r.T = fe_select(Dp, Dm, neg);
+  return r;
+}
+
+// P +- Q with Q affine (niels form): the fixed-base table path
+OURO_FI ge_p1p1 ge_add_niels(const ge_p3& p, const ge_niels& q, bool neg) {
+  fe qa = fe_select(q.yminusx, q.yplusx, neg);
+  fe qb = fe_select(q.yplusx, q.yminusx, neg);
+  fe A = fe_mul(fe_add(p.Y, p.X), qa);
+  fe B = fe_mul(fe_sub(p.Y, p.X), qb);
+  fe C = fe_mul(q.xy2d, p.T);
+  fe D = fe_add(p.Z, p.Z);
+  fe Dp = fe_add(D, C), Dm = fe_sub(D, C);
+  ge_p1p1 r;
+  r.X = fe_sub(A, B);
+  r.Y = fe_add(A, B);
+  r.Z = fe_select(Dm, Dp, neg);
+  r.T = fe_select(Dp, Dm, neg);
+  return r;
+}
+
+OURO_FI ge_p3 ge_p3_add(const ge_p3& p, const ge_p3& q) {
+  return ge_p1p1_to_p3(ge_add_cached(p, ge_p3_to_cached(q), false));
+}
+
+OURO_FI ge_p3 ge_p3_neg(const ge_p3& p) { return ge_p3{fe_neg(p.X), p.Y, p.Z, fe_neg(p.T)}; }
+
+// [8]P
+OURO_FI ge_p3 ge_mul8(const ge_p3& p) {
+  ge_p2 t = ge_p1p1_to_p2(ge_p3_dbl(p));
+  t = ge_p1p1_to_p2(ge_p2_dbl(t));
+  return ge_p1p1_to_p3(ge_p2_dbl(t));
+}
+
+// canonical encoding given 1/Z
+OURO_FI void ge_encode_with_inv(uint32_t out[8], const fe& X, const fe& Y, const fe& zinv) {
+  fe x = fe_mul(X, zinv);
+  fe y = fe_mul(Y, zinv);
+  uint32_t xw[8];
+  fe_to_words(out, y);
+  fe_to_words(xw, x);
+  out[7] ^= (xw[0] & 1u) << 31;
+}
+
+OURO_FI void ge_p2_encode(uint32_t out[8], const ge_p2& p) {
+  ge_encode_with_inv(out, p.X, p.Y, fe_invert(p.Z));
+}
+
+// ---- decoding & acceptance predicates (libsodium 1.0.18) -------------------
+
+// ge25519_frombytes (negate = false) / ge25519_frombytes_negate_vartime
+// (negate = true).  y is read mod 2^255; x = 0 with the sign bit set is
+// accepted.  Returns false when (y^2 - 1)/(d y^2 + 1) is not a square.
+OURO_FI bool ge_decode(ge_p3* h, const uint32_t s[8], bool negate) {
+  const fe one = fe_one();
+  fe y = fe_from_words(s);
+  fe u = fe_sq(y);
+  fe v = fe_mul(u, fe_d());
+  u = fe_sub(u, one);  // y^2 - 1
+  v = fe_add(v, one);  // d y^2 + 1
+  fe v3 = fe_mul(fe_sq(v), v);
+  fe x = fe_mul(fe_mul(fe_sq(v3), v), u);  // u v^7
+  x = fe_pow22523(x);
+  x = fe_mul(fe_mul(x, v3), u);  // u v^3 (u v^7)^((p-5)/8)
+  fe vxx = fe_mul(fe_sq(x), v);
+  bool m_root = fe_iszero(fe_sub(vxx, u));
+  bool p_root = fe_iszero(fe_add(vxx, u));
+  x = fe_select(x, fe_mul(x, fe_sqrtm1()), m_root);
+  const bool sign = (s[7] >> 31) != 0;
+  const bool flip = negate ? (fe_isnegative(x) == sign) : (fe_isnegative(x) != sign);
+  x = fe_select(fe_neg(x), x, flip);
+  h->X = x;
+  h->Y = y;
+  h->Z = one;
+  h->T = fe_mul(x, y);
+  return m_root || p_root;
+}
+
+// ge25519_is_canonical: y (bit 255 masked) < p
+OURO_FI bool ge_is_canonical(const uint32_t s[8]) {
+  bool top_all_ones = (s[7] & 0x7fffffffu) == 0x7fffffffu;
+#pragma unroll
+  for (int i = 1; i < 7; i++) top_all_ones = top_all_ones && (s[i] == 0xffffffffu);
+  return !(top_all_ones && s[0] >= 0xffffffedu);
+}
+
+// ge25519_has_small_order: y (sign bit masked) in the 7-entry blocklist
+// {0, 1, y8, -y8, p-1, p, p+1}, y8 the order-8 y coordinate.
+OURO_FI bool ge_has_small_order(const uint32_t s[8]) {
+  const uint32_t top = s[7] & 0x7fffffffu;
+  bool mid_zero = true, mid_ones = true;
+#pragma unroll
+  for (int i = 1; i < 7; i++) {
+    mid_zero = mid_zero && s[i] == 0;
+    mid_ones = mid_ones && s[i] == 0xffffffffu;
+  }
+  bool small = (mid_zero && top == 0 && (s[0] == 0 || s[0] == 1)) ||
+               (mid_ones && top == 0x7fffffffu &&
+                (s[0] == 0xffffffecu || s[0] == 0xffffffedu || s[0] == 0xffffffeeu));
+  // y8 = 0x05fc536d...b2c28f95e826 (LE words below), -y8 = p - y8
+  const uint32_t y8[8] = {0x8f95e826u, 0xb027b2c2u, 0x89f4c345u, 0xf098eff2u,
+                          0x05acdfd5u, 0x3933c6d3u, 0x880238b1u, 0x05fc536du};
+  const uint32_t ny8[8] = {0x706a17c7u, 0x4fd84d3du, 0x760b3cbau, 0x0f67100du,
+                           0xfa53202au, 0xc6cc392cu, 0x77fdc74eu, 0x7a03ac92u};
+  bool e1 = top == y8[7], e2 = top == ny8[7];
+#pragma unroll
+  for (int i = 0; i < 7; i++) {
+    e1 = e1 && s[i] == y8[i];
+    e2 = e2 && s[i] == ny8[i];
+  }
+  return small || e1 || e2;
+}
+
+}  // namespace ouro

@@ -1,0 +1,689 @@
+// kernels.hip -- gfx950 kernels and the C-ABI runtime (include/ouro_verify.h).
+//
+// One item per lane, 256-thread workgroups, grid-stride over the batch with a
+// grid capped at the resident capacity the occupancy API reports, so the
+// per-lane scratch slots (verify.h) are bounded by the grid, not the batch.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/ouro_verify.h"
+#include "verify.h"
+
+using namespace ouro;
+
+namespace {
+
+constexpr int kBlock = 256;
+
+// message bytes held in registers (the 48-byte OCertSignable); a select chain
+// keeps a dynamic byte index out of scratch
+struct RegTail48 {
+  uint32_t w[12];
+  OURO_FI uint32_t tail(uint32_t q) const {
+    uint32_t r = w[0];
+#pragma unroll
+    for (int i = 1; i < 12; i++) r = ((q >> 2) == (uint32_t)i) ? w[i] : r;
+    return (r >> (8 * (q & 3))) & 0xffu;
+  }
+};
+
+__device__ __forceinline__ void load_words(uint32_t* w, const uint8_t* p, int nwords16) {
+  const uint4* q = reinterpret_cast<const uint4*>(p);
+#pragma unroll
+  for (int i = 0; i < nwords16; i++) {
+    uint4 v = q[i];
+    w[4 * i] = v.x; w[4 * i + 1] = v.y; w[4 * i + 2] = v.z; w[4 * i + 3] = v.w;
+  }
+}
+__device__ __forceinline__ void store_words(uint8_t* p, const uint32_t* w, int nwords16) {
+  uint4* q = reinterpret_cast<uint4*>(p);
+#pragma unroll
+  for (int i = 0; i < nwords16; i++) q[i] = make_uint4(w[4 * i], w[4 * i + 1], w[4 * i + 2], w[4 * i + 3]);
+}
+
+__device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
+
+}  // namespace
+
+// ---------------------------------------------------------------- kernels ----
+
+__global__ void __launch_bounds__(kBlock) k_ed25519_verify(
+    size_t n, const uint8_t* __restrict__ pk, const uint8_t* __restrict__ sig,
+    const uint8_t* __restrict__ msg, const uint64_t* __restrict__ msg_off,
+    const uint32_t* __restrict__ msg_len, uint8_t* __restrict__ verdict, int32_t* scratch,
+    const int32_t* __restrict__ btab) {
+  const size_t tid = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const size_t nth = (size_t)gridDim.x * blockDim.x;
+  int32_t* lane = scratch + tid * kLaneWords;
+  for (size_t i = tid; i < n; i += nth) {
+    uint32_t s[16], p[8];
+    load_words(s, sig + 64 * i, 4);
+    load_words(p, pk + 32 * i, 2);
+    const bool ok = ed25519_verify_lane(s, p, ShaGlobalTail{msg + msg_off[i]}, msg_len[i], lane, btab);
+    verdict[i] = ok ? 1 : 0;
+  }
+}
+
+__global__ void __launch_bounds__(kBlock) k_vrf03_verify(
+    size_t n, const uint8_t* __restrict__ pk, const uint8_t* __restrict__ proof,
+    const uint8_t* __restrict__ alpha, const uint64_t* __restrict__ alpha_off,
+    const uint32_t* __restrict__ alpha_len, uint8_t* __restrict__ beta,
+    uint8_t* __restrict__ verdict, int32_t* scratch, const int32_t* __restrict__ btab) {
+  const size_t tid = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const size_t nth = (size_t)gridDim.x * blockDim.x;
+  int32_t* lane = scratch + tid * kLaneWords;
+  for (size_t i = tid; i < n; i += nth) {
+    uint32_t p[8], pi[20], b[16];
+    load_words(p, pk + 32 * i, 2);
+    load_words(pi, proof + 80 * i, 5);
+    const bool ok = vrf03_verify_lane(b, p, pi, ShaGlobalTail{alpha + alpha_off[i]}, alpha_len[i], lane, btab);
+    store_words(beta + 64 * i, b, 4);
+    verdict[i] = ok ? 1 : 0;
+  }
+}
+
+__global__ void __launch_bounds__(kBlock) k_sum6kes_verify(
+    size_t n, const uint8_t* __restrict__ vk, const uint32_t* __restrict__ t,
+    const uint8_t* __restrict__ msg, const uint64_t* __restrict__ msg_off,
+    const uint32_t* __restrict__ msg_len, const uint8_t* __restrict__ sig,
+    uint8_t* __restrict__ verdict, int32_t* scratch, const int32_t* __restrict__ btab) {
+  const size_t tid = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const size_t nth = (size_t)gridDim.x * blockDim.x;
+  int32_t* lane = scratch + tid * kLaneWords;
+  for (size_t i = tid; i < n; i += nth) {
+    uint32_t v[8];
+    load_words(v, vk + 32 * i, 2);
+    const uint32_t* sw = reinterpret_cast<const uint32_t*>(sig + 448 * i);
+    const bool ok = sum6kes_verify_lane(v, t[i], sw, ShaGlobalTail{msg + msg_off[i]}, msg_len[i], lane, btab);
+    verdict[i] = ok ? 1 : 0;
+  }
+}
+
+__global__ void __launch_bounds__(kBlock) k_tpraos_verify(ouro_tpraos_batch b,
+                                                          uint8_t* __restrict__ verdict,
+                                                          uint8_t* __restrict__ beta_eta,
+                                                          uint8_t* __restrict__ beta_leader,
+                                                          int32_t* scratch,
+                                                          const int32_t* __restrict__ btab) {
+  const size_t tid = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const size_t nth = (size_t)gridDim.x * blockDim.x;
+  int32_t* lane = scratch + tid * kLaneWords;
+  for (size_t i = tid; i < b.n; i += nth) {
+    uint32_t v = 0;
+    // OCERT: Ed25519 by the cold key over hotVk || BE64(n) || BE64(c0)
+    {
+      uint32_t s[16], p[8];
+      load_words(s, b.ocert_sigma + 64 * i, 4);
+      load_words(p, b.issuer_vk + 32 * i, 2);
+      RegTail48 m;
+      load_words(m.w, b.hot_vk + 32 * i, 2);
+      const uint64_t ctr = b.ocert_counter[i], c0 = b.ocert_kes_period[i];
+      m.w[8] = bswap32((uint32_t)(ctr >> 32));
+      m.w[9] = bswap32((uint32_t)ctr);
+      m.w[10] = bswap32((uint32_t)(c0 >> 32));
+      m.w[11] = bswap32((uint32_t)c0);
+      if (ed25519_verify_lane(s, p, m, 48, lane, btab)) v |= OURO_HDR_OCERT_OK;
+    }
+    // OCERT: Sum6KES by the hot key over the raw header body
+    {
+      uint32_t hv[8];
+      load_words(hv, b.hot_vk + 32 * i, 2);
+      const uint32_t* sw = reinterpret_cast<const uint32_t*>(b.kes_sig + 448 * i);
+      if (sum6kes_verify_lane(hv, b.kes_t[i], sw, ShaGlobalTail{b.body + b.body_off[i]},
+                              b.body_len[i], lane, btab))
+        v |= OURO_HDR_KES_OK;
+    }
+    // OVERLAY: the two VRF certificates under the same VRF key
+#pragma unroll 1
+    for (int which = 0; which < 2; which++) {
+      uint32_t p[8], pi[20], out[16];
+      load_words(p, b.vrf_vk + 32 * i, 2);
+      load_words(pi, (which ? b.leader_proof : b.eta_proof) + 80 * i, 5);
+      const uint8_t* a = (which ? b.leader_alpha : b.eta_alpha) + 32 * i;
+      const bool ok = vrf03_verify_lane(out, p, pi, ShaGlobalTail{a}, 32, lane, btab);
+      uint8_t* dst = which ? beta_leader : beta_eta;
+      if (dst) store_words(dst + 64 * i, out, 4);
+      if (ok) v |= which ? OURO_HDR_VRF_LEADER_OK : OURO_HDR_VRF_ETA_OK;
+    }
+    verdict[i] = (uint8_t)v;
+  }
+}
+
+// proof_to_hash only (no verification): beta = H(0x04 || 0x03 || [8]Gamma)
+__global__ void __launch_bounds__(kBlock) k_vrf03_proof_to_hash(size_t n,
+                                                                const uint8_t* __restrict__ proof,
+                                                                uint8_t* __restrict__ beta,
+                                                                uint8_t* __restrict__ verdict) {
+  const size_t tid = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const size_t nth = (size_t)gridDim.x * blockDim.x;
+  for (size_t i = tid; i < n; i += nth) {
+    uint32_t G[8];
+    load_words(G, proof + 80 * i, 2);
+    ge_p3 Gamma;
+    bool ok = ge_is_canonical(G);
+    ok = ge_decode(&Gamma, G, false) && ok;
+    ge_p3 G8 = ge_mul8(Gamma);
+    uint32_t enc[8];
+    ge_encode_with_inv(enc, G8.X, G8.Y, fe_invert(G8.Z));
+    uint32_t bp[9];
+    bp[0] = 0x04u | (0x03u << 8) | (enc[0] << 16);
+#pragma unroll
+    for (int k = 1; k < 8; k++) bp[k] = (enc[k - 1] >> 16) | (enc[k] << 16);
+    bp[8] = enc[7] >> 16;
+    uint64_t H[8];
+    sha512_prefixed<34>(H, bp, ShaNoTail{}, 0);
+    uint32_t w[16];
+    sha512_digest_words(w, H);
+#pragma unroll
+    for (int k = 0; k < 16; k++) w[k] = ok ? w[k] : 0u;
+    store_words(beta + 64 * i, w, 4);
+    verdict[i] = ok ? 1 : 0;
+  }
+}
+
+// ---------------------------------------------------------------- runtime ----
+
+namespace {
+
+thread_local std::string t_last_error;
+thread_local int t_device = -1;
+
+int fail(int code, const std::string& what) {
+  t_last_error = what;
+  return code;
+}
+
+#define OURO_HIP(call)                                                               \
+  do {                                                                               \
+    hipError_t e_ = (call);                                                          \
+    if (e_ != hipSuccess)                                                            \
+      return fail(OURO_EDEVICE, std::string(#call) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+
+struct DeviceState {
+  bool ready = false;
+  int err = OURO_OK;
+  std::string err_msg;
+  int32_t* btab = nullptr;
+  int cus = 0;
+  int max_blocks[8] = {0};  // per kernel id
+};
+
+std::mutex g_dev_mu;
+std::map<int, DeviceState> g_dev;
+
+enum KernelId { kEd = 0, kVrf = 1, kKes = 2, kHdr = 3, kP2H = 4 };
+
+const void* kernel_ptr(int id) {
+  switch (id) {
+    case kEd: return reinterpret_cast<const void*>(&k_ed25519_verify);
+    case kVrf: return reinterpret_cast<const void*>(&k_vrf03_verify);
+    case kKes: return reinterpret_cast<const void*>(&k_sum6kes_verify);
+    case kHdr: return reinterpret_cast<const void*>(&k_tpraos_verify);
+    default: return reinterpret_cast<const void*>(&k_vrf03_proof_to_hash);
+  }
+}
+
+int current_device(int* dev) {
+  if (t_device < 0) {
+    int d = 0;
+    OURO_HIP(hipGetDevice(&d));
+    t_device = d;
+  }
+  OURO_HIP(hipSetDevice(t_device));
+  *dev = t_device;
+  return OURO_OK;
+}
+
+int device_state(DeviceState** out) {
+  int dev;
+  int rc = current_device(&dev);
+  if (rc) return rc;
+  std::lock_guard<std::mutex> g(g_dev_mu);
+  DeviceState& s = g_dev[dev];
+  if (!s.ready) {
+    hipDeviceProp_t prop;
+    OURO_HIP(hipGetDeviceProperties(&prop, dev));
+    if (std::string(prop.gcnArchName).rfind("gfx950", 0) != 0)
+      return fail(OURO_ENODEV, std::string("device is ") + prop.gcnArchName + ", need gfx950");
+    s.cus = prop.multiProcessorCount;
+    std::vector<int32_t> tab(kBTabWords);
+    build_btab(tab.data());
+    OURO_HIP(hipMalloc(&s.btab, sizeof(int32_t) * kBTabWords));
+    OURO_HIP(hipMemcpy(s.btab, tab.data(), sizeof(int32_t) * kBTabWords, hipMemcpyHostToDevice));
+    for (int id = 0; id < 5; id++) {
+      int per_cu = 0;
+      OURO_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel_ptr(id), kBlock, 0));
+      s.max_blocks[id] = std::max(1, per_cu) * s.cus;
+    }
+    s.ready = true;
+  }
+  *out = &s;
+  return OURO_OK;
+}
+
+// per-thread stream + growable device buffers
+struct Buf {
+  void* p = nullptr;
+  size_t cap = 0;
+};
+struct ThreadCtx {
+  int dev = -1;
+  hipStream_t stream = nullptr;
+  std::map<hipStream_t, Buf> scratch;  // per stream: concurrent launches never share slots
+  Buf in[32];  // staging slots; the header batch uses 18
+  ~ThreadCtx() {
+    // process teardown: the runtime may already be gone; leak rather than fault
+  }
+};
+thread_local ThreadCtx t_ctx;
+
+int ensure(Buf& b, size_t bytes) {
+  if (b.cap >= bytes) return OURO_OK;
+  if (b.p) OURO_HIP(hipFree(b.p));
+  b.p = nullptr;
+  b.cap = 0;
+  size_t want = std::max<size_t>(bytes, 4096);
+  OURO_HIP(hipMalloc(&b.p, want));
+  b.cap = want;
+  return OURO_OK;
+}
+
+int thread_stream(hipStream_t* s) {
+  int dev;
+  int rc = current_device(&dev);
+  if (rc) return rc;
+  if (t_ctx.stream == nullptr || t_ctx.dev != dev) {
+    OURO_HIP(hipStreamCreateWithFlags(&t_ctx.stream, hipStreamNonBlocking));
+    t_ctx.dev = dev;
+  }
+  *s = t_ctx.stream;
+  return OURO_OK;
+}
+
+// grid for n items of kernel `id`; returns the scratch slot count
+int plan(DeviceState* ds, int id, size_t n, hipStream_t stream, int* grid, int32_t** scratch) {
+  size_t blocks = (n + kBlock - 1) / kBlock;
+  blocks = std::max<size_t>(1, std::min<size_t>(blocks, (size_t)ds->max_blocks[id]));
+  *grid = (int)blocks;
+  if (scratch) {
+    Buf& b = t_ctx.scratch[stream];
+    int rc = ensure(b, blocks * kBlock * sizeof(int32_t) * kLaneWords);
+    if (rc) return rc;
+    *scratch = static_cast<int32_t*>(b.p);
+  }
+  return OURO_OK;
+}
+
+int launch_check() {
+  OURO_HIP(hipGetLastError());
+  return OURO_OK;
+}
+
+// ---- device-pointer launches (shared by the host-buffer and device APIs) ----
+int launch_ed(hipStream_t st, size_t n, const uint8_t* pk, const uint8_t* sig, const uint8_t* msg,
+              const uint64_t* off, const uint32_t* len, uint8_t* verdict) {
+  DeviceState* ds;
+  int rc = device_state(&ds);
+  if (rc) return rc;
+  int grid;
+  int32_t* scr;
+  if ((rc = plan(ds, kEd, n, st, &grid, &scr))) return rc;
+  hipLaunchKernelGGL(k_ed25519_verify, dim3(grid), dim3(kBlock), 0, st, n, pk, sig, msg, off, len,
+                     verdict, scr, ds->btab);
+  return launch_check();
+}
+
+int launch_vrf(hipStream_t st, size_t n, const uint8_t* pk, const uint8_t* proof,
+               const uint8_t* alpha, const uint64_t* off, const uint32_t* len, uint8_t* beta,
+               uint8_t* verdict) {
+  DeviceState* ds;
+  int rc = device_state(&ds);
+  if (rc) return rc;
+  int grid;
+  int32_t* scr;
+  if ((rc = plan(ds, kVrf, n, st, &grid, &scr))) return rc;
+  hipLaunchKernelGGL(k_vrf03_verify, dim3(grid), dim3(kBlock), 0, st, n, pk, proof, alpha, off,
+                     len, beta, verdict, scr, ds->btab);
+  return launch_check();
+}
+
+int launch_kes(hipStream_t st, size_t n, const uint8_t* vk, const uint32_t* t, const uint8_t* msg,
+               const uint64_t* off, const uint32_t* len, const uint8_t* sig, uint8_t* verdict) {
+  DeviceState* ds;
+  int rc = device_state(&ds);
+  if (rc) return rc;
+  int grid;
+  int32_t* scr;
+  if ((rc = plan(ds, kKes, n, st, &grid, &scr))) return rc;
+  hipLaunchKernelGGL(k_sum6kes_verify, dim3(grid), dim3(kBlock), 0, st, n, vk, t, msg, off, len,
+                     sig, verdict, scr, ds->btab);
+  return launch_check();
+}
+
+int launch_hdr(hipStream_t st, const ouro_tpraos_batch& b, uint8_t* verdict, uint8_t* be,
+               uint8_t* bl) {
+  DeviceState* ds;
+  int rc = device_state(&ds);
+  if (rc) return rc;
+  int grid;
+  int32_t* scr;
+  if ((rc = plan(ds, kHdr, b.n, st, &grid, &scr))) return rc;
+  hipLaunchKernelGGL(k_tpraos_verify, dim3(grid), dim3(kBlock), 0, st, b, verdict, be, bl, scr,
+                     ds->btab);
+  return launch_check();
+}
+
+// ---- host-buffer staging ----
+struct Stager {
+  hipStream_t st;
+  int slot = 0;
+  int rc = OURO_OK;
+  template <class T>
+  T* up(const T* host, size_t count) {
+    if (rc) return nullptr;
+    const size_t bytes = std::max<size_t>(count * sizeof(T), 16);
+    Buf& b = t_ctx.in[slot++];
+    if ((rc = ensure(b, bytes))) return nullptr;
+    if (count) {
+      hipError_t e = hipMemcpyAsync(b.p, host, count * sizeof(T), hipMemcpyHostToDevice, st);
+      if (e != hipSuccess) rc = fail(OURO_EDEVICE, std::string("H2D: ") + hipGetErrorString(e));
+    }
+    return static_cast<T*>(b.p);
+  }
+  template <class T>
+  T* out(size_t count) {
+    if (rc) return nullptr;
+    Buf& b = t_ctx.in[slot++];
+    if ((rc = ensure(b, std::max<size_t>(count * sizeof(T), 16)))) return nullptr;
+    return static_cast<T*>(b.p);
+  }
+};
+
+// total bytes addressed by (off, len) pairs
+size_t span_of(size_t n, const uint64_t* off, const uint32_t* len) {
+  size_t hi = 0;
+  for (size_t i = 0; i < n; i++) hi = std::max<size_t>(hi, off[i] + len[i]);
+  return hi;
+}
+
+int finish(hipStream_t st) {
+  OURO_HIP(hipStreamSynchronize(st));
+  return OURO_OK;
+}
+
+int download(hipStream_t st, void* host, const void* dev, size_t bytes) {
+  if (!host || !bytes) return OURO_OK;
+  OURO_HIP(hipMemcpyAsync(host, dev, bytes, hipMemcpyDeviceToHost, st));
+  return OURO_OK;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------- C ABI ------
+extern "C" {
+
+int ouro_set_device(int device) {
+  int count = 0;
+  if (hipGetDeviceCount(&count) != hipSuccess || device < 0 || device >= count)
+    return fail(OURO_ENODEV, "no such device");
+  t_device = device;
+  return OURO_OK;
+}
+
+const char* ouro_last_error(void) { return t_last_error.c_str(); }
+
+int ouro_ed25519_verify_batch(size_t n, const uint8_t* pk, const uint8_t* sig, const uint8_t* msg,
+                              const uint64_t* msg_off, const uint32_t* msg_len, uint8_t* verdict) {
+  if (n == 0) return OURO_OK;
+  if (!pk || !sig || !msg_off || !msg_len || !verdict) return fail(OURO_EINVAL, "null argument");
+  hipStream_t st;
+  int rc = thread_stream(&st);
+  if (rc) return rc;
+  const size_t span = span_of(n, msg_off, msg_len);
+  if (span && !msg) return fail(OURO_EINVAL, "null message buffer");
+  Stager sg{st};
+  auto dpk = sg.up(pk, 32 * n);
+  auto dsig = sg.up(sig, 64 * n);
+  auto dmsg = sg.up(msg, span);
+  auto doff = sg.up(msg_off, n);
+  auto dlen = sg.up(msg_len, n);
+  auto dver = sg.out<uint8_t>(n);
+  if (sg.rc) return sg.rc;
+  if ((rc = launch_ed(st, n, dpk, dsig, dmsg, doff, dlen, dver))) return rc;
+  std::vector<uint8_t> tmp(n);
+  if ((rc = download(st, tmp.data(), dver, n))) return rc;
+  if ((rc = finish(st))) return rc;
+  memcpy(verdict, tmp.data(), n);
+  return OURO_OK;
+}
+
+int ouro_vrf03_verify_batch(size_t n, const uint8_t* pk, const uint8_t* proof, const uint8_t* alpha,
+                            const uint64_t* alpha_off, const uint32_t* alpha_len, uint8_t* beta,
+                            uint8_t* verdict) {
+  if (n == 0) return OURO_OK;
+  if (!pk || !proof || !alpha_off || !alpha_len || !verdict) return fail(OURO_EINVAL, "null argument");
+  hipStream_t st;
+  int rc = thread_stream(&st);
+  if (rc) return rc;
+  const size_t span = span_of(n, alpha_off, alpha_len);
+  if (span && !alpha) return fail(OURO_EINVAL, "null alpha buffer");
+  Stager sg{st};
+  auto dpk = sg.up(pk, 32 * n);
+  auto dpi = sg.up(proof, 80 * n);
+  auto dal = sg.up(alpha, span);
+  auto doff = sg.up(alpha_off, n);
+  auto dlen = sg.up(alpha_len, n);
+  auto dbeta = sg.out<uint8_t>(64 * n);
+  auto dver = sg.out<uint8_t>(n);
+  if (sg.rc) return sg.rc;
+  if ((rc = launch_vrf(st, n, dpk, dpi, dal, doff, dlen, dbeta, dver))) return rc;
+  std::vector<uint8_t> tv(n), tb(beta ? 64 * n : 0);
+  if ((rc = download(st, tv.data(), dver, n))) return rc;
+  if (beta && (rc = download(st, tb.data(), dbeta, 64 * n))) return rc;
+  if ((rc = finish(st))) return rc;
+  memcpy(verdict, tv.data(), n);
+  if (beta) memcpy(beta, tb.data(), 64 * n);
+  return OURO_OK;
+}
+
+int ouro_sum6kes_verify_batch(size_t n, const uint8_t* vk, const uint32_t* t, const uint8_t* msg,
+                              const uint64_t* msg_off, const uint32_t* msg_len, const uint8_t* sig,
+                              uint8_t* verdict) {
+  if (n == 0) return OURO_OK;
+  if (!vk || !t || !msg_off || !msg_len || !sig || !verdict) return fail(OURO_EINVAL, "null argument");
+  hipStream_t st;
+  int rc = thread_stream(&st);
+  if (rc) return rc;
+  const size_t span = span_of(n, msg_off, msg_len);
+  if (span && !msg) return fail(OURO_EINVAL, "null message buffer");
+  Stager sg{st};
+  auto dvk = sg.up(vk, 32 * n);
+  auto dt = sg.up(t, n);
+  auto dmsg = sg.up(msg, span);
+  auto doff = sg.up(msg_off, n);
+  auto dlen = sg.up(msg_len, n);
+  auto dsig = sg.up(sig, 448 * n);
+  auto dver = sg.out<uint8_t>(n);
+  if (sg.rc) return sg.rc;
+  if ((rc = launch_kes(st, n, dvk, dt, dmsg, doff, dlen, dsig, dver))) return rc;
+  std::vector<uint8_t> tv(n);
+  if ((rc = download(st, tv.data(), dver, n))) return rc;
+  if ((rc = finish(st))) return rc;
+  memcpy(verdict, tv.data(), n);
+  return OURO_OK;
+}
+
+int ouro_tpraos_verify_batch(const ouro_tpraos_batch* b, uint8_t* verdict, uint8_t* beta_eta,
+                             uint8_t* beta_leader) {
+  if (!b) return fail(OURO_EINVAL, "null batch");
+  const size_t n = b->n;
+  if (n == 0) return OURO_OK;
+  if (!b->issuer_vk || !b->vrf_vk || !b->eta_proof || !b->leader_proof || !b->eta_alpha ||
+      !b->leader_alpha || !b->hot_vk || !b->ocert_counter || !b->ocert_kes_period ||
+      !b->ocert_sigma || !b->kes_t || !b->kes_sig || !b->body_off || !b->body_len || !verdict)
+    return fail(OURO_EINVAL, "null argument");
+  hipStream_t st;
+  int rc = thread_stream(&st);
+  if (rc) return rc;
+  const size_t span = span_of(n, b->body_off, b->body_len);
+  if (span && !b->body) return fail(OURO_EINVAL, "null body buffer");
+  Stager sg{st};
+  ouro_tpraos_batch d;
+  d.n = n;
+  d.issuer_vk = sg.up(b->issuer_vk, 32 * n);
+  d.vrf_vk = sg.up(b->vrf_vk, 32 * n);
+  d.eta_proof = sg.up(b->eta_proof, 80 * n);
+  d.leader_proof = sg.up(b->leader_proof, 80 * n);
+  d.eta_alpha = sg.up(b->eta_alpha, 32 * n);
+  d.leader_alpha = sg.up(b->leader_alpha, 32 * n);
+  d.hot_vk = sg.up(b->hot_vk, 32 * n);
+  d.ocert_counter = sg.up(b->ocert_counter, n);
+  d.ocert_kes_period = sg.up(b->ocert_kes_period, n);
+  d.ocert_sigma = sg.up(b->ocert_sigma, 64 * n);
+  d.kes_t = sg.up(b->kes_t, n);
+  d.kes_sig = sg.up(b->kes_sig, 448 * n);
+  d.body = sg.up(b->body, span);
+  d.body_off = sg.up(b->body_off, n);
+  d.body_len = sg.up(b->body_len, n);
+  uint8_t* dver = sg.out<uint8_t>(n);
+  uint8_t* dbe = sg.out<uint8_t>(64 * n);
+  uint8_t* dbl = sg.out<uint8_t>(64 * n);
+  if (sg.rc) return sg.rc;
+  if ((rc = launch_hdr(st, d, dver, dbe, dbl))) return rc;
+  std::vector<uint8_t> tv(n), te(beta_eta ? 64 * n : 0), tl(beta_leader ? 64 * n : 0);
+  if ((rc = download(st, tv.data(), dver, n))) return rc;
+  if (beta_eta && (rc = download(st, te.data(), dbe, 64 * n))) return rc;
+  if (beta_leader && (rc = download(st, tl.data(), dbl, 64 * n))) return rc;
+  if ((rc = finish(st))) return rc;
+  memcpy(verdict, tv.data(), n);
+  if (beta_eta) memcpy(beta_eta, te.data(), 64 * n);
+  if (beta_leader) memcpy(beta_leader, tl.data(), 64 * n);
+  return OURO_OK;
+}
+
+// ---- single item: a batch of one (ABI-identical to the symbols replaced) ----
+int ouro_ed25519_verify(const unsigned char* sig, const unsigned char* m, unsigned long long mlen,
+                        const unsigned char* pk) {
+  if (!sig || !pk || (mlen && !m)) return OURO_INVALID;
+  const uint64_t off = 0;
+  const uint32_t len = (uint32_t)mlen;
+  if ((unsigned long long)len != mlen) return fail(OURO_EINVAL, "message too long");
+  uint8_t v = 0;
+  static const uint8_t empty[1] = {0};
+  int rc = ouro_ed25519_verify_batch(1, pk, sig, mlen ? m : empty, &off, &len, &v);
+  if (rc) return rc;
+  return v ? OURO_OK : OURO_INVALID;
+}
+
+int ouro_vrf03_verify(unsigned char* output, const unsigned char* pk, const unsigned char* proof,
+                      const unsigned char* msg, unsigned long long msglen) {
+  if (!pk || !proof || (msglen && !msg)) return OURO_INVALID;
+  const uint64_t off = 0;
+  const uint32_t len = (uint32_t)msglen;
+  if ((unsigned long long)len != msglen) return fail(OURO_EINVAL, "message too long");
+  uint8_t v = 0, beta[64];
+  static const uint8_t empty[1] = {0};
+  int rc = ouro_vrf03_verify_batch(1, pk, proof, msglen ? msg : empty, &off, &len, beta, &v);
+  if (rc) return rc;
+  if (!v) return OURO_INVALID;
+  if (output) memcpy(output, beta, 64);  // written only on success, like the original
+  return OURO_OK;
+}
+
+int ouro_vrf03_proof_to_hash(unsigned char* output, const unsigned char* proof) {
+  if (!output || !proof) return OURO_INVALID;
+  hipStream_t st;
+  int rc = thread_stream(&st);
+  if (rc) return rc;
+  DeviceState* ds;
+  if ((rc = device_state(&ds))) return rc;
+  Stager sg{st};
+  auto dpi = sg.up(proof, 80);
+  auto dbeta = sg.out<uint8_t>(64);
+  auto dver = sg.out<uint8_t>(1);
+  if (sg.rc) return sg.rc;
+  hipLaunchKernelGGL(k_vrf03_proof_to_hash, dim3(1), dim3(kBlock), 0, st, (size_t)1, dpi, dbeta, dver);
+  if ((rc = launch_check())) return rc;
+  uint8_t beta[64], v = 0;
+  if ((rc = download(st, beta, dbeta, 64))) return rc;
+  if ((rc = download(st, &v, dver, 1))) return rc;
+  if ((rc = finish(st))) return rc;
+  if (!v) return OURO_INVALID;
+  memcpy(output, beta, 64);
+  return OURO_OK;
+}
+
+int ouro_sum6kes_verify(const unsigned char* vk, unsigned int t, const unsigned char* m,
+                        unsigned long long mlen, const unsigned char* sig) {
+  if (!vk || !sig || (mlen && !m)) return OURO_INVALID;
+  const uint64_t off = 0;
+  const uint32_t len = (uint32_t)mlen;
+  if ((unsigned long long)len != mlen) return fail(OURO_EINVAL, "message too long");
+  uint8_t v = 0;
+  const uint32_t tt = t;
+  static const uint8_t empty[1] = {0};
+  int rc = ouro_sum6kes_verify_batch(1, vk, &tt, mlen ? m : empty, &off, &len, sig, &v);
+  if (rc) return rc;
+  return v ? OURO_OK : OURO_INVALID;
+}
+
+// ---- device-resident batches ----
+int ouro_ed25519_verify_batch_device(void* stream, size_t n, const uint8_t* pk, const uint8_t* sig,
+                                     const uint8_t* msg, const uint64_t* msg_off,
+                                     const uint32_t* msg_len, uint8_t* verdict) {
+  if (n == 0) return OURO_OK;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  if (!st) {
+    int rc = thread_stream(&st);
+    if (rc) return rc;
+  }
+  return launch_ed(st, n, pk, sig, msg, msg_off, msg_len, verdict);
+}
+
+int ouro_vrf03_verify_batch_device(void* stream, size_t n, const uint8_t* pk, const uint8_t* proof,
+                                   const uint8_t* alpha, const uint64_t* alpha_off,
+                                   const uint32_t* alpha_len, uint8_t* beta, uint8_t* verdict) {
+  if (n == 0) return OURO_OK;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  if (!st) {
+    int rc = thread_stream(&st);
+    if (rc) return rc;
+  }
+  return launch_vrf(st, n, pk, proof, alpha, alpha_off, alpha_len, beta, verdict);
+}
+
+int ouro_sum6kes_verify_batch_device(void* stream, size_t n, const uint8_t* vk, const uint32_t* t,
+                                     const uint8_t* msg, const uint64_t* msg_off,
+                                     const uint32_t* msg_len, const uint8_t* sig,
+                                     uint8_t* verdict) {
+  if (n == 0) return OURO_OK;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  if (!st) {
+    int rc = thread_stream(&st);
+    if (rc) return rc;
+  }
+  return launch_kes(st, n, vk, t, msg, msg_off, msg_len, sig, verdict);
+}
+
+int ouro_tpraos_verify_batch_device(void* stream, const ouro_tpraos_batch* b, uint8_t* verdict,
+                                    uint8_t* beta_eta, uint8_t* beta_leader) {
+  if (!b) return fail(OURO_EINVAL, "null batch");
+  if (b->n == 0) return OURO_OK;
+  if (!beta_eta || !beta_leader) return fail(OURO_EINVAL, "device API needs both beta buffers");
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  if (!st) {
+    int rc = thread_stream(&st);
+    if (rc) return rc;
+  }
+  return launch_hdr(st, *b, verdict, beta_eta, beta_leader);
+}
+
+}  // extern "C"

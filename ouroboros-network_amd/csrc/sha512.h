@@ -1,0 +1,146 @@
+// sha512.h -- per-lane SHA-512 (FIPS 180-4) for gfx950.
+//
+// The inner hash of Ed25519 (h = H(R || A || M)) and of the draft-03 VRF
+// (hash-to-curve, challenge, proof_to_hash).  Messages are assembled on the
+// fly from a byte source: a wave-uniform register prefix followed by bytes
+// fetched from global memory, so nothing is staged per lane.
+#pragma once
+#include "common.h"
+
+namespace ouro {
+
+constexpr uint64_t kSha512K[80] = {
+    0x428a2f98d728ae22ULL, 0x7137449123ef65cdULL, 0xb5c0fbcfec4d3b2fULL, 0xe9b5dba58189dbbcULL,
+    0x3956c25bf348b538ULL, 0x59f111f1b605d019ULL, 0x923f82a4af194f9bULL, 0xab1c5ed5da6d8118ULL,
+    0xd807aa98a3030242ULL, 0x12835b0145706fbeULL, 0x243185be4ee4b28cULL, 0x550c7dc3d5ffb4e2ULL,
+    0x72be5d74f27b896fULL, 0x80deb1fe3b1696b1ULL, 0x9bdc06a725c71235ULL, 0xc19bf174cf692694ULL,
+    0xe49b69c19ef14ad2ULL, 0xefbe4786384f25e3ULL, 0x0fc19dc68b8cd5b5ULL, 0x240ca1cc77ac9c65ULL,
+    0x2de92c6f592b0275ULL, 0x4a7484aa6ea6e483ULL, 0x5cb0a9dcbd41fbd4ULL, 0x76f988da831153b5ULL,
+    0x983e5152ee66dfabULL, 0xa831c66d2db43210ULL, 0xb00327c898fb213fULL, 0xbf597fc7beef0ee4ULL,
+    0xc6e00bf33da88fc2ULL, 0xd5a79147930aa725ULL, 0x06ca6351e003826fULL, 0x142929670a0e6e70ULL,
+    0x27b70a8546d22ffcULL, 0x2e1b21385c26c926ULL, 0x4d2c6dfc5ac42aedULL, 0x53380d139d95b3dfULL,
+    0x650a73548baf63deULL, 0x766a0abb3c77b2a8ULL, 0x81c2c92e47edaee6ULL, 0x92722c851482353bULL,
+    0xa2bfe8a14cf10364ULL, 0xa81a664bbc423001ULL, 0xc24b8b70d0f89791ULL, 0xc76c51a30654be30ULL,
+    0xd192e819d6ef5218ULL, 0xd69906245565a910ULL, 0xf40e35855771202aULL, 0x106aa07032bbd1b8ULL,
+    0x19a4c116b8d2d0c8ULL, 0x1e376c085141ab53ULL, 0x2748774cdf8eeb99ULL, 0x34b0bcb5e19b48a8ULL,
+    0x391c0cb3c5c95a63ULL, 0x4ed8aa4ae3418acbULL, 0x5b9cca4f7763e373ULL, 0x682e6ff3d6b2b8a3ULL,
+    0x748f82ee5defb2fcULL, 0x78a5636f43172f60ULL, 0x84c87814a1f0ab72ULL, 0x8cc702081a6439ecULL,
+    0x90befffa23631e28ULL, 0xa4506cebde82bde9ULL, 0xbef9a3f7b2c67915ULL, 0xc67178f2e372532bULL,
+    0xca273eceea26619cULL, 0xd186b8c721c0c207ULL, 0xeada7dd6cde0eb1eULL, 0xf57d4f7fee6ed178ULL,
+    0x06f067aa72176fbaULL, 0x0a637dc5a2c898a6ULL, 0x113f9804bef90daeULL, 0x1b710b35131c471bULL,
+    0x28db77f523047d84ULL, 0x32caab7b40c72493ULL, 0x3c9ebe0a15c9bebcULL, 0x431d67c49c100d4cULL,
+    0x4cc5d4becb3e42b6ULL, 0x597f299cfc657e2aULL, 0x5fcb6fab3ad6faecULL, 0x6c44198c4a475817ULL};
+
+OURO_FI uint64_t rotr64(uint64_t x, int n) { return (x >> n) | (x << (64 - n)); }
+
+OURO_FI void sha512_init(uint64_t H[8]) {
+  H[0] = 0x6a09e667f3bcc908ULL; H[1] = 0xbb67ae8584caa73bULL;
+  H[2] = 0x3c6ef372fe94f82bULL; H[3] = 0xa54ff53a5f1d36f1ULL;
+  H[4] = 0x510e527fade682d1ULL; H[5] = 0x9b05688c2b3e6c1fULL;
+  H[6] = 0x1f83d9abfb41bd6bULL; H[7] = 0x5be0cd19137e2179ULL;
+}
+
+// 80 rounds as 5 passes of 16 with the schedule kept in a 16-word ring
+OURO_FI void sha512_compress(uint64_t H[8], uint64_t W[16]) {
+  uint64_t a = H[0], b = H[1], c = H[2], d = H[3], e = H[4], f = H[5], g = H[6], h = H[7];
+#pragma unroll 1
+  for (int r0 = 0; r0 < 80; r0 += 16) {
+#pragma unroll
+    for (int i = 0; i < 16; i++) {
+      if (r0 > 0) {
+        const uint64_t w15 = W[(i + 1) & 15], w2 = W[(i + 14) & 15];
+        const uint64_t s0 = rotr64(w15, 1) ^ rotr64(w15, 8) ^ (w15 >> 7);
+        const uint64_t s1 = rotr64(w2, 19) ^ rotr64(w2, 61) ^ (w2 >> 6);
+        W[i] += s0 + W[(i + 9) & 15] + s1;
+      }
+      const uint64_t S1 = rotr64(e, 14) ^ rotr64(e, 18) ^ rotr64(e, 41);
+      const uint64_t ch = (e & f) ^ (~e & g);
+      const uint64_t T1 = h + S1 + ch + kSha512K[r0 + i] + W[i];
+      const uint64_t S0 = rotr64(a, 28) ^ rotr64(a, 34) ^ rotr64(a, 39);
+      const uint64_t mj = (a & b) ^ (a & c) ^ (b & c);
+      h = g; g = f; f = e; e = d + T1; d = c; c = b; b = a; a = T1 + S0 + mj;
+    }
+  }
+  H[0] += a; H[1] += b; H[2] += c; H[3] += d; H[4] += e; H[5] += f; H[6] += g; H[7] += h;
+}
+
+// Byte sources.  `prefix(p)` is only ever asked for a compile-time p < PL in
+// the first block; `tail(q)` reads message byte q from global memory.
+struct ShaNoTail {
+  OURO_FI uint32_t tail(uint32_t) const { return 0; }
+};
+struct ShaGlobalTail {
+  const uint8_t* msg;
+  OURO_FI uint32_t tail(uint32_t q) const { return msg[q]; }
+};
+
+// SHA-512 over prefix (PL bytes, as little-endian packed words) || tail (tl
+// bytes).  PL <= 128 - 17 is not required: the prefix may spill into block 1
+// only for all-register inputs (tail length 0), which stay fully unrolled.
+template <int PL, class Tail>
+OURO_FI void sha512_prefixed(uint64_t out[8], const uint32_t* prefix, const Tail& tail,
+                             uint32_t tl) {
+  const uint32_t total = PL + tl;
+  const uint32_t nb = (total + 17 + 127) >> 7;
+  uint64_t H[8];
+  sha512_init(H);
+  // blocks that may touch the prefix: static byte positions
+  constexpr int kStaticBlocks = (PL + 127) / 128 > 0 ? (PL + 127) / 128 : 1;
+#pragma unroll
+  for (int b = 0; b < kStaticBlocks; b++) {
+    if (b > 0 && (uint32_t)b >= nb) break;
+    uint64_t W[16];
+#pragma unroll
+    for (int w = 0; w < 16; w++) {
+      uint64_t r = 0;
+#pragma unroll
+      for (int k = 0; k < 8; k++) {
+        const uint32_t p = (uint32_t)(b * 128 + w * 8 + k);
+        uint32_t byte;
+        if (p < (uint32_t)PL) byte = byte_of(prefix, (int)p);
+        else byte = (p < total) ? tail.tail(p - PL) : (p == total ? 0x80u : 0u);
+        r = (r << 8) | byte;
+      }
+      const uint32_t widx = (uint32_t)(b * 16 + w);
+      if (widx == nb * 16 - 1) r = (uint64_t)total << 3;
+      else if (widx == nb * 16 - 2) r = 0;
+      W[w] = r;
+    }
+    sha512_compress(H, W);
+  }
+  // remaining blocks read only the tail
+#pragma unroll 1
+  for (uint32_t b = kStaticBlocks; b < nb; b++) {
+    uint64_t W[16];
+#pragma unroll
+    for (int w = 0; w < 16; w++) {
+      uint64_t r = 0;
+#pragma unroll
+      for (int k = 0; k < 8; k++) {
+        const uint32_t p = b * 128 + w * 8 + k;
+        const uint32_t byte = (p < total) ? tail.tail(p - PL) : (p == total ? 0x80u : 0u);
+        r = (r << 8) | byte;
+      }
+      const uint32_t widx = b * 16 + w;
+      if (widx == nb * 16 - 1) r = (uint64_t)total << 3;
+      else if (widx == nb * 16 - 2) r = 0;
+      W[w] = r;
+    }
+    sha512_compress(H, W);
+  }
+#pragma unroll
+  for (int i = 0; i < 8; i++) out[i] = H[i];
+}
+
+// big-endian digest word i -> little-endian packed byte words
+OURO_FI void sha512_digest_words(uint32_t out[16], const uint64_t H[8]) {
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    const uint64_t v = H[i];
+    const uint32_t hi = (uint32_t)(v >> 32), lo = (uint32_t)v;
+    out[2 * i] = __builtin_bswap32(hi);
+    out[2 * i + 1] = __builtin_bswap32(lo);
+  }
+}
+
+}  // namespace ouro

@@ -1,0 +1,452 @@
+// verify.h -- lane-level verification routines (one item per lane).
+//
+// Every routine here is the per-item body of a gfx950 kernel in kernels.hip:
+//   ed25519_verify_lane  <- libsodium 1.0.18 crypto_sign_ed25519_verify_detached
+//                           
+//   vrf03_verify_lane    <- crypto_vrf_ietfdraft03_verify + proof_to_hash
+//                           (cardano-crypto-praos; §8(a) a5/a6, App. B.3)
+//   sum6kes_verify_lane  <- cardano-crypto-class SumKES/SingleKES verifyKES
+//                           (§8(a) a3, App. B.2)
+// Control flow is wave-uniform: rejected items still run the arithmetic and
+// are masked at the end, so no lane diverges on secret-independent but
+// data-dependent checks.
+//
+// Double-scalar multiplication: signed fixed windows (width 4 for variable
+// points, width 8 for the fixed base B), one doubling chain shared by every
+// scalar, so the adds happen at the same bit positions in every lane.  Per-lane
+// tables of [1..8]P in cached form live in a per-lane global scratch slot;
+// the [1..128]B niels table is shared (global, L1/L2 resident).
+#pragma once
+#include "blake2b.h"
+#include "ge25519.h"
+#include "sc25519.h"
+#include "sha512.h"
+
+namespace ouro {
+
+// ---- per-lane scratch slot layout (int32 words) ----------------------------
+constexpr int kCachedWords = 40;                  // 4 fe
+constexpr int kTabEntries = 8;                    // [1..8]P
+constexpr int kTabWords = kTabEntries * kCachedWords;
+constexpr int kSlotTab1 = 0;
+constexpr int kSlotTab2 = kTabWords;
+constexpr int kSlotA1 = 2 * kTabWords;            // 8 words
+constexpr int kSlotA2 = kSlotA1 + 8;
+constexpr int kSlotB = kSlotA2 + 8;
+constexpr int kSlotCarry = kSlotB + 8;            // 6 words (3 x u64)
+constexpr int kSlotOut = kSlotCarry + 8;          // p2 result: 3 fe at 12-word stride
+constexpr int kLaneWords = kSlotOut + 36;         // 708 words = 2832 B (16-B multiple)
+
+constexpr int kBTabEntries = 128;                 // [1..128]B
+constexpr int kNielsWords = 32;                   // 30 used, padded for 16-B loads
+constexpr int kBTabWords = kBTabEntries * kNielsWords;
+
+// ---- vector load/store helpers ---------------------------------------------
+OURO_FI void st_fe(int32_t* p, const fe& f) {
+  int4* q = reinterpret_cast<int4*>(p);
+  // 10 words: store as 2 x int4 + int2
+  q[0] = make_int4(f.v[0], f.v[1], f.v[2], f.v[3]);
+  q[1] = make_int4(f.v[4], f.v[5], f.v[6], f.v[7]);
+  reinterpret_cast<int2*>(p + 8)[0] = make_int2(f.v[8], f.v[9]);
+}
+OURO_FI fe ld_fe(const int32_t* p) {
+  const int4* q = reinterpret_cast<const int4*>(p);
+  int4 a = q[0], b = q[1];
+  int2 c = reinterpret_cast<const int2*>(p + 8)[0];
+  fe f = OURO_FE(a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w, c.x, c.y);
+  return f;
+}
+// cached point: 40 words = 10 x int4, fe k at words [10k, 10k+10)
+OURO_FI void st_cached(int32_t* p, const ge_cached& c) {
+  int4* q = reinterpret_cast<int4*>(p);
+  const int32_t* s[4] = {c.YplusX.v, c.YminusX.v, c.Z.v, c.T2d.v};
+  int32_t w[40];
+#pragma unroll
+  for (int k = 0; k < 4; k++)
+#pragma unroll
+    for (int i = 0; i < 10; i++) w[10 * k + i] = s[k][i];
+#pragma unroll
+  for (int i = 0; i < 10; i++) q[i] = make_int4(w[4 * i], w[4 * i + 1], w[4 * i + 2], w[4 * i + 3]);
+}
+OURO_FI ge_cached ld_cached(const int32_t* p) {
+  const int4* q = reinterpret_cast<const int4*>(p);
+  int32_t w[40];
+#pragma unroll
+  for (int i = 0; i < 10; i++) {
+    int4 v = q[i];
+    w[4 * i] = v.x; w[4 * i + 1] = v.y; w[4 * i + 2] = v.z; w[4 * i + 3] = v.w;
+  }
+  ge_cached c;
+#pragma unroll
+  for (int i = 0; i < 10; i++) {
+    c.YplusX.v[i] = w[i];
+    c.YminusX.v[i] = w[10 + i];
+    c.Z.v[i] = w[20 + i];
+    c.T2d.v[i] = w[30 + i];
+  }
+  return c;
+}
+OURO_FI ge_niels ld_niels(const int32_t* p) {
+  const int4* q = reinterpret_cast<const int4*>(p);
+  int32_t w[32];
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    int4 v = q[i];
+    w[4 * i] = v.x; w[4 * i + 1] = v.y; w[4 * i + 2] = v.z; w[4 * i + 3] = v.w;
+  }
+  ge_niels n;
+#pragma unroll
+  for (int i = 0; i < 10; i++) {
+    n.yplusx.v[i] = w[i];
+    n.yminusx.v[i] = w[10 + i];
+    n.xy2d.v[i] = w[20 + i];
+  }
+  return n;
+}
+OURO_FI void st_words8(int32_t* p, const uint32_t w[8]) {
+  int4* q = reinterpret_cast<int4*>(p);
+  q[0] = make_int4((int)w[0], (int)w[1], (int)w[2], (int)w[3]);
+  q[1] = make_int4((int)w[4], (int)w[5], (int)w[6], (int)w[7]);
+}
+OURO_FI void ld_words8(uint32_t w[8], const int32_t* p) {
+  const int4* q = reinterpret_cast<const int4*>(p);
+  int4 a = q[0], b = q[1];
+  w[0] = a.x; w[1] = a.y; w[2] = a.z; w[3] = a.w;
+  w[4] = b.x; w[5] = b.y; w[6] = b.z; w[7] = b.w;
+}
+
+// [1..8]P in cached form into a per-lane table
+OURO_HD inline void build_table(int32_t* tab, const ge_p3& P) {
+  ge_cached c1 = ge_p3_to_cached(P);
+  st_cached(tab, c1);
+  ge_p3 Pk = ge_p1p1_to_p3(ge_p3_dbl(P));
+  st_cached(tab + kCachedWords, ge_p3_to_cached(Pk));
+#pragma unroll 1
+  for (int k = 2; k < kTabEntries; k++) {
+    Pk = ge_p1p1_to_p3(ge_add_cached(Pk, c1, false));
+    st_cached(tab + k * kCachedWords, ge_p3_to_cached(Pk));
+  }
+}
+
+// ---- the double-scalar multiplication ---------------------------------------
+// cfg: bits 0..6 = number of active width-4 windows of scalar a1 (table 1),
+//      bits 8..14 = same for a2 (table 2, 0 = unused), bit 16 = add [b]B.
+// Reads a1/a2/b and their recoding carries from the lane slot, writes the
+// resulting p2 point to lane[kSlotOut..].  Out of line: the header kernel calls
+// it six times per item, and the loop body is the I-cache-critical code.
+constexpr uint32_t dsm_cfg(int nw1, int nw2, bool useB) {
+  return (uint32_t)nw1 | ((uint32_t)nw2 << 8) | (useB ? (1u << 16) : 0u);
+}
+
+OURO_NI void dsm(int32_t* lane, const int32_t* btab, uint32_t cfg) {
+  const int nw1 = (int)(cfg & 0x7f), nw2 = (int)((cfg >> 8) & 0x7f);
+  const bool useB = (cfg >> 16) & 1;
+  uint32_t a1[8], a2[8], b[8];
+  ld_words8(a1, lane + kSlotA1);
+  ld_words8(a2, lane + kSlotA2);
+  ld_words8(b, lane + kSlotB);
+  const uint64_t* carr = reinterpret_cast<const uint64_t*>(lane + kSlotCarry);
+  const uint64_t c1 = carr[0], c2 = carr[1], cb = carr[2];
+  int top = nw1 > nw2 ? nw1 : nw2;
+  if (useB) top = 64;
+  // t starts as the identity in p1p1 form (X/Z = 0, Y/T = 1)
+  ge_p1p1 t{fe_zero(), fe_one(), fe_one(), fe_one()};
+#pragma unroll 1
+  for (int j = top - 1; j >= 0; j--) {
+#pragma unroll 1
+    for (int k = 0; k < 4; k++) t = ge_p2_dbl(ge_p1p1_to_p2(t));
+    // up to three additions, each from a wave-uniform source
+#pragma unroll 1
+    for (int src = 0; src < 3; src++) {
+      bool active;
+      int32_t d;
+      if (src == 0) {
+        active = j < nw1;
+        d = active ? sc_digit<4>(a1, c1, j) : 0;
+      } else if (src == 1) {
+        active = j < nw2;
+        d = active ? sc_digit<4>(a2, c2, j) : 0;
+      } else {
+        active = useB && (j & 1) == 0;
+        d = active ? sc_digit<8>(b, cb, j >> 1) : 0;
+      }
+      if (!active) continue;
+      const bool neg = d < 0;
+      const int32_t mag = neg ? -d : d;
+      const int idx = mag > 0 ? mag - 1 : 0;
+      ge_cached q;
+      if (src < 2) {
+        q = ld_cached(lane + (src == 0 ? kSlotTab1 : kSlotTab2) + idx * kCachedWords);
+      } else {
+        ge_niels nq = ld_niels(btab + idx * kNielsWords);
+        q = ge_cached{nq.yplusx, nq.yminusx, fe_one(), nq.xy2d};
+      }
+      if (mag == 0) q = ge_cached_identity();
+      t = ge_add_cached(ge_p1p1_to_p3(t), q, neg);
+    }
+  }
+  ge_p2 r = ge_p1p1_to_p2(t);
+  st_fe(lane + kSlotOut, r.X);
+  st_fe(lane + kSlotOut + 12, r.Y);
+  st_fe(lane + kSlotOut + 24, r.Z);
+}
+
+OURO_FI ge_p2 dsm_result(const int32_t* lane) {
+  return ge_p2{ld_fe(lane + kSlotOut), ld_fe(lane + kSlotOut + 12), ld_fe(lane + kSlotOut + 24)};
+}
+
+// ---- Ed25519 ------------------------------------------------------------------
+// sig = R || S (16 words), pk (8 words), message bytes from global memory.
+template <class Tail>
+OURO_HD inline bool ed25519_verify_lane(const uint32_t sig[16], const uint32_t pk[8],
+                                        const Tail& msg, uint32_t mlen, int32_t* lane,
+                                        const int32_t* btab) {
+  uint32_t R[8], S[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    R[i] = sig[i];
+    S[i] = sig[8 + i];
+  }
+  bool ok = sc_is_canonical(S) && !ge_has_small_order(R);
+  ok = ok && ge_is_canonical(pk) && !ge_has_small_order(pk);
+  ge_p3 negA;
+  ok = ge_decode(&negA, pk, true) && ok;
+  // h = SHA-512(R || A || M) mod L
+  uint32_t pre[16];
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    pre[i] = R[i];
+    pre[8 + i] = pk[i];
+  }
+  uint64_t H[8];
+  sha512_prefixed<64>(H, pre, msg, mlen);
+  uint32_t hw[16], h[8];
+  sha512_digest_words(hw, H);
+  sc_reduce512(h, hw);
+  // R' = [h](-A) + [S]B
+  build_table(lane + kSlotTab1, negA);
+  st_words8(lane + kSlotA1, h);
+  st_words8(lane + kSlotB, S);
+  uint64_t* carr = reinterpret_cast<uint64_t*>(lane + kSlotCarry);
+  carr[0] = sc_recode_carries<4, 64>(h);
+  carr[2] = sc_recode_carries<8, 32>(S);
+  dsm(lane, btab, dsm_cfg(64, 0, true));
+  uint32_t enc[8];
+  ge_p2_encode(enc, dsm_result(lane));
+  bool eq = true;
+#pragma unroll
+  for (int i = 0; i < 8; i++) eq = eq && enc[i] == R[i];
+  return ok && eq;
+}
+
+// ---- ECVRF-ED25519-SHA512-Elligator2 (draft-03) -------------------------------
+// libsodium 1.0.18 ge25519_from_uniform with x_sign = 0 (the VRF clears bit 255
+// of r before calling it): returns [8] of the Elligator2 image.
+OURO_HD inline ge_p3 elligator2_h(const uint32_t r[8]) {
+  const fe one = fe_one();
+  const fe A = fe_mont_a();
+  fe rr = fe_from_words(r);
+  fe den = fe_add(fe_sq2(rr), one);          // 1 + 2 r^2
+  fe x = fe_neg(fe_mul(A, fe_invert(den)));  // -A / (1 + 2 r^2)
+  fe x2 = fe_sq(x);
+  fe e = fe_add(fe_add(fe_mul(x, x2), x), fe_mul(x2, A));  // x^3 + A x^2 + x
+  // chi(e) = e^((p-1)/2) = (e^(2^252-3))^4 e^2
+  fe chi = fe_mul(fe_sq(fe_sq(fe_pow22523(e))), fe_sq(e));
+  uint32_t cw[8];
+  fe_to_words(cw, chi);
+  const bool e_is_minus_1 = (cw[0] >> 8) & 1;  // byte 1, bit 0 (libsodium's test)
+  x = fe_select(fe_sub(fe_neg(x), A), x, e_is_minus_1);
+  // y_ed = (x - 1) / (x + 1), decoded with sign 0, then cleared of the cofactor
+  fe yed = fe_mul(fe_sub(x, one), fe_invert(fe_add(x, one)));
+  uint32_t yw[8];
+  fe_to_words(yw, yed);
+  ge_p3 P;
+  ge_decode(&P, yw, false);  // always a square here (libsodium aborts otherwise)
+  return ge_mul8(P);
+}
+
+// Montgomery batch inversion of 4 elements
+OURO_FI void fe_invert4(fe out[4], const fe z[4]) {
+  fe a1 = fe_mul(z[0], z[1]);
+  fe a2 = fe_mul(a1, z[2]);
+  fe a3 = fe_mul(a2, z[3]);
+  fe inv = fe_invert(a3);
+  out[3] = fe_mul(inv, a2);
+  inv = fe_mul(inv, z[3]);
+  out[2] = fe_mul(inv, a1);
+  inv = fe_mul(inv, z[2]);
+  out[1] = fe_mul(inv, z[0]);
+  out[0] = fe_mul(inv, z[1]);
+}
+
+// pi = Gamma (8 words) || c (4 words) || s (8 words); alpha from global memory.
+// On success writes beta (16 words, the 64-byte output) and returns true; on
+// failure beta is zeroed.
+template <class Tail>
+OURO_HD inline bool vrf03_verify_lane(uint32_t beta[16], const uint32_t pk[8],
+                                      const uint32_t pi[20], const Tail& alpha, uint32_t alen,
+                                      int32_t* lane, const int32_t* btab) {
+  uint32_t G[8], c[8], s_raw[8], s[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    G[i] = pi[i];
+    s_raw[i] = pi[12 + i];
+    c[i] = i < 4 ? pi[8 + i] : 0u;
+  }
+  // validate_key + decode_proof
+  ge_p3 Y, Gamma;
+  bool ok = !ge_has_small_order(pk) && ge_is_canonical(pk);
+  ok = ge_decode(&Y, pk, false) && ok;
+  ok = ge_is_canonical(G) && ok;
+  ok = ge_decode(&Gamma, G, false) && ok;
+  sc_reduce256(s, s_raw);
+  // H = hash_to_curve(Y, alpha): r = SHA-512(0x04 || 0x01 || Y || alpha)[0:32]
+  uint32_t pre[9];
+  pre[0] = 0x04u | (0x01u << 8) | (pk[0] << 16);
+#pragma unroll
+  for (int i = 1; i < 8; i++) pre[i] = (pk[i - 1] >> 16) | (pk[i] << 16);
+  pre[8] = pk[7] >> 16;
+  uint64_t Hs[8];
+  sha512_prefixed<34>(Hs, pre, alpha, alen);
+  uint32_t rw[16];
+  sha512_digest_words(rw, Hs);
+  rw[7] &= 0x7fffffffu;
+  ge_p3 Hp = elligator2_h(rw);
+  // U = [s]B - [c]Y
+  build_table(lane + kSlotTab1, ge_p3_neg(Y));
+  st_words8(lane + kSlotA1, c);
+  st_words8(lane + kSlotB, s);
+  uint64_t* carr = reinterpret_cast<uint64_t*>(lane + kSlotCarry);
+  carr[0] = sc_recode_carries<4, 33>(c);
+  carr[2] = sc_recode_carries<8, 32>(s);
+  dsm(lane, btab, dsm_cfg(33, 0, true));
+  ge_p2 U = dsm_result(lane);
+  // V = [s]H - [c]Gamma
+  build_table(lane + kSlotTab1, Hp);
+  build_table(lane + kSlotTab2, ge_p3_neg(Gamma));
+  st_words8(lane + kSlotA1, s);
+  st_words8(lane + kSlotA2, c);
+  carr[0] = sc_recode_carries<4, 64>(s);
+  carr[1] = sc_recode_carries<4, 33>(c);
+  dsm(lane, btab, dsm_cfg(64, 33, false));
+  ge_p2 V = dsm_result(lane);
+  ge_p3 G8 = ge_mul8(Gamma);
+  // one inversion for the four encodings
+  fe z[4] = {Hp.Z, U.Z, V.Z, G8.Z}, zi[4];
+  fe_invert4(zi, z);
+  uint32_t Henc[8], Uenc[8], Venc[8], G8enc[8], Genc[8];
+  ge_encode_with_inv(Henc, Hp.X, Hp.Y, zi[0]);
+  ge_encode_with_inv(Uenc, U.X, U.Y, zi[1]);
+  ge_encode_with_inv(Venc, V.X, V.Y, zi[2]);
+  ge_encode_with_inv(G8enc, G8.X, G8.Y, zi[3]);
+  // Gamma re-encoded: the input bytes, except x = 0 encodes with sign 0
+#pragma unroll
+  for (int i = 0; i < 8; i++) Genc[i] = G[i];
+  if (fe_iszero(Gamma.X)) Genc[7] &= 0x7fffffffu;
+  // c' = SHA-512(0x04 || 0x02 || H || Gamma || U || V)[0:16]
+  uint32_t hp[33];
+  hp[0] = 0x04u | (0x02u << 8) | (Henc[0] << 16);
+#pragma unroll
+  for (int i = 1; i < 8; i++) hp[i] = (Henc[i - 1] >> 16) | (Henc[i] << 16);
+  hp[8] = (Henc[7] >> 16) | (Genc[0] << 16);
+#pragma unroll
+  for (int i = 1; i < 8; i++) hp[8 + i] = (Genc[i - 1] >> 16) | (Genc[i] << 16);
+  hp[16] = (Genc[7] >> 16) | (Uenc[0] << 16);
+#pragma unroll
+  for (int i = 1; i < 8; i++) hp[16 + i] = (Uenc[i - 1] >> 16) | (Uenc[i] << 16);
+  hp[24] = (Uenc[7] >> 16) | (Venc[0] << 16);
+#pragma unroll
+  for (int i = 1; i < 8; i++) hp[24 + i] = (Venc[i - 1] >> 16) | (Venc[i] << 16);
+  hp[32] = Venc[7] >> 16;
+  uint64_t Hc[8];
+  sha512_prefixed<130>(Hc, hp, ShaNoTail{}, 0);
+  uint32_t cw[16];
+  sha512_digest_words(cw, Hc);
+  bool ceq = true;
+#pragma unroll
+  for (int i = 0; i < 4; i++) ceq = ceq && cw[i] == c[i];
+  ok = ok && ceq;
+  // beta = SHA-512(0x04 || 0x03 || encode([8]Gamma))
+  uint32_t bp[9];
+  bp[0] = 0x04u | (0x03u << 8) | (G8enc[0] << 16);
+#pragma unroll
+  for (int i = 1; i < 8; i++) bp[i] = (G8enc[i - 1] >> 16) | (G8enc[i] << 16);
+  bp[8] = G8enc[7] >> 16;
+  uint64_t Hb[8];
+  sha512_prefixed<34>(Hb, bp, ShaNoTail{}, 0);
+  uint32_t bw[16];
+  sha512_digest_words(bw, Hb);
+#pragma unroll
+  for (int i = 0; i < 16; i++) beta[i] = ok ? bw[i] : 0u;
+  return ok;
+}
+
+// ---- Sum6KES --------------------------------------------------------------------
+// sig (448 B) is read from global memory: leaf signature, then (vk0, vk1) for
+// levels 1..6 bottom-up; verification walks top-down from the root vk.
+template <class Tail>
+OURO_HD inline bool sum6kes_verify_lane(const uint32_t vk[8], uint32_t t, const uint32_t* sigw,
+                                        const Tail& msg, uint32_t mlen, int32_t* lane,
+                                        const int32_t* btab) {
+  uint32_t cur[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) cur[i] = vk[i];
+  bool ok = true;
+#pragma unroll 1
+  for (int k = 6; k >= 1; k--) {
+    const uint32_t* pair = sigw + 16 + 16 * (k - 1);
+    uint32_t pw[16], h[8];
+    const uint4* p4 = reinterpret_cast<const uint4*>(pair);
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      uint4 v = p4[i];
+      pw[4 * i] = v.x; pw[4 * i + 1] = v.y; pw[4 * i + 2] = v.z; pw[4 * i + 3] = v.w;
+    }
+    blake2b256_64(h, pw);
+#pragma unroll
+    for (int i = 0; i < 8; i++) ok = ok && h[i] == cur[i];
+    const uint32_t half = 1u << (k - 1);
+    const bool right = t >= half;
+    t = right ? t - half : t;
+#pragma unroll
+    for (int i = 0; i < 8; i++) cur[i] = right ? pw[8 + i] : pw[i];
+  }
+  uint32_t sig[16];
+  const uint4* s4 = reinterpret_cast<const uint4*>(sigw);
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    uint4 v = s4[i];
+    sig[4 * i] = v.x; sig[4 * i + 1] = v.y; sig[4 * i + 2] = v.z; sig[4 * i + 3] = v.w;
+  }
+  const bool leaf = ed25519_verify_lane(sig, cur, msg, mlen, lane, btab);
+  return ok && leaf;
+}
+
+// ---- fixed-base table (host side, computed once per process) -----------------
+// [k]B for k = 1..128 as (y + x, y - x, 2 d x y), affine, reduced limbs.
+OURO_HD inline void build_btab(int32_t* out) {
+  // B = (x, 4/5) with x even: encoding 0x5866...66 (little-endian)
+  uint32_t by[8];
+  for (int i = 0; i < 8; i++) by[i] = 0x66666666u;
+  by[0] = 0x66666658u;
+  ge_p3 B;
+  ge_decode(&B, by, false);
+  ge_p3 P = B;
+  for (int k = 0; k < kBTabEntries; k++) {
+    if (k > 0) P = ge_p3_add(P, B);
+    fe zi = fe_invert(P.Z);
+    fe x = fe_mul(P.X, zi), y = fe_mul(P.Y, zi);
+    fe yp = fe_carry(fe_add(y, x)), ym = fe_carry(fe_sub(y, x));
+    fe xy2d = fe_mul(fe_mul(x, y), fe_d2());
+    int32_t* e = out + k * kNielsWords;
+    for (int i = 0; i < 10; i++) {
+      e[i] = yp.v[i];
+      e[10 + i] = ym.v[i];
+      e[20 + i] = xy2d.v[i];
+    }
+    e[30] = 0;
+    e[31] = 0;
+  }
+}
+
+}  // namespace ouro

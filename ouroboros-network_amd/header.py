@@ -1,0 +1,218 @@
+"""Shelley-family header wire format -> SoA batch.
+
+Wire shape (ouroboros-network/test/messages.cddl:27-34; decoder with the raw
+bytes kept via Annotator at
+ouroboros-consensus-shelley/src/Ouroboros/Consensus/Shelley/Ledger/Block.hs:216-217;
+N2N wrapping at .../Shelley/Node/Serialisation.hs:88-90):
+
+    header      = #6.24(bytes .cbor [header_body, kes_sig])          (N2N v1)
+    hfc_header  = [era, #6.24(bytes .cbor [header_body, kes_sig])]   (Cardano N2N v2+)
+    header_body = [blockNo, slot, prevHash, issuerVk, vrfVk, etaCert,
+                   leaderCert, bodySize, bodyHash, hotVk, counter,
+                   kesPeriod, sigma, protMajor, protMinor]
+    cert        = [output(64 B), proof(80 B)]
+
+The KES message is the *raw* header_body bytes, so the slicer records byte
+spans instead of re-encoding anything.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import List, Sequence, Tuple
+
+import numpy as np
+
+from .tpraos import HeaderBatch
+
+
+class CBORError(ValueError):
+    pass
+
+
+def _head(buf: bytes, i: int) -> Tuple[int, int, int]:
+    """(major type, argument, index after the head) of the item at i."""
+    if i >= len(buf):
+        raise CBORError("truncated")
+    ib = buf[i]
+    mt, ai = ib >> 5, ib & 31
+    i += 1
+    if ai < 24:
+        return mt, ai, i
+    if ai in (24, 25, 26, 27):
+        n = 1 << (ai - 24)
+        if i + n > len(buf):
+            raise CBORError("truncated")
+        return mt, int.from_bytes(buf[i:i + n], "big"), i + n
+    if ai == 31:
+        return mt, -1, i  # indefinite length
+    raise CBORError(f"reserved additional info {ai}")
+
+
+def skip(buf: bytes, i: int) -> int:
+    """Index just past the CBOR data item starting at i."""
+    mt, arg, j = _head(buf, i)
+    if mt in (0, 1, 7):
+        return j
+    if mt in (2, 3):
+        if arg < 0:
+            while buf[j] != 0xFF:
+                j = skip(buf, j)
+            return j + 1
+        return j + arg
+    if mt in (4, 5):
+        count = arg * (2 if mt == 5 else 1)
+        if arg < 0:
+            while buf[j] != 0xFF:
+                j = skip(buf, j)
+            return j + 1
+        for _ in range(count):
+            j = skip(buf, j)
+        return j
+    if mt == 6:
+        return skip(buf, j)
+    raise CBORError("bad major type")
+
+
+def array_items(buf: bytes, i: int) -> List[Tuple[int, int]]:
+    """Spans [(start, end)] of the elements of the definite array at i."""
+    mt, arg, j = _head(buf, i)
+    if mt != 4 or arg < 0:
+        raise CBORError(f"expected definite array at {i}")
+    out = []
+    for _ in range(arg):
+        k = skip(buf, j)
+        out.append((j, k))
+        j = k
+    return out
+
+
+def uint_at(buf: bytes, i: int) -> int:
+    mt, arg, _ = _head(buf, i)
+    if mt != 0:
+        raise CBORError(f"expected uint at {i}")
+    return arg
+
+
+def bytes_at(buf: bytes, i: int) -> bytes:
+    mt, arg, j = _head(buf, i)
+    if mt != 2 or arg < 0:
+        raise CBORError(f"expected definite bytes at {i}")
+    return bytes(buf[j:j + arg])
+
+
+@dataclass
+class ShelleyHeader:
+    era: int                 # HFC era tag (1 Shelley, 2 Allegra, 3 Mary), 1 if unwrapped
+    block_no: int
+    slot: int
+    issuer_vk: bytes
+    vrf_vk: bytes
+    eta_output: bytes
+    eta_proof: bytes
+    leader_output: bytes
+    leader_proof: bytes
+    hot_vk: bytes
+    ocert_counter: int
+    ocert_kes_period: int
+    ocert_sigma: bytes
+    body: bytes              # raw header_body CBOR = the KES message
+    kes_sig: bytes
+    body_span: Tuple[int, int]  # offsets of `body` inside the input bytes
+
+
+def parse_header(raw: bytes) -> ShelleyHeader:
+    """Parse an N2N (v1: tag-24 wrapped) or Cardano HFC-wrapped Shelley-era header."""
+    buf = bytes(raw)
+    era, i = 1, 0
+    mt, arg, j = _head(buf, 0)
+    if mt == 4 and arg == 2:  # [era, wrapped]
+        era = uint_at(buf, j)
+        if era == 0:
+            raise CBORError("Byron header: not a TPraos header")
+        i = skip(buf, j)
+    mt, arg, j = _head(buf, i)
+    if mt != 6 or arg != 24:
+        raise CBORError("expected #6.24 wrapped header")
+    mt, arg, k = _head(buf, j)
+    if mt != 2:
+        raise CBORError("expected CBOR-in-bytes")
+    inner_start = k
+    top = array_items(buf, inner_start)
+    if len(top) != 2:
+        raise CBORError("header must be [body, sig]")
+    (b0, b1), (s0, _s1) = top
+    f = array_items(buf, b0)
+    if len(f) != 15:
+        raise CBORError(f"header body must have 15 fields, got {len(f)}")
+    eta = array_items(buf, f[5][0])
+    lead = array_items(buf, f[6][0])
+    return ShelleyHeader(
+        era=era,
+        block_no=uint_at(buf, f[0][0]),
+        slot=uint_at(buf, f[1][0]),
+        issuer_vk=bytes_at(buf, f[3][0]),
+        vrf_vk=bytes_at(buf, f[4][0]),
+        eta_output=bytes_at(buf, eta[0][0]),
+        eta_proof=bytes_at(buf, eta[1][0]),
+        leader_output=bytes_at(buf, lead[0][0]),
+        leader_proof=bytes_at(buf, lead[1][0]),
+        hot_vk=bytes_at(buf, f[9][0]),
+        ocert_counter=uint_at(buf, f[10][0]),
+        ocert_kes_period=uint_at(buf, f[11][0]),
+        ocert_sigma=bytes_at(buf, f[12][0]),
+        body=buf[b0:b1],
+        kes_sig=bytes_at(buf, s0),
+        body_span=(b0, b1),
+    )
+
+
+def kes_t(slot: int, slots_per_kes_period: int, c0: int) -> int:
+    """Integrity.hs:38-44: kesPeriod(slot) - c0, clamped at 0."""
+    cur = slot // slots_per_kes_period
+    return cur - c0 if cur >= c0 else 0
+
+
+def pack(headers: Sequence[ShelleyHeader], eta_alpha: Sequence[bytes],
+         leader_alpha: Sequence[bytes], slots_per_kes_period: int) -> HeaderBatch:
+    """SoA batch from parsed headers and the caller's VRF inputs (mkSeed values)."""
+    n = len(headers)
+    if len(eta_alpha) != n or len(leader_alpha) != n:
+        raise ValueError("one eta/leader alpha per header")
+
+    def rows(get, w):
+        return np.frombuffer(b"".join(get(h) for h in headers), np.uint8).reshape(n, w) if n \
+            else np.zeros((0, w), np.uint8)
+
+    lens = np.array([len(h.body) for h in headers], np.uint32)
+    offs = np.zeros(n, np.uint64)
+    if n > 1:
+        offs[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
+    return HeaderBatch(
+        issuer_vk=rows(lambda h: h.issuer_vk, 32),
+        vrf_vk=rows(lambda h: h.vrf_vk, 32),
+        eta_proof=rows(lambda h: h.eta_proof, 80),
+        leader_proof=rows(lambda h: h.leader_proof, 80),
+        eta_alpha=np.frombuffer(b"".join(eta_alpha), np.uint8).reshape(n, 32),
+        leader_alpha=np.frombuffer(b"".join(leader_alpha), np.uint8).reshape(n, 32),
+        hot_vk=rows(lambda h: h.hot_vk, 32),
+        ocert_counter=np.array([h.ocert_counter for h in headers], np.uint64),
+        ocert_kes_period=np.array([h.ocert_kes_period for h in headers], np.uint64),
+        ocert_sigma=rows(lambda h: h.ocert_sigma, 64),
+        kes_t=np.array([kes_t(h.slot, slots_per_kes_period, h.ocert_kes_period)
+                        for h in headers], np.uint32),
+        kes_sig=rows(lambda h: h.kes_sig, 448),
+        body=np.frombuffer(b"".join(h.body for h in headers) or b"\0", np.uint8),
+        body_off=offs,
+        body_len=lens,
+    )
+
+
+def mk_seed(universal_nonce: bytes, slot: int, epoch_nonce: bytes, blake2b_256) -> bytes:
+    """ledger-specs mkSeed (as recalled; PARITY UNPINNED in this container,
+    SURVEY.md §8(f) row 2): Blake2b_256(BE64(slot) || eta0) XOR ucNonce, where
+    seedEta/seedL = Blake2b_256(BE64(0/1)).  `blake2b_256` is injected so the
+    host picks its own hash implementation."""
+    h = blake2b_256(slot.to_bytes(8, "big") + (epoch_nonce or b""))
+    if universal_nonce is None:
+        return h
+    return bytes(a ^ b for a, b in zip(h, universal_nonce))

@@ -1,0 +1,62 @@
+"""Sum6KES (SumKES^6 over SingleKES Ed25519DSIGN, Blake2b_256) on gfx950 --
+mirror of cardano-crypto-class ``Cardano.Crypto.KES.Sum`` (verify side).
+
+Reference surface: ``verifyKES :: ContextKES v -> VerKeyKES v -> Period -> a ->
+SigKES v -> Either String ()`` / ``verifySignedKES``, called at
+ouroboros-consensus-shelley/src/Ouroboros/Consensus/Shelley/Ledger/Integrity.hs:27
+with t computed at Integrity.hs:38-44 (``kes_period`` below).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from . import _native
+from ._pack import as_rows, ints, msgs_arg, ptr
+
+SIZE_VERKEY = 32
+SIZE_SIG = 448
+TOTAL_PERIODS = 64
+
+
+def kes_period(slot: int, slots_per_kes_period: int, start_of_kes_period: int) -> int:
+    """t of verifyHeaderIntegrity (Integrity.hs:38-44): clamped at 0."""
+    current = slot // slots_per_kes_period
+    return current - start_of_kes_period if current >= start_of_kes_period else 0
+
+
+class Sum6KES:
+    @staticmethod
+    def verify_kes(ctx, vk: bytes, period: int, msg: bytes, sig: bytes):
+        """``verifyKES () vk t msg sig``: None (Right ()) or an error string."""
+        if len(vk) != SIZE_VERKEY or len(sig) != SIZE_SIG:
+            return "Reject"
+        rc = _native.load().ouro_sum6kes_verify(vk, int(period) & 0xFFFFFFFF, msg, len(msg), sig)
+        if rc == _native.OURO_OK:
+            return None
+        if rc == _native.OURO_INVALID:
+            return "Reject"
+        _native.check(rc, "ouro_sum6kes_verify")
+        return "Reject"
+
+    verify_signed_kes = verify_kes
+
+    @staticmethod
+    def verify_batch(vks, periods, msgs, sigs) -> np.ndarray:
+        vk = as_rows(vks, SIZE_VERKEY, "vk")
+        sg = as_rows(sigs, SIZE_SIG, "sig")
+        t = ints(periods, np.uint32)
+        buf, off, ln = msgs_arg(msgs)
+        n = vk.shape[0]
+        if sg.shape[0] != n or t.shape[0] != n or off.shape[0] != n:
+            raise ValueError("vk, t, msg and sig batches differ in length")
+        out = np.zeros(n, dtype=np.uint8)
+        if n:
+            rc = _native.load().ouro_sum6kes_verify_batch(
+                n, ptr(vk), ptr(t), ptr(buf), ptr(off), ptr(ln), ptr(sg), ptr(out))
+            _native.check(rc, "ouro_sum6kes_verify_batch")
+        return out.astype(bool)
+
+
+verify_kes = Sum6KES.verify_kes
+verify_signed_kes = Sum6KES.verify_signed_kes
+verify_batch = Sum6KES.verify_batch

@@ -1,0 +1,199 @@
+"""ctypes access to the CPU oracle (oracle/build/liboracle.so) for the tests.
+
+The oracle is test infrastructure: it is the checker here, never the thing
+under test.  It is built by ``make -C oracle`` (or __graft_entry__.build()).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ORACLE_SO = os.path.join(ROOT, "oracle", "build", "liboracle.so")
+SODIUM_SO = "/opt/conda/lib/libsodium.so.23"
+
+_lib = None
+
+
+def lib() -> ctypes.CDLL:
+    global _lib
+    if _lib is None:
+        if not os.path.exists(ORACLE_SO):
+            subprocess.run(["make", "-C", os.path.join(ROOT, "oracle")], check=True,
+                           stdout=subprocess.DEVNULL)
+        _lib = ctypes.CDLL(ORACLE_SO)
+        P, SZ, I = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int
+        sig = {
+            "orc_sha512": (None, [P, P, SZ]),
+            "orc_blake2b_256": (None, [P, P, SZ]),
+            "orc_ed25519_seed_keypair": (None, [P, P, P]),
+            "orc_ed25519_sign": (None, [P, P, SZ, P]),
+            "orc_ed25519_verify": (I, [P, P, SZ, P]),
+            "orc_ed25519_verify_byron": (I, [P, P, SZ, P]),
+            "orc_elligator2_from_uniform": (None, [P, P]),
+            "orc_vrf03_verify": (I, [P, P, P, P, SZ]),
+            "orc_vrf03_proof_to_hash": (I, [P, P]),
+            "orc_vrf03_keypair": (None, [P, P, P]),
+            "orc_vrf03_prove": (I, [P, P, P, SZ]),
+            "orc_sum6kes_verify": (I, [P, ctypes.c_uint32, P, SZ, P]),
+            "orc_sum6kes_keygen": (None, [P, P]),
+            "orc_sum6kes_sign": (None, [P, P, ctypes.c_uint32, P, SZ]),
+            "orc_ed25519_verify_batch": (None, [SZ, P, P, P, P, P, P, I]),
+            "orc_vrf03_verify_batch": (None, [SZ, P, P, P, SZ, P, P, I]),
+            "orc_sum6kes_verify_batch": (None, [SZ, P, P, P, P, P, P, P, I]),
+            "orc_tpraos_verify_batch": (None, [P, P, P, P, I]),
+            "orc_synth_ed25519": (None, [SZ, ctypes.c_uint64, P, P, P, I]),
+            "orc_synth_vrf": (None, [SZ, ctypes.c_uint64, P, P, P, I]),
+        }
+        for name, (res, args) in sig.items():
+            fn = getattr(_lib, name)
+            fn.restype = res
+            fn.argtypes = args
+    return _lib
+
+
+def _b(n):
+    return ctypes.create_string_buffer(n)
+
+
+def sha512(m: bytes) -> bytes:
+    out = _b(64)
+    lib().orc_sha512(out, m, len(m))
+    return out.raw
+
+
+def blake2b_256(m: bytes) -> bytes:
+    out = _b(32)
+    lib().orc_blake2b_256(out, m, len(m))
+    return out.raw
+
+
+def ed25519_keypair(seed: bytes):
+    pk, sk = _b(32), _b(64)
+    lib().orc_ed25519_seed_keypair(pk, sk, seed)
+    return pk.raw, sk.raw
+
+
+def ed25519_sign(sk: bytes, m: bytes) -> bytes:
+    sig = _b(64)
+    lib().orc_ed25519_sign(sig, m, len(m), sk)
+    return sig.raw
+
+
+def ed25519_verify(sig: bytes, m: bytes, pk: bytes) -> bool:
+    return lib().orc_ed25519_verify(sig, m, len(m), pk) == 0
+
+
+def ed25519_verify_byron(sig: bytes, m: bytes, pk: bytes) -> bool:
+    return lib().orc_ed25519_verify_byron(sig, m, len(m), pk) == 0
+
+
+def elligator2(r: bytes) -> bytes:
+    out = _b(32)
+    lib().orc_elligator2_from_uniform(out, r)
+    return out.raw
+
+
+def vrf_keypair(seed: bytes):
+    pk, sk = _b(32), _b(64)
+    lib().orc_vrf03_keypair(pk, sk, seed)
+    return pk.raw, sk.raw
+
+
+def vrf_prove(sk: bytes, alpha: bytes) -> bytes:
+    pi = _b(80)
+    assert lib().orc_vrf03_prove(pi, sk, alpha, len(alpha)) == 0
+    return pi.raw
+
+
+def vrf_verify(pk: bytes, proof: bytes, alpha: bytes):
+    out = _b(64)
+    rc = lib().orc_vrf03_verify(out, pk, proof, alpha, len(alpha))
+    return out.raw if rc == 0 else None
+
+
+def vrf_proof_to_hash(proof: bytes):
+    out = _b(64)
+    return out.raw if lib().orc_vrf03_proof_to_hash(out, proof) == 0 else None
+
+
+def kes_keygen(seed: bytes) -> bytes:
+    vk = _b(32)
+    lib().orc_sum6kes_keygen(vk, seed)
+    return vk.raw
+
+
+def kes_sign(seed: bytes, t: int, m: bytes) -> bytes:
+    sig = _b(448)
+    lib().orc_sum6kes_sign(sig, seed, t, m, len(m))
+    return sig.raw
+
+
+def kes_verify(vk: bytes, t: int, m: bytes, sig: bytes) -> bool:
+    return lib().orc_sum6kes_verify(vk, t, m, len(m), sig) == 0
+
+
+def p(a: np.ndarray) -> int:
+    return a.ctypes.data
+
+
+def synth_ed25519(n: int, first: int = 0, threads: int = 8):
+    pk = np.zeros((n, 32), np.uint8)
+    sig = np.zeros((n, 64), np.uint8)
+    msg = np.zeros((n, 32), np.uint8)
+    lib().orc_synth_ed25519(n, first, p(pk), p(sig), p(msg), threads)
+    return pk, sig, msg
+
+
+def synth_vrf(n: int, first: int = 0, threads: int = 8):
+    pk = np.zeros((n, 32), np.uint8)
+    proof = np.zeros((n, 80), np.uint8)
+    alpha = np.zeros((n, 32), np.uint8)
+    lib().orc_synth_vrf(n, first, p(pk), p(proof), p(alpha), threads)
+    return pk, proof, alpha
+
+
+def ed25519_verify_batch(pk, sig, buf, off, ln, threads: int = 8) -> np.ndarray:
+    n = pk.shape[0]
+    out = np.zeros(n, np.uint8)
+    lib().orc_ed25519_verify_batch(n, p(pk), p(sig), p(buf), p(off), p(ln), p(out), threads)
+    return out.astype(bool)
+
+
+def vrf_verify_batch(pk, proof, alpha32, threads: int = 8):
+    n = pk.shape[0]
+    beta = np.zeros((n, 64), np.uint8)
+    ver = np.zeros(n, np.uint8)
+    lib().orc_vrf03_verify_batch(n, p(pk), p(proof), p(alpha32), 32, p(beta), p(ver), threads)
+    return ver.astype(bool), beta
+
+
+def kes_verify_batch(vk, t, buf, off, ln, sig, threads: int = 8) -> np.ndarray:
+    n = vk.shape[0]
+    out = np.zeros(n, np.uint8)
+    lib().orc_sum6kes_verify_batch(n, p(vk), p(t), p(buf), p(off), p(ln), p(sig), p(out), threads)
+    return out.astype(bool)
+
+
+def tpraos_verify_batch(hb, threads: int = 8):
+    """hb: ouroboros_network_amd.tpraos.HeaderBatch (same SoA as the oracle's)."""
+    n = len(hb)
+    s = hb.c_struct()  # identical field order to orc_tpraos_batch
+    verdict = np.zeros(n, np.uint8)
+    be = np.zeros((n, 64), np.uint8)
+    bl = np.zeros((n, 64), np.uint8)
+    lib().orc_tpraos_verify_batch(ctypes.addressof(s), p(verdict), p(be), p(bl), threads)
+    return verdict, be, bl
+
+
+def sodium():
+    """conda libsodium 1.0.18 (the reference CI's pin), or None if absent."""
+    if not os.path.exists(SODIUM_SO):
+        return None
+    s = ctypes.CDLL(SODIUM_SO)
+    if s.sodium_init() < 0:
+        return None
+    return s
