@@ -1,0 +1,359 @@
+#!/usr/bin/env python3
+"""bench.py -- TPraos header-crypto throughput on MI355X (BASELINE.json metric).
+
+Workload (BASELINE.json configs[3]): full TPraos header batches -- per header
+the opcert Ed25519, Sum6KES (6 Blake2b Merkle levels + Ed25519 leaf over the
+544-byte body) and the eta + leader draft-03 VRF verifies with their outputs.
+Each rank verifies its own contiguous shard of 1,048,576 synthetic headers per
+step (weak scaling; no data-path collective); for N > 1 the step ends with the
+one RCCL all-gather of verdicts and VRF outputs the north star names.
+
+Inputs are synthesised on the device (lib/libouro_synth.so, deterministic
+seeds) and are resident in HBM before timing starts.  The
+CPU baseline is the oracle (oracle/build/liboracle.so, a C port) on a bounded
+sample of the same headers, at the box's CPU share of threads.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--headers H]
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "TPraos header verifies/sec (VRF+KES+Ed25519) at 1/2/4/8 MI355X; Ed25519 ver/s"
+# algorithmic work per unit, SURVEY.md §8(d) / BASELINE.md (limb-MACs)
+MACS_PER_HEADER = 1_319_424
+MACS_PER_ED25519 = 190_912
+SYNTH_SO = os.path.join(ROOT, "ouroboros-network_amd", "lib", "libouro_synth.so")
+
+
+def body_template() -> bytes:
+    """The golden Shelley header body (544 B) from the committed fixtures."""
+    with open(os.path.join(ROOT, "tests", "golden", "reference_kats.json")) as f:
+        kats = json.load(f)
+    from ouroboros_network_amd import header as H
+
+    return H.parse_header(bytes.fromhex(kats["headers"][0]["raw"])).body
+
+
+def synth_headers(n: int, npools: int, device, first: int = 0):
+    """Device-resident SoA header batch (torch uint8 tensors)."""
+    import torch
+
+    lib = ctypes.CDLL(SYNTH_SO)
+    tmpl = body_template()
+    blen = len(tmpl)
+    u8 = dict(dtype=torch.uint8, device=device)
+    t = {
+        "issuer_vk": torch.empty(n * 32, **u8), "vrf_vk": torch.empty(n * 32, **u8),
+        "eta_proof": torch.empty(n * 80, **u8), "leader_proof": torch.empty(n * 80, **u8),
+        "eta_alpha": torch.empty(n * 32, **u8), "leader_alpha": torch.empty(n * 32, **u8),
+        "hot_vk": torch.empty(n * 32, **u8), "ocert_counter": torch.empty(n * 8, **u8),
+        "ocert_kes_period": torch.empty(n * 8, **u8), "ocert_sigma": torch.empty(n * 64, **u8),
+        "kes_t": torch.empty(n * 4, **u8), "kes_sig": torch.empty(n * 448, **u8),
+        "body": torch.empty(n * blen, **u8), "body_off": torch.empty(n * 8, **u8),
+        "body_len": torch.empty(n * 4, **u8),
+    }
+    nodes = torch.empty(npools * 127 * 32, **u8)
+    pool = torch.empty(npools * 56 * 4, **u8)
+    dtmpl = torch.frombuffer(bytearray(tmpl), dtype=torch.uint8).to(device)
+    P = ctypes.c_void_p
+    fn = lib.ouro_synth_headers
+    fn.restype = ctypes.c_int
+    fn.argtypes = [ctypes.c_size_t, ctypes.c_uint64, ctypes.c_int, P, ctypes.c_uint32] + [P] * 17
+    order = ["issuer_vk", "vrf_vk", "eta_proof", "leader_proof", "eta_alpha", "leader_alpha",
+             "hot_vk", "ocert_counter", "ocert_kes_period", "ocert_sigma", "kes_t", "kes_sig",
+             "body", "body_off", "body_len"]
+    rc = fn(n, first, npools, dtmpl.data_ptr(), blen, nodes.data_ptr(), pool.data_ptr(),
+            *[t[k].data_ptr() for k in order])
+    if rc != 0:
+        raise RuntimeError(f"ouro_synth_headers failed: {rc}")
+    torch.cuda.synchronize()
+    return t, blen
+
+
+class DeviceHeaders:
+    """Binds a device SoA to the C ABI's ouro_tpraos_batch."""
+
+    def __init__(self, t, n, device):
+        import torch
+
+        from ouroboros_network_amd import _native
+
+        self.lib = _native.load()
+        self.n = n
+        self.t = t
+        self.s = _native.TPraosBatch()
+        self.s.n = n
+        for k, v in t.items():
+            setattr(self.s, k, v.data_ptr())
+        self.verdict = torch.zeros(n, dtype=torch.uint8, device=device)
+        self.beta_eta = torch.zeros(n * 64, dtype=torch.uint8, device=device)
+        self.beta_leader = torch.zeros(n * 64, dtype=torch.uint8, device=device)
+
+    def launch(self, stream) -> None:
+        from ouroboros_network_amd import _native
+
+        rc = self.lib.ouro_tpraos_verify_batch_device(
+            ctypes.c_void_p(stream.cuda_stream), ctypes.byref(self.s), self.verdict.data_ptr(),
+            self.beta_eta.data_ptr(), self.beta_leader.data_ptr())
+        _native.check(rc, "ouro_tpraos_verify_batch_device")
+
+    def host_sample(self, m: int):
+        """First m headers copied to host as a HeaderBatch (for the CPU leg)."""
+        from ouroboros_network_amd.tpraos import HeaderBatch
+
+        def h(k, dt, w=None):
+            a = self.t[k].cpu().numpy().view(dt)
+            return a.reshape(-1, w)[:m] if w else a[:m]
+
+        blen = int(h("body_len", np.uint32)[0])
+        body = self.t["body"][: m * blen].cpu().numpy()
+        return HeaderBatch(
+            issuer_vk=h("issuer_vk", np.uint8, 32), vrf_vk=h("vrf_vk", np.uint8, 32),
+            eta_proof=h("eta_proof", np.uint8, 80), leader_proof=h("leader_proof", np.uint8, 80),
+            eta_alpha=h("eta_alpha", np.uint8, 32), leader_alpha=h("leader_alpha", np.uint8, 32),
+            hot_vk=h("hot_vk", np.uint8, 32), ocert_counter=h("ocert_counter", np.uint64),
+            ocert_kes_period=h("ocert_kes_period", np.uint64),
+            ocert_sigma=h("ocert_sigma", np.uint8, 64), kes_t=h("kes_t", np.uint32),
+            kes_sig=h("kes_sig", np.uint8, 448), body=body, body_off=h("body_off", np.uint64),
+            body_len=h("body_len", np.uint32))
+
+
+def measure_peak_mac(device) -> float:
+    """Live v_mad_u64_u32 rate (TMAC/s) from the microbenchmark kernel."""
+    lib = ctypes.CDLL(SYNTH_SO)
+    fn = lib.ouro_peak_mad_u64_tmacs
+    fn.restype = ctypes.c_double
+    return float(fn())
+
+
+def ed25519_rate(device, n: int, reps: int):
+    """Ed25519 verifies/s on n device-resident synthetic signatures."""
+    import torch
+
+    from ouroboros_network_amd import _native
+
+    lib = ctypes.CDLL(SYNTH_SO)
+    u8 = dict(dtype=torch.uint8, device=device)
+    pk, sig, msg = torch.empty(n * 32, **u8), torch.empty(n * 64, **u8), torch.empty(n * 32, **u8)
+    lib.ouro_synth_ed25519.argtypes = [ctypes.c_size_t, ctypes.c_uint64] + [ctypes.c_void_p] * 3
+    if lib.ouro_synth_ed25519(n, 0, pk.data_ptr(), sig.data_ptr(), msg.data_ptr()) != 0:
+        raise RuntimeError("ouro_synth_ed25519 failed")
+    off = torch.arange(n, dtype=torch.int64, device=device) * 32
+    ln = torch.full((n,), 32, dtype=torch.int32, device=device)
+    ver = torch.zeros(n, **u8)
+    v = _native.load()
+    st = torch.cuda.current_stream()
+
+    def go():
+        rc = v.ouro_ed25519_verify_batch_device(ctypes.c_void_p(st.cuda_stream), n, pk.data_ptr(),
+                                                 sig.data_ptr(), msg.data_ptr(), off.data_ptr(),
+                                                 ln.data_ptr(), ver.data_ptr())
+        _native.check(rc, "ed25519 device batch")
+
+    go()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        go()
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    ok = int(ver.sum().item())
+    return {"value": n / (ms * 1e-3), "unit": "verifies/s", "n": n, "ms_per_launch": ms,
+            "all_valid": ok == n,
+            "roofline_frac": (n * MACS_PER_ED25519 / (ms * 1e-3) / 1e12)}
+
+
+def cpu_baseline(hb, threads: int):
+    """The oracle (C port) on a bounded sample; returns (rate, results)."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_ffi as O
+
+    O.lib()
+    t0 = time.perf_counter()
+    res = O.tpraos_verify_batch(hb, threads=threads)
+    dt = time.perf_counter() - t0
+    return len(hb) / dt, dt, res
+
+
+def load_pmc_traffic():
+    """HBM bytes per launch of the header kernel from the committed PMC run."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        return d.get("k_tpraos_verify_bytes_per_launch_per_header")
+    except (OSError, ValueError):
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--headers", type=int, default=1 << 20, help="headers per GPU per step")
+    ap.add_argument("--pools", type=int, default=1024)
+    ap.add_argument("--cpu-sample", type=int, default=16384)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-extras", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        if world == 1 and args.gpus > 1:
+            raise SystemExit("--gpus > 1 must be launched with torch.distributed.run")
+    torch.cuda.set_device(local)
+    device = torch.device("cuda", local)
+    from ouroboros_network_amd import _native
+
+    _native.load().ouro_set_device(local)
+    if world > 1:
+        os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        dist.init_process_group("nccl", device_id=device)
+
+    n = args.headers
+    # each rank synthesises its own contiguous shard: global headers
+    # [rank*n, (rank+1)*n), seeds indexed by the global header number
+    t_syn = time.perf_counter()
+    tensors, blen = synth_headers(n, args.pools, device, first=rank * n)
+    syn_s = time.perf_counter() - t_syn
+    hdr = DeviceHeaders(tensors, n, device)
+    stream = torch.cuda.current_stream()
+
+    gather_bufs = None
+    if world > 1:
+        out_bytes = n * 129
+        gather_bufs = [torch.empty(out_bytes, dtype=torch.uint8, device=device) for _ in range(world)]
+
+    def step():
+        hdr.launch(stream)
+        if world > 1:
+            mine = torch.cat([hdr.verdict, hdr.beta_eta, hdr.beta_leader])
+            dist.all_gather(gather_bufs, mine)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    # correctness gate: every synthetic header must verify
+    all_ok = bool((hdr.verdict == 15).all().item())
+
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(args.steps)]
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        ev[k][0].record(stream)
+        hdr.launch(stream)
+        ev[k][1].record(stream)
+        if world > 1:
+            mine = torch.cat([hdr.verdict, hdr.beta_eta, hdr.beta_leader])
+            dist.all_gather(gather_bufs, mine)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    if world > 1:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+        ok_t = torch.tensor([1 if all_ok else 0], dtype=torch.int32, device=device)
+        dist.all_reduce(ok_t, op=dist.ReduceOp.MIN)
+        all_ok = bool(ok_t.item())
+
+    total = n * world * args.steps
+    value = total / elapsed
+    ms_per_step = elapsed / args.steps * 1e3
+
+    if rank == 0:
+        peak = None
+        try:
+            peak = measure_peak_mac(device)
+        except Exception as e:  # noqa: BLE001
+            print(f"# peak microbench failed: {e}", file=sys.stderr)
+        achieved = n * MACS_PER_HEADER / (kern_ms * 1e-3) / 1e12
+        traffic_per_header = load_pmc_traffic()
+        roof = {
+            "bound": "valu",
+            "kernel": "k_tpraos_verify",
+            "achieved": round(achieved, 3),
+            "peak": round(peak, 3) if peak else None,
+            "unit": "TMAC/s",
+            "frac": round(achieved / peak, 4) if peak else None,
+            "traffic": (traffic_per_header * n if traffic_per_header else None),
+            "macs_per_header": MACS_PER_HEADER,
+            "kernel_ms_per_launch": round(kern_ms, 3),
+        }
+        out = {
+            "metric": METRIC,
+            "value": round(value, 1),
+            "unit": "headers/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u32/u64 (GF(2^255-19) int limbs)",
+            "data": "synthetic (device-signed, deterministic seeds)",
+            "config": {"workload": "tpraos_header_batch (configs[3])",
+                       "headers_per_gpu": n, "global_batch": n * world,
+                       "pools": args.pools, "body_bytes": blen,
+                       "parallelism": f"shard{world}"},
+            "all_valid": all_ok,
+            "synth_s": round(syn_s, 2),
+            "roofline": roof,
+        }
+        if not args.no_extras:
+            try:
+                out["ed25519"] = ed25519_rate(device, 1 << 20, 3)
+                if peak:
+                    out["ed25519"]["roofline_frac"] = round(out["ed25519"]["roofline_frac"] / peak, 4)
+            except Exception as e:  # noqa: BLE001
+                out["ed25519"] = {"error": str(e)}
+        if not args.no_cpu and world == 1:
+            threads = min(16, os.cpu_count() or 1)
+            m = min(args.cpu_sample, n)
+            hb = hdr.host_sample(m)
+            rate, dt, (cv, cbe, cbl) = cpu_baseline(hb, threads)
+            rate1, dt1, _ = cpu_baseline(hb.slice(0, min(512, m)), 1)
+            gv = hdr.verdict[:m].cpu().numpy()
+            gbe = hdr.beta_eta[: m * 64].cpu().numpy().reshape(m, 64)
+            gbl = hdr.beta_leader[: m * 64].cpu().numpy().reshape(m, 64)
+            out["cpu_baseline"] = {
+                "value": round(rate, 1), "unit": "headers/s", "cores": threads,
+                "kind": "port",
+                "sample": f"first {m} of the same synthetic headers, oracle/ C port, "
+                          f"{threads} threads, {dt:.1f} s wall",
+                "one_core": round(rate1, 1),
+                "gpu_equals_cpu_on_sample": bool((gv == cv).all() and (gbe == cbe).all()
+                                                 and (gbl == cbl).all()),
+            }
+        print(json.dumps(out))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

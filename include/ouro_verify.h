@@ -132,7 +132,7 @@ int ouro_tpraos_verify_batch(const ouro_tpraos_batch *b, uint8_t *verdict,
 
 /* ----------------------------------- batch, device-resident buffers ----- */
 /* Same kernels on caller-owned device memory, enqueued on `stream` (a
- * hipStream_t, NULL = the thread's stream) and NOT synchronised: the caller
+ * hipStream_t; NULL = HIP's default stream) and NOT synchronised: the caller
  * orders its own copies/events around them.  `msg_off`/`msg_len` etc. are
  * device pointers too.  Used by bench.py (inputs resident in HBM) and by
  * pipelined callers that overlap H2D of the next window with this one. */

@@ -143,16 +143,20 @@ void orc_tpraos_verify_batch(const orc_tpraos_batch *b, uint8_t *verdict, uint8_
 }
 
 /* ---------------------------------------------------------- synthesis ---- */
-static void seed_of(uint8_t out[32], const char *tag, uint64_t i) {
-  uint8_t buf[64];
+/* tag zero-padded to 12 bytes: every seed message is 32 bytes */
+void orc_seed(uint8_t out[32], const char *tag, uint64_t i) {
+  uint8_t buf[32];
   size_t tl = strlen(tag);
+  if (tl > 12) tl = 12;
+  memset(buf, 0, sizeof buf);
   memcpy(buf, "ouro-mi355x/", 12);
   memcpy(buf + 12, tag, tl);
-  for (int k = 0; k < 8; k++) buf[12 + tl + k] = (uint8_t)(i >> (8 * k));
+  for (int k = 0; k < 8; k++) buf[24 + k] = (uint8_t)(i >> (8 * k));
   uint8_t h[64];
-  orc_sha512(h, buf, 12 + tl + 8);
+  orc_sha512(h, buf, 32);
   memcpy(out, h, 32);
 }
+#define seed_of orc_seed
 
 typedef struct {
   uint64_t first;

@@ -36,15 +36,18 @@ int orc_sum6kes_verify(const uint8_t vk[32], uint32_t t, const uint8_t *m, size_
   return orc_ed25519_verify(sig, m, mlen, cur);
 }
 
-/* ---- synthetic tree (test data only) ---- */
+/* ---- synthetic tree (test data only) ----
+ * leaf i seed = SHA-512(tree seed || LE32(i))[0:32]; the device synthesiser
+ * (ouroboros-network_amd/csrc/synth.hip) derives the same keys. */
 static void leaf_seed(uint8_t out[32], const uint8_t seed[32], uint32_t i) {
-  uint8_t buf[36];
+  uint8_t buf[36], h[64];
   memcpy(buf, seed, 32);
   buf[32] = (uint8_t)i;
   buf[33] = (uint8_t)(i >> 8);
   buf[34] = (uint8_t)(i >> 16);
   buf[35] = (uint8_t)(i >> 24);
-  orc_blake2b_256(out, buf, sizeof buf);
+  orc_sha512(h, buf, sizeof buf);
+  memcpy(out, h, 32);
 }
 
 /* level[0] = 64 leaf vks, level[k] = 64 >> k node hashes */

@@ -66,7 +66,7 @@ int orc_vrf03_prove(uint8_t proof[80], const uint8_t sk[64], const uint8_t *m, s
 #define ORC_KES_SIGBYTES 448
 int orc_sum6kes_verify(const uint8_t vk[32], uint32_t t, const uint8_t *m, size_t mlen,
                        const uint8_t sig[ORC_KES_SIGBYTES]);
-/* Synthetic tree (test data only): 64 leaf seeds = Blake2b_256(seed || LE32(i)).
+/* Synthetic tree (test data only): 64 leaf seeds = SHA-512(seed || LE32(i))[0:32].
  * Writes the root vk; sign produces the 448-B signature for period t. */
 void orc_sum6kes_keygen(uint8_t root_vk[32], const uint8_t seed[32]);
 void orc_sum6kes_sign(uint8_t sig[ORC_KES_SIGBYTES], const uint8_t seed[32], uint32_t t,
@@ -115,7 +115,9 @@ void orc_sum6kes_verify_batch(size_t n, const uint8_t *vk, const uint32_t *t,
 void orc_tpraos_verify_batch(const orc_tpraos_batch *b, uint8_t *verdict, uint8_t *beta_eta,
                              uint8_t *beta_leader, int threads);
 
-/* synthesis helpers (threaded) used by tests/bench to build inputs */
+/* synthesis helpers (threaded) used by tests to build inputs;
+ * seed(tag, i) = SHA-512("ouro-mi355x/" || tag zero-padded to 12 B || LE64(i))[0:32] */
+void orc_seed(uint8_t out[32], const char *tag, uint64_t i);
 void orc_synth_ed25519(size_t n, uint64_t first, uint8_t *pk, uint8_t *sig, uint8_t *msg32,
                        int threads);
 void orc_synth_vrf(size_t n, uint64_t first, uint8_t *pk, uint8_t *proof, uint8_t *alpha32,

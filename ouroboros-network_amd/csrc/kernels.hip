@@ -54,7 +54,7 @@ __device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap
 
 // ---------------------------------------------------------------- kernels ----
 
-__global__ void __launch_bounds__(kBlock) k_ed25519_verify(
+__global__ void __launch_bounds__(kBlock, 2) k_ed25519_verify(
     size_t n, const uint8_t* __restrict__ pk, const uint8_t* __restrict__ sig,
     const uint8_t* __restrict__ msg, const uint64_t* __restrict__ msg_off,
     const uint32_t* __restrict__ msg_len, uint8_t* __restrict__ verdict, int32_t* scratch,
@@ -71,7 +71,7 @@ __global__ void __launch_bounds__(kBlock) k_ed25519_verify(
   }
 }
 
-__global__ void __launch_bounds__(kBlock) k_vrf03_verify(
+__global__ void __launch_bounds__(kBlock, 2) k_vrf03_verify(
     size_t n, const uint8_t* __restrict__ pk, const uint8_t* __restrict__ proof,
     const uint8_t* __restrict__ alpha, const uint64_t* __restrict__ alpha_off,
     const uint32_t* __restrict__ alpha_len, uint8_t* __restrict__ beta,
@@ -89,7 +89,7 @@ __global__ void __launch_bounds__(kBlock) k_vrf03_verify(
   }
 }
 
-__global__ void __launch_bounds__(kBlock) k_sum6kes_verify(
+__global__ void __launch_bounds__(kBlock, 2) k_sum6kes_verify(
     size_t n, const uint8_t* __restrict__ vk, const uint32_t* __restrict__ t,
     const uint8_t* __restrict__ msg, const uint64_t* __restrict__ msg_off,
     const uint32_t* __restrict__ msg_len, const uint8_t* __restrict__ sig,
@@ -106,7 +106,7 @@ __global__ void __launch_bounds__(kBlock) k_sum6kes_verify(
   }
 }
 
-__global__ void __launch_bounds__(kBlock) k_tpraos_verify(ouro_tpraos_batch b,
+__global__ void __launch_bounds__(kBlock, 2) k_tpraos_verify(ouro_tpraos_batch b,
                                                           uint8_t* __restrict__ verdict,
                                                           uint8_t* __restrict__ beta_eta,
                                                           uint8_t* __restrict__ beta_leader,
@@ -157,7 +157,7 @@ __global__ void __launch_bounds__(kBlock) k_tpraos_verify(ouro_tpraos_batch b,
 }
 
 // proof_to_hash only (no verification): beta = H(0x04 || 0x03 || [8]Gamma)
-__global__ void __launch_bounds__(kBlock) k_vrf03_proof_to_hash(size_t n,
+__global__ void __launch_bounds__(kBlock, 2) k_vrf03_proof_to_hash(size_t n,
                                                                 const uint8_t* __restrict__ proof,
                                                                 uint8_t* __restrict__ beta,
                                                                 uint8_t* __restrict__ verdict) {
@@ -640,11 +640,7 @@ int ouro_ed25519_verify_batch_device(void* stream, size_t n, const uint8_t* pk, 
                                      const uint8_t* msg, const uint64_t* msg_off,
                                      const uint32_t* msg_len, uint8_t* verdict) {
   if (n == 0) return OURO_OK;
-  hipStream_t st = static_cast<hipStream_t>(stream);
-  if (!st) {
-    int rc = thread_stream(&st);
-    if (rc) return rc;
-  }
+  hipStream_t st = static_cast<hipStream_t>(stream);  // NULL = HIP's default stream
   return launch_ed(st, n, pk, sig, msg, msg_off, msg_len, verdict);
 }
 
@@ -652,11 +648,7 @@ int ouro_vrf03_verify_batch_device(void* stream, size_t n, const uint8_t* pk, co
                                    const uint8_t* alpha, const uint64_t* alpha_off,
                                    const uint32_t* alpha_len, uint8_t* beta, uint8_t* verdict) {
   if (n == 0) return OURO_OK;
-  hipStream_t st = static_cast<hipStream_t>(stream);
-  if (!st) {
-    int rc = thread_stream(&st);
-    if (rc) return rc;
-  }
+  hipStream_t st = static_cast<hipStream_t>(stream);  // NULL = HIP's default stream
   return launch_vrf(st, n, pk, proof, alpha, alpha_off, alpha_len, beta, verdict);
 }
 
@@ -665,11 +657,7 @@ int ouro_sum6kes_verify_batch_device(void* stream, size_t n, const uint8_t* vk, 
                                      const uint32_t* msg_len, const uint8_t* sig,
                                      uint8_t* verdict) {
   if (n == 0) return OURO_OK;
-  hipStream_t st = static_cast<hipStream_t>(stream);
-  if (!st) {
-    int rc = thread_stream(&st);
-    if (rc) return rc;
-  }
+  hipStream_t st = static_cast<hipStream_t>(stream);  // NULL = HIP's default stream
   return launch_kes(st, n, vk, t, msg, msg_off, msg_len, sig, verdict);
 }
 
@@ -678,11 +666,7 @@ int ouro_tpraos_verify_batch_device(void* stream, const ouro_tpraos_batch* b, ui
   if (!b) return fail(OURO_EINVAL, "null batch");
   if (b->n == 0) return OURO_OK;
   if (!beta_eta || !beta_leader) return fail(OURO_EINVAL, "device API needs both beta buffers");
-  hipStream_t st = static_cast<hipStream_t>(stream);
-  if (!st) {
-    int rc = thread_stream(&st);
-    if (rc) return rc;
-  }
+  hipStream_t st = static_cast<hipStream_t>(stream);  // NULL = HIP's default stream
   return launch_hdr(st, *b, verdict, beta_eta, beta_leader);
 }
 

@@ -146,7 +146,9 @@ def parse_header(raw: bytes) -> ShelleyHeader:
         raise CBORError(f"header body must have 15 fields, got {len(f)}")
     eta = array_items(buf, f[5][0])
     lead = array_items(buf, f[6][0])
-    return ShelleyHeader(
+    if len(eta) != 2 or len(lead) != 2:
+        raise CBORError("VRF certificates must be [output, proof]")
+    hdr = ShelleyHeader(
         era=era,
         block_no=uint_at(buf, f[0][0]),
         slot=uint_at(buf, f[1][0]),
@@ -164,6 +166,13 @@ def parse_header(raw: bytes) -> ShelleyHeader:
         kes_sig=bytes_at(buf, s0),
         body_span=(b0, b1),
     )
+    # rawDeserialise* of the fixed-size crypto types rejects any other length
+    for name, want in (("issuer_vk", 32), ("vrf_vk", 32), ("eta_output", 64),
+                       ("eta_proof", 80), ("leader_output", 64), ("leader_proof", 80),
+                       ("hot_vk", 32), ("ocert_sigma", 64), ("kes_sig", 448)):
+        if len(getattr(hdr, name)) != want:
+            raise CBORError(f"{name}: expected {want} bytes")
+    return hdr
 
 
 def kes_t(slot: int, slots_per_kes_period: int, c0: int) -> int:

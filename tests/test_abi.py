@@ -1,0 +1,81 @@
+"""The C-ABI boundary (CPU-only): the product library loads, exports every
+symbol include/*.h declares, and the Python mirror types every one of them.
+No compute calls are made here; on a host without a GPU the library must
+report an error -- never "valid".
+"""
+import ctypes
+import glob
+import os
+import re
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB = os.path.join(ROOT, "ouroboros-network_amd", "lib", "libouro_verify.so")
+
+
+def declared_symbols():
+    syms = set()
+    for h in glob.glob(os.path.join(ROOT, "include", "*.h")):
+        text = open(h).read()
+        text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+        for m in re.finditer(r"\b(ouro_[a-z0-9_]+)\s*\(", text):
+            syms.add(m.group(1))
+    return syms
+
+
+def test_header_declares_the_boundary():
+    syms = declared_symbols()
+    for s in ("ouro_ed25519_verify", "ouro_vrf03_verify", "ouro_vrf03_proof_to_hash",
+              "ouro_sum6kes_verify", "ouro_ed25519_verify_batch", "ouro_vrf03_verify_batch",
+              "ouro_sum6kes_verify_batch", "ouro_tpraos_verify_batch",
+              "ouro_tpraos_verify_batch_device"):
+        assert s in syms
+
+
+def test_library_exports_every_declared_symbol():
+    assert os.path.exists(LIB), "build the library first (__graft_entry__.build())"
+    lib = ctypes.CDLL(LIB)
+    missing = [s for s in declared_symbols() if not hasattr(lib, s)]
+    assert not missing, missing
+
+
+def test_python_mirror_types_every_symbol():
+    from ouroboros_network_amd import _native
+
+    assert set(_native.SIGNATURES) == declared_symbols()
+
+
+def test_struct_layout_matches_header():
+    """ouro_tpraos_batch field order/size as the C header declares it."""
+    from ouroboros_network_amd import _native
+
+    text = open(os.path.join(ROOT, "include", "ouro_verify.h")).read()
+    body = text[text.index("typedef struct ouro_tpraos_batch"):text.index("} ouro_tpraos_batch;")]
+    names = re.findall(r"\*?\s*\b([a-z_]+);", body)
+    assert [f[0] for f in _native.TPraosBatch._fields_] == names
+    assert ctypes.sizeof(_native.TPraosBatch) == 16 * 8
+
+
+def test_no_device_is_an_error_not_an_accept():
+    import torch
+
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is present")
+    lib = ctypes.CDLL(LIB)
+    lib.ouro_ed25519_verify.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_ulonglong,
+                                        ctypes.c_void_p]
+    rc = lib.ouro_ed25519_verify(bytes(64), b"", 0, bytes(32))
+    assert rc != 0
+
+
+def test_missing_library_fails_loudly(tmp_path):
+    from ouroboros_network_amd import _native
+
+    with pytest.raises(_native.NativeUnavailable):
+        _native._lib_saved = _native._lib
+        _native._lib = None
+        try:
+            _native.load(str(tmp_path / "nope.so"))
+        finally:
+            _native._lib = _native._lib_saved

@@ -1,0 +1,140 @@
+"""The kernels' lane routines (verify.h), compiled for the host by hipcc, against
+the oracle and exact integer arithmetic (CPU-only; no GPU needed).
+
+This checks the arithmetic the gfx950 kernels execute -- same source, same
+limb representation -- before any GPU time is spent.  It is not the product
+path: the product library only runs these routines inside kernels.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+import oracle_ffi as O
+from edge_cases import ed25519_edge_cases, vrf_edge_cases
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SO = os.path.join(ROOT, "ouroboros-network_amd", "lib", "libouro_devhost_test.so")
+P = 2**255 - 19
+L = 2**252 + 27742317777372353535851937790883648493
+
+
+@pytest.fixture(scope="module")
+def dh():
+    if not os.path.exists(SO):
+        subprocess.run(["make", "-C", os.path.join(ROOT, "ouroboros-network_amd"),
+                        "lib/libouro_devhost_test.so"], check=True, stdout=subprocess.DEVNULL)
+    return ctypes.CDLL(SO)
+
+
+def enc(x):
+    return (x % P).to_bytes(32, "little")
+
+
+def dec(b):
+    return int.from_bytes(b, "little")
+
+
+def test_field_ops(dh):
+    rng = np.random.default_rng(0)
+    out = ctypes.create_string_buffer(32)
+    specials = [0, 1, 2, P - 1, P - 2, 19, 2**255 - 20, 2**254, (P - 1) // 2]
+    vals = specials + [int.from_bytes(rng.bytes(32), "little") % P for _ in range(300)]
+    for i, x in enumerate(vals):
+        y = vals[(7 * i + 3) % len(vals)]
+        dh.dh_fe_mul(out, enc(x), enc(y))
+        assert dec(out.raw) == x * y % P
+        dh.dh_fe_sq(out, enc(x))
+        assert dec(out.raw) == x * x % P
+        dh.dh_fe_sub(out, enc(x), enc(y))
+        assert dec(out.raw) == (x - y) % P
+    for x in specials[1:6] + vals[20:40]:
+        dh.dh_fe_invert(out, enc(x))
+        assert dec(out.raw) == pow(x, P - 2, P)
+
+
+def test_tobytes_canonicalises_unreduced_limbs(dh):
+    """fe_to_words on limb vectors at and beyond the 'reduced' bounds."""
+    rng = np.random.default_rng(1)
+    E = [0, 26, 51, 77, 102, 128, 153, 179, 204, 230]
+    out = ctypes.create_string_buffer(32)
+    for _ in range(500):
+        limbs = [int(rng.integers(-(3 << 25), 3 << 25)) for _ in range(10)]
+        arr = (ctypes.c_int32 * 10)(*limbs)
+        dh.dh_fe_limbs_tobytes(out, arr)
+        want = sum(l << E[i] for i, l in enumerate(limbs)) % P
+        assert dec(out.raw) == want
+
+
+def test_scalar_reduce(dh):
+    rng = np.random.default_rng(2)
+    out = ctypes.create_string_buffer(32)
+    for v in [b"\xff" * 64, bytes(64), L.to_bytes(64, "little"), (L - 1).to_bytes(64, "little"),
+              (2 * L).to_bytes(64, "little")] + [rng.bytes(64) for _ in range(200)]:
+        dh.dh_sc_reduce64(out, v)
+        assert dec(out.raw) == dec(v) % L
+
+
+def test_hashes(dh):
+    import hashlib
+
+    rng = np.random.default_rng(3)
+    out = ctypes.create_string_buffer(64)
+    for n in [0, 1, 47, 48, 49, 63, 64, 65, 175, 176, 177, 544, 1000]:
+        pre, m = rng.bytes(64), rng.bytes(n)
+        dh.dh_sha512_prefixed64(out, pre, m, n)
+        assert out.raw == hashlib.sha512(pre + m).digest()
+    x = rng.bytes(64)
+    dh.dh_blake2b256_64(out, x)
+    assert out.raw[:32] == hashlib.blake2b(x, digest_size=32).digest()
+
+
+def test_elligator2(dh):
+    rng = np.random.default_rng(4)
+    out = ctypes.create_string_buffer(32)
+    for _ in range(40):
+        r = bytearray(rng.bytes(32))
+        r[31] &= 0x7F
+        dh.dh_elligator2(out, bytes(r))
+        assert out.raw == O.elligator2(bytes(r))
+
+
+def test_ed25519_lane(dh):
+    pk, sig, msg = O.synth_ed25519(48, first=9)
+    for i in range(48):
+        s = bytearray(sig[i])
+        if i % 3 == 1:
+            s[i % 64] ^= 0x10
+        m = bytes(msg[i])
+        assert (dh.dh_ed25519_verify(bytes(s), m, len(m), bytes(pk[i])) == 0) == \
+            O.ed25519_verify(bytes(s), m, bytes(pk[i]))
+
+
+def test_ed25519_lane_edge_cases(dh):
+    for pk, sig, m in ed25519_edge_cases():
+        assert (dh.dh_ed25519_verify(sig, m, len(m), pk) == 0) == O.ed25519_verify(sig, m, pk)
+
+
+def test_vrf_lane(dh, kats):
+    out = ctypes.create_string_buffer(64)
+    for v in kats["vrf_draft03"]:
+        a = bytes.fromhex(v["alpha"])
+        assert dh.dh_vrf03_verify(out, bytes.fromhex(v["pk"]), bytes.fromhex(v["pi"]), a, len(a)) == 0
+        assert out.raw.hex() == v["beta"]
+    for pk, pi, a in vrf_edge_cases():
+        rc = dh.dh_vrf03_verify(out, pk, pi, a, len(a))
+        want = O.vrf_verify(pk, pi, a)
+        assert (rc == 0) == (want is not None)
+        if want is not None:
+            assert out.raw == want
+
+
+def test_kes_lane_golden(dh, kats):
+    from ouroboros_network_amd import header as H
+
+    for h in kats["headers"]:
+        hd = H.parse_header(bytes.fromhex(h["raw"]))
+        assert dh.dh_sum6kes_verify(hd.hot_vk, 0, hd.body, len(hd.body), hd.kes_sig) == 0
+        assert dh.dh_sum6kes_verify(hd.hot_vk, 1, hd.body, len(hd.body), hd.kes_sig) != 0
