@@ -13,6 +13,10 @@
 
 using namespace ouro;
 
+#if defined(OURO_COUNT_OPS)
+thread_local unsigned long long g_ouro_nmul = 0, g_ouro_nsq = 0, g_ouro_bound_violations = 0;
+#endif
+
 namespace {
 const int32_t* host_btab() {
   static std::vector<int32_t> tab = [] {
@@ -38,6 +42,28 @@ void fe_to_bytes(uint8_t* out, const fe& f) {
 }  // namespace
 
 extern "C" {
+
+// field-operation counters (valid when built with -DOURO_COUNT_OPS)
+void dh_count_reset(void) {
+#if defined(OURO_COUNT_OPS)
+  g_ouro_nmul = g_ouro_nsq = 0;
+#endif
+}
+unsigned long long dh_bound_violations(void) {
+#if defined(OURO_COUNT_OPS)
+  return g_ouro_bound_violations;
+#else
+  return ~0ull;
+#endif
+}
+void dh_count_get(unsigned long long* nmul, unsigned long long* nsq) {
+#if defined(OURO_COUNT_OPS)
+  *nmul = g_ouro_nmul;
+  *nsq = g_ouro_nsq;
+#else
+  *nmul = *nsq = 0;
+#endif
+}
 
 // field ops on canonical 32-byte encodings
 void dh_fe_mul(uint8_t* out, const uint8_t* a, const uint8_t* b) {
@@ -83,6 +109,15 @@ void dh_elligator2(uint8_t* out, const uint8_t* r32) {
   bytes_to_words8(r, r32);
   r[7] &= 0x7fffffffu;
   ge_p3 H = elligator2_h(r);
+  uint32_t enc[8];
+  ge_encode_with_inv(enc, H.X, H.Y, fe_invert(H.Z));
+  memcpy(out, enc, 32);
+}
+void dh_elligator2_ref(uint8_t* out, const uint8_t* r32) {
+  uint32_t r[8];
+  bytes_to_words8(r, r32);
+  r[7] &= 0x7fffffffu;
+  ge_p3 H = elligator2_h_ref(r);
   uint32_t enc[8];
   ge_encode_with_inv(enc, H.X, H.Y, fe_invert(H.Z));
   memcpy(out, enc, 32);

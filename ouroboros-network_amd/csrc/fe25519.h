@@ -15,6 +15,25 @@
 #pragma once
 #include "common.h"
 
+// Operation counting for the host test build only (tools/count_ops.py): the
+// device code never defines OURO_COUNT_OPS.
+// The same build also checks the bound discipline below on every multiplier
+// input (tests assert zero violations over all vectors).
+#if defined(OURO_COUNT_OPS) && !defined(__HIP_DEVICE_COMPILE__)
+extern thread_local unsigned long long g_ouro_nmul, g_ouro_nsq, g_ouro_bound_violations;
+#define OURO_COUNT_MUL() (++g_ouro_nmul)
+#define OURO_COUNT_SQ() (++g_ouro_nsq)
+#define OURO_CHECK_BOUNDS(f)                                                  \
+  do {                                                                        \
+    for (int i_ = 0; i_ < 10; i_++)                                           \
+      if ((f).v[i_] > 113025455 || (f).v[i_] < -113025455) ++g_ouro_bound_violations; \
+  } while (0)
+#else
+#define OURO_COUNT_MUL() ((void)0)
+#define OURO_COUNT_SQ() ((void)0)
+#define OURO_CHECK_BOUNDS(f) ((void)0)
+#endif
+
 namespace ouro {
 
 struct fe {
@@ -122,6 +141,9 @@ OURO_FI fe fe_carry(const fe& f) {
 // terms carry a factor 2 (2^ceil(25.5 i) 2^ceil(25.5 j) = 2 * 2^ceil(25.5 (i+j)))
 // and wrapped terms a factor 19 (2^255 = 19).
 OURO_FI fe fe_mul(const fe& f, const fe& g) {
+  OURO_COUNT_MUL();
+  OURO_CHECK_BOUNDS(f);
+  OURO_CHECK_BOUNDS(g);
   int32_t g19[10], f2[10];
 #pragma unroll
   for (int i = 0; i < 10; i++) {
@@ -146,6 +168,8 @@ OURO_FI fe fe_mul(const fe& f, const fe& g) {
 
 // Column sums of f^2 (before carry); shared by fe_sq and fe_sq2.
 OURO_FI void fe_sq_cols(int64_t t[10], const fe& f) {
+  OURO_COUNT_SQ();
+  OURO_CHECK_BOUNDS(f);
   int32_t f2[10], f4[10], f19[10];
 #pragma unroll
   for (int i = 0; i < 10; i++) {

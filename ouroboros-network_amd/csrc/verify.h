@@ -37,9 +37,9 @@ constexpr int kSlotCarry = kSlotB + 8;            // 6 words (3 x u64)
 constexpr int kSlotOut = kSlotCarry + 8;          // p2 result: 3 fe at 12-word stride
 constexpr int kLaneWords = kSlotOut + 36;         // 708 words = 2832 B (16-B multiple)
 
-constexpr int kBTabEntries = 128;                 // [1..128]B
+constexpr int kBTabEntries = 128;                 // [1..128]B, then [1..128](2^128 B)
 constexpr int kNielsWords = 32;                   // 30 used, padded for 16-B loads
-constexpr int kBTabWords = kBTabEntries * kNielsWords;
+constexpr int kBTabWords = 2 * kBTabEntries * kNielsWords;
 
 // ---- vector load/store helpers ---------------------------------------------
 OURO_FI void st_fe(int32_t* p, const fe& f) {
@@ -130,17 +130,22 @@ OURO_HD inline void build_table(int32_t* tab, const ge_p3& P) {
 
 // ---- the double-scalar multiplication ---------------------------------------
 // cfg: bits 0..6 = number of active width-4 windows of scalar a1 (table 1),
-//      bits 8..14 = same for a2 (table 2, 0 = unused), bit 16 = add [b]B.
+//      bits 8..14 = same for a2 (table 2, 0 = unused), bit 16 = add [b]B,
+//      bit 17 = split b: its width-8 digits 0..15 go with B and digits 16..31
+//      with B' = 2^128 B, so the doubling chain only spans 128 bits
+//      (U = [s]B - [c]Y in the VRF, where c has 128 bits).
 // Reads a1/a2/b and their recoding carries from the lane slot, writes the
 // resulting p2 point to lane[kSlotOut..].  Out of line: the header kernel calls
 // it six times per item, and the loop body is the I-cache-critical code.
-constexpr uint32_t dsm_cfg(int nw1, int nw2, bool useB) {
-  return (uint32_t)nw1 | ((uint32_t)nw2 << 8) | (useB ? (1u << 16) : 0u);
+constexpr uint32_t dsm_cfg(int nw1, int nw2, bool useB, bool splitB = false) {
+  return (uint32_t)nw1 | ((uint32_t)nw2 << 8) | (useB ? (1u << 16) : 0u) |
+         (splitB ? (1u << 17) : 0u);
 }
 
 OURO_NI void dsm(int32_t* lane, const int32_t* btab, uint32_t cfg) {
   const int nw1 = (int)(cfg & 0x7f), nw2 = (int)((cfg >> 8) & 0x7f);
   const bool useB = (cfg >> 16) & 1;
+  const bool splitB = (cfg >> 17) & 1;
   uint32_t a1[8], a2[8], b[8];
   ld_words8(a1, lane + kSlotA1);
   ld_words8(a2, lane + kSlotA2);
@@ -148,16 +153,16 @@ OURO_NI void dsm(int32_t* lane, const int32_t* btab, uint32_t cfg) {
   const uint64_t* carr = reinterpret_cast<const uint64_t*>(lane + kSlotCarry);
   const uint64_t c1 = carr[0], c2 = carr[1], cb = carr[2];
   int top = nw1 > nw2 ? nw1 : nw2;
-  if (useB) top = 64;
+  if (useB) top = splitB ? (top > 32 ? top : 32) : 64;
   // t starts as the identity in p1p1 form (X/Z = 0, Y/T = 1)
   ge_p1p1 t{fe_zero(), fe_one(), fe_one(), fe_one()};
 #pragma unroll 1
   for (int j = top - 1; j >= 0; j--) {
 #pragma unroll 1
     for (int k = 0; k < 4; k++) t = ge_p2_dbl(ge_p1p1_to_p2(t));
-    // up to three additions, each from a wave-uniform source
+    // up to four additions, each from a wave-uniform source
 #pragma unroll 1
-    for (int src = 0; src < 3; src++) {
+    for (int src = 0; src < 4; src++) {
       bool active;
       int32_t d;
       if (src == 0) {
@@ -166,9 +171,12 @@ OURO_NI void dsm(int32_t* lane, const int32_t* btab, uint32_t cfg) {
       } else if (src == 1) {
         active = j < nw2;
         d = active ? sc_digit<4>(a2, c2, j) : 0;
-      } else {
-        active = useB && (j & 1) == 0;
+      } else if (src == 2) {
+        active = useB && (j & 1) == 0 && (!splitB || j < 32);
         d = active ? sc_digit<8>(b, cb, j >> 1) : 0;
+      } else {
+        active = splitB && (j & 1) == 0 && j < 32;
+        d = active ? sc_digit<8>(b, cb, (j >> 1) + 16) : 0;
       }
       if (!active) continue;
       const bool neg = d < 0;
@@ -178,7 +186,8 @@ OURO_NI void dsm(int32_t* lane, const int32_t* btab, uint32_t cfg) {
       if (src < 2) {
         q = ld_cached(lane + (src == 0 ? kSlotTab1 : kSlotTab2) + idx * kCachedWords);
       } else {
-        ge_niels nq = ld_niels(btab + idx * kNielsWords);
+        const int base = src == 3 ? kBTabEntries : 0;
+        ge_niels nq = ld_niels(btab + (base + idx) * kNielsWords);
         q = ge_cached{nq.yplusx, nq.yminusx, fe_one(), nq.xy2d};
       }
       if (mag == 0) q = ge_cached_identity();
@@ -242,7 +251,54 @@ OURO_HD inline bool ed25519_verify_lane(const uint32_t sig[16], const uint32_t p
 // ---- ECVRF-ED25519-SHA512-Elligator2 (draft-03) -------------------------------
 // libsodium 1.0.18 ge25519_from_uniform with x_sign = 0 (the VRF clears bit 255
 // of r before calling it): returns [8] of the Elligator2 image.
+//
+// Same point as the reference, two exponentiations instead of four.  With
+// D = 1 + 2r^2 the Montgomery x = -A/D is kept as a fraction:
+//   e = x^3 + A x^2 + x has chi(e) = chi(-A W D), W = D^2 - 2 A^2 r^2
+//   (e and -A W D differ by the square D^4);  -x - A = -2 A r^2 / D, so
+//   x_final = Xn / D with Xn = -A (chi = 1 or 0) or -2 A r^2 (chi = -1);
+//   y_ed = (x_final - 1)/(x_final + 1) = (Xn - D)/(Xn + D) = n/m
+// and the Edwards x comes straight from the ratio
+//   x^2 = (y^2 - 1)/(d y^2 + 1) = (n^2 - m^2)/(d n^2 + m^2)
+// with one square-root-of-ratio exponentiation, sign chosen even as
+// ge25519_frombytes does for the (canonical, sign 0) encoding of y_ed.
+// D != 0 (-2 is a non-square mod p) and m != 0 (neither (A-1)/2 nor
+// 1/(2(A-1)) is a square; tools/check_elligator_exceptions.py), so no inverse
+// of zero can occur where libsodium would have computed one.
 OURO_HD inline ge_p3 elligator2_h(const uint32_t r[8]) {
+  const fe one = fe_one();
+  const fe A = fe_mont_a();
+  fe rr = fe_from_words(r);
+  fe r2 = fe_sq(rr);
+  fe D = fe_carry(fe_add(fe_add(r2, r2), one));         // 1 + 2 r^2 (re-balanced:
+                                                        // n = Xn - D below sums 4 terms)
+  fe A2r2 = fe_mul(fe_mul(A, A), r2);                   // A^2 r^2
+  fe W = fe_sub(fe_sq(D), fe_add(A2r2, A2r2));          // D^2 - 2 A^2 r^2
+  fe e = fe_neg(fe_mul(fe_mul(A, W), D));               // -A W D
+  fe chi = fe_mul(fe_sq(fe_sq(fe_pow22523(e))), fe_sq(e));  // e^((p-1)/2)
+  uint32_t cw[8];
+  fe_to_words(cw, chi);
+  const bool e_is_minus_1 = (cw[0] >> 8) & 1;  // libsodium's byte-1 test
+  fe Ar2 = fe_mul(A, r2);
+  fe Xn = fe_carry(fe_select(fe_neg(fe_add(Ar2, Ar2)), fe_neg(A), e_is_minus_1));
+  fe n = fe_sub(Xn, D), m = fe_add(Xn, D);
+  // x = sqrt(u / v), u = n^2 - m^2, v = d n^2 + m^2
+  fe n2 = fe_sq(n), m2 = fe_sq(m);
+  fe u = fe_sub(n2, m2);
+  fe v = fe_add(fe_mul(n2, fe_d()), m2);
+  fe v3 = fe_mul(fe_sq(v), v);
+  fe x = fe_mul(fe_mul(u, v3), fe_pow22523(fe_mul(fe_mul(fe_sq(v3), v), u)));
+  fe vxx = fe_mul(fe_sq(x), v);
+  const bool m_root = fe_iszero(fe_sub(vxx, u));
+  x = fe_select(x, fe_mul(x, fe_sqrtm1()), m_root);
+  x = fe_select(fe_neg(x), x, fe_isnegative(x));  // sign bit 0: even x
+  ge_p3 P{fe_mul(x, m), n, m, fe_mul(x, n)};
+  return ge_mul8(P);
+}
+
+// The straight restatement of ge25519_from_uniform (4 exponentiations), kept
+// for the host tests that pin elligator2_h against it.
+OURO_HD inline ge_p3 elligator2_h_ref(const uint32_t r[8]) {
   const fe one = fe_one();
   const fe A = fe_mont_a();
   fe rr = fe_from_words(r);
@@ -319,7 +375,7 @@ OURO_HD inline bool vrf03_verify_lane(uint32_t beta[16], const uint32_t pk[8],
   uint64_t* carr = reinterpret_cast<uint64_t*>(lane + kSlotCarry);
   carr[0] = sc_recode_carries<4, 33>(c);
   carr[2] = sc_recode_carries<8, 32>(s);
-  dsm(lane, btab, dsm_cfg(33, 0, true));
+  dsm(lane, btab, dsm_cfg(33, 0, true, true));
   ge_p2 U = dsm_result(lane);
   // V = [s]H - [c]Gamma
   build_table(lane + kSlotTab1, Hp);
@@ -422,18 +478,13 @@ OURO_HD inline bool sum6kes_verify_lane(const uint32_t vk[8], uint32_t t, const 
   return ok && leaf;
 }
 
-// ---- fixed-base table (host side, computed once per process) -----------------
-// [k]B for k = 1..128 as (y + x, y - x, 2 d x y), affine, reduced limbs.
-OURO_HD inline void build_btab(int32_t* out) {
-  // B = (x, 4/5) with x even: encoding 0x5866...66 (little-endian)
-  uint32_t by[8];
-  for (int i = 0; i < 8; i++) by[i] = 0x66666666u;
-  by[0] = 0x66666658u;
-  ge_p3 B;
-  ge_decode(&B, by, false);
-  ge_p3 P = B;
+// ---- fixed-base tables (host side, computed once per process) ----------------
+// [k]G for k = 1..128 as (y + x, y - x, 2 d x y), affine, reduced limbs, for
+// G = B and G = 2^128 B (the split-scalar table of dsm_cfg bit 17).
+OURO_HD inline void build_btab_one(int32_t* out, const ge_p3& G) {
+  ge_p3 P = G;
   for (int k = 0; k < kBTabEntries; k++) {
-    if (k > 0) P = ge_p3_add(P, B);
+    if (k > 0) P = ge_p3_add(P, G);
     fe zi = fe_invert(P.Z);
     fe x = fe_mul(P.X, zi), y = fe_mul(P.Y, zi);
     fe yp = fe_carry(fe_add(y, x)), ym = fe_carry(fe_sub(y, x));
@@ -447,6 +498,19 @@ OURO_HD inline void build_btab(int32_t* out) {
     e[30] = 0;
     e[31] = 0;
   }
+}
+
+OURO_HD inline void build_btab(int32_t* out) {
+  // B = (x, 4/5) with x even: encoding 0x5866...66 (little-endian)
+  uint32_t by[8];
+  for (int i = 0; i < 8; i++) by[i] = 0x66666666u;
+  by[0] = 0x66666658u;
+  ge_p3 B;
+  ge_decode(&B, by, false);
+  build_btab_one(out, B);
+  ge_p3 B128 = B;
+  for (int i = 0; i < 128; i++) B128 = ge_p1p1_to_p3(ge_p3_dbl(B128));
+  build_btab_one(out + kBTabEntries * kNielsWords, B128);
 }
 
 }  // namespace ouro

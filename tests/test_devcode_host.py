@@ -138,3 +138,17 @@ def test_kes_lane_golden(dh, kats):
         hd = H.parse_header(bytes.fromhex(h["raw"]))
         assert dh.dh_sum6kes_verify(hd.hot_vk, 0, hd.body, len(hd.body), hd.kes_sig) == 0
         assert dh.dh_sum6kes_verify(hd.hot_vk, 1, hd.body, len(hd.body), hd.kes_sig) != 0
+
+
+def test_zero_bound_violations(dh):
+    """Every multiplier input seen by the tests above stayed inside the limb
+    bounds fe25519.h's overflow analysis assumes (run last in this module)."""
+    dh.dh_bound_violations.restype = ctypes.c_ulonglong
+    # exercise the VRF / Elligator paths once more on fresh random inputs
+    rng = np.random.default_rng(99)
+    out = ctypes.create_string_buffer(32)
+    for _ in range(200):
+        r = bytearray(rng.bytes(32))
+        r[31] &= 0x7F
+        dh.dh_elligator2(out, bytes(r))
+    assert dh.dh_bound_violations() == 0

@@ -1,0 +1,50 @@
+#!/usr/bin/env python3
+"""Count the GF(2^255-19) multiplications/squarings the kernels' lane routines
+actually execute per unit (host build of verify.h with -DOURO_COUNT_OPS).
+
+Used for DESIGN.md's work table: the roofline numerator stays SURVEY.md
+§8(d)'s canonical figure; this shows how much of it the implementation does.
+"""
+import ctypes
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+import oracle_ffi as O  # noqa: E402
+
+SO = os.path.join(ROOT, "ouroboros-network_amd", "lib", "libouro_devhost_test.so")
+
+
+def main():
+    d = ctypes.CDLL(SO)
+    nm, ns = ctypes.c_ulonglong(), ctypes.c_ulonglong()
+
+    def measure(fn):
+        d.dh_count_reset()
+        fn()
+        d.dh_count_get(ctypes.byref(nm), ctypes.byref(ns))
+        return {"mul": nm.value, "sq": ns.value, "M": nm.value + ns.value}
+
+    pk, sig, msg = O.synth_ed25519(1, first=0)
+    ed = measure(lambda: d.dh_ed25519_verify(bytes(sig[0]), bytes(msg[0]), 32, bytes(pk[0])))
+    vpk, proof, alpha = O.synth_vrf(1, first=0)
+    out = ctypes.create_string_buffer(64)
+    vrf = measure(lambda: d.dh_vrf03_verify(out, bytes(vpk[0]), bytes(proof[0]), bytes(alpha[0]), 32))
+    kats = json.load(open(os.path.join(ROOT, "tests", "golden", "reference_kats.json")))
+    from ouroboros_network_amd import header as H
+
+    hd = H.parse_header(bytes.fromhex(kats["headers"][0]["raw"]))
+    kes = measure(lambda: d.dh_sum6kes_verify(hd.hot_vk, 0, hd.body, len(hd.body), hd.kes_sig))
+    header_M = 2 * vrf["M"] + kes["M"] + ed["M"]
+    res = {"ed25519_verify": ed, "vrf03_verify": vrf, "sum6kes_verify": kes,
+           "tpraos_header_M": header_M,
+           "canonical_M (SURVEY.md §8(d))": {"ed25519": 2983, "vrf": 7325, "header": 20616}}
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    main()
