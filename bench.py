@@ -176,6 +176,58 @@ def ed25519_rate(device, n: int, reps: int):
             "roofline_frac": (n * MACS_PER_ED25519 / (ms * 1e-3) / 1e12)}
 
 
+def component_rates(hdr, n: int, reps: int = 3):
+    """configs[1] and configs[2]: VRF verify + output and Sum6KES verify over
+    the n device-resident items of the synthetic header batch (its eta proofs
+    and its KES signatures), timed with HIP events on the launch stream."""
+    import torch
+
+    from ouroboros_network_amd import _native
+
+    v = _native.load()
+    dev = hdr.verdict.device
+    st = torch.cuda.current_stream()
+    t = hdr.t
+    a_off = torch.arange(n, dtype=torch.int64, device=dev) * 32
+    a_len = torch.full((n,), 32, dtype=torch.int32, device=dev)
+    beta = torch.zeros(n * 64, dtype=torch.uint8, device=dev)
+    ver = torch.zeros(n, dtype=torch.uint8, device=dev)
+    S = ctypes.c_void_p
+
+    def vrf():
+        rc = v.ouro_vrf03_verify_batch_device(S(st.cuda_stream), n, t["vrf_vk"].data_ptr(),
+                                               t["eta_proof"].data_ptr(), t["eta_alpha"].data_ptr(),
+                                               a_off.data_ptr(), a_len.data_ptr(), beta.data_ptr(),
+                                               ver.data_ptr())
+        _native.check(rc, "vrf device batch")
+
+    def kes():
+        rc = v.ouro_sum6kes_verify_batch_device(S(st.cuda_stream), n, t["hot_vk"].data_ptr(),
+                                                 t["kes_t"].data_ptr(), t["body"].data_ptr(),
+                                                 t["body_off"].data_ptr(), t["body_len"].data_ptr(),
+                                                 t["kes_sig"].data_ptr(), ver.data_ptr())
+        _native.check(rc, "kes device batch")
+
+    out = {}
+    for name, fn, macs in (("vrf", vrf, 468_800), ("kes", kes, 190_912)):
+        fn()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(st)
+        for _ in range(reps):
+            fn()
+        e1.record(st)
+        torch.cuda.synchronize()
+        ms = e0.elapsed_time(e1) / reps
+        out[name] = {"value": round(n / (ms * 1e-3), 1), "unit": "verifies/s", "n": n,
+                     "ms_per_launch": round(ms, 3), "all_valid": bool((ver == 1).all().item()),
+                     "achieved_tmacs": round(n * macs / (ms * 1e-3) / 1e12, 3)}
+        if name == "vrf":
+            # the computed outputs must equal the header kernel's eta outputs
+            out[name]["beta_equals_header_kernel"] = bool(torch.equal(beta, hdr.beta_eta))
+    return out
+
+
 def cpu_baseline(hb, threads: int):
     """The oracle (C port) on a bounded sample; returns (rate, results)."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
@@ -209,6 +261,9 @@ def main():
     ap.add_argument("--cpu-sample", type=int, default=16384)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-extras", action="store_true")
+    ap.add_argument("--dist-backend", default="nccl",
+                    help="nccl (RCCL over xGMI, the real path) or gloo (rehearsal of the "
+                         "multi-rank path on fewer GPUs: ranks share devices, gather via host)")
     args = ap.parse_args()
 
     import torch
@@ -220,14 +275,18 @@ def main():
     if world != args.gpus:
         if world == 1 and args.gpus > 1:
             raise SystemExit("--gpus > 1 must be launched with torch.distributed.run")
-    torch.cuda.set_device(local)
-    device = torch.device("cuda", local)
+    gpu = local % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(gpu)
+    device = torch.device("cuda", gpu)
     from ouroboros_network_amd import _native
 
-    _native.load().ouro_set_device(local)
+    _native.load().ouro_set_device(gpu)
     if world > 1:
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-        dist.init_process_group("nccl", device_id=device)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=device)
+        else:
+            dist.init_process_group(args.dist_backend)
 
     n = args.headers
     # each rank synthesises its own contiguous shard: global headers
@@ -238,16 +297,20 @@ def main():
     hdr = DeviceHeaders(tensors, n, device)
     stream = torch.cuda.current_stream()
 
-    gather_bufs = None
-    if world > 1:
-        out_bytes = n * 129
-        gather_bufs = [torch.empty(out_bytes, dtype=torch.uint8, device=device) for _ in range(world)]
+    from ouroboros_network_amd.shard import all_gather_results, pack_results
+
+    def gather():
+        # the one collective of the path: every rank receives all verdicts and
+        # VRF outputs (RCCL all-gather over xGMI), SURVEY.md §8(e)
+        local = pack_results(hdr.verdict, hdr.beta_eta, hdr.beta_leader)
+        if args.dist_backend != "nccl":
+            local = local.cpu()
+        return all_gather_results(local, n * world, world)
 
     def step():
         hdr.launch(stream)
         if world > 1:
-            mine = torch.cat([hdr.verdict, hdr.beta_eta, hdr.beta_leader])
-            dist.all_gather(gather_bufs, mine)
+            gather()
 
     for _ in range(args.warmup):
         step()
@@ -266,18 +329,18 @@ def main():
         hdr.launch(stream)
         ev[k][1].record(stream)
         if world > 1:
-            mine = torch.cat([hdr.verdict, hdr.beta_eta, hdr.beta_leader])
-            dist.all_gather(gather_bufs, mine)
+            gather()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
     if world > 1:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        red_dev = device if args.dist_backend == "nccl" else torch.device("cpu")
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=red_dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
-        ok_t = torch.tensor([1 if all_ok else 0], dtype=torch.int32, device=device)
+        ok_t = torch.tensor([1 if all_ok else 0], dtype=torch.int32, device=red_dev)
         dist.all_reduce(ok_t, op=dist.ReduceOp.MIN)
         all_ok = bool(ok_t.item())
 
@@ -332,6 +395,14 @@ def main():
                     out["ed25519"]["roofline_frac"] = round(out["ed25519"]["roofline_frac"] / peak, 4)
             except Exception as e:  # noqa: BLE001
                 out["ed25519"] = {"error": str(e)}
+            try:
+                comp = component_rates(hdr, n)
+                for k, val in comp.items():
+                    if peak:
+                        val["roofline_frac"] = round(val["achieved_tmacs"] / peak, 4)
+                    out[k] = val
+            except Exception as e:  # noqa: BLE001
+                out["components_error"] = str(e)
         if not args.no_cpu and world == 1:
             threads = min(16, os.cpu_count() or 1)
             m = min(args.cpu_sample, n)

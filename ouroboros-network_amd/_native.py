@@ -11,7 +11,8 @@ import os
 import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libouro_verify.so")
+# OURO_VERIFY_LIB overrides the library (A/B runs of build variants, tools/ab_variants.py)
+LIB_PATH = os.environ.get("OURO_VERIFY_LIB") or os.path.join(_HERE, "lib", "libouro_verify.so")
 
 OURO_OK = 0
 OURO_INVALID = -1
