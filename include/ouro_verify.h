@@ -130,6 +130,22 @@ typedef struct ouro_tpraos_batch {
 int ouro_tpraos_verify_batch(const ouro_tpraos_batch *b, uint8_t *verdict,
                              uint8_t *beta_eta, uint8_t *beta_leader);
 
+/* Latency-oriented variant for small batches (ChainSync windows of up to 300
+ * pipelined headers, ouroboros-network/src/Ouroboros/Network/NodeToNode.hs:197-200):
+ * the six checks of a header run on six lanes concurrently, then one finish
+ * pass.  Same verdicts and outputs as ouro_tpraos_verify_batch. */
+int ouro_tpraos_verify_batch_lowlat(const ouro_tpraos_batch *b, uint8_t *verdict,
+                                    uint8_t *beta_eta, uint8_t *beta_leader);
+
+/* A captured plan for repeated fixed-capacity batches: pinned staging and one
+ * hipGraph (H2D, the two latency-mode kernels, D2H) replayed per call.  A plan
+ * is used by one thread at a time; any n <= max_headers per run. */
+typedef struct ouro_tpraos_plan ouro_tpraos_plan;
+ouro_tpraos_plan *ouro_tpraos_plan_create(size_t max_headers, size_t max_body_bytes);
+int ouro_tpraos_plan_run(ouro_tpraos_plan *plan, const ouro_tpraos_batch *b, uint8_t *verdict,
+                         uint8_t *beta_eta, uint8_t *beta_leader);
+void ouro_tpraos_plan_destroy(ouro_tpraos_plan *plan);
+
 /* ----------------------------------- batch, device-resident buffers ----- */
 /* Same kernels on caller-owned device memory, enqueued on `stream` (a
  * hipStream_t; NULL = HIP's default stream) and NOT synchronised: the caller

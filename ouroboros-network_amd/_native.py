@@ -78,6 +78,10 @@ SIGNATURES = {
     "ouro_vrf03_verify_batch_device": (_I, [_P, _SZ, _P, _P, _P, _P, _P, _P, _P]),
     "ouro_sum6kes_verify_batch_device": (_I, [_P, _SZ, _P, _P, _P, _P, _P, _P, _P]),
     "ouro_tpraos_verify_batch_device": (_I, [_P, ctypes.POINTER(TPraosBatch), _P, _P, _P]),
+    "ouro_tpraos_verify_batch_lowlat": (_I, [ctypes.POINTER(TPraosBatch), _P, _P, _P]),
+    "ouro_tpraos_plan_create": (_P, [_SZ, _SZ]),
+    "ouro_tpraos_plan_run": (_I, [_P, ctypes.POINTER(TPraosBatch), _P, _P, _P]),
+    "ouro_tpraos_plan_destroy": (None, [_P]),
 }
 
 _lib = None

@@ -9,7 +9,7 @@
 #include <cstring>
 #include <vector>
 
-#include "verify.h"
+#include "tpraos.h"
 
 using namespace ouro;
 
@@ -147,5 +147,21 @@ int dh_sum6kes_verify(const uint8_t* vk, uint32_t t, const uint8_t* m, uint32_t 
   memcpy(sw, sig, 448);
   Lane lane;
   return sum6kes_verify_lane(v, t, sw, ShaGlobalTail{m}, mlen, lane.w, host_btab()) ? 0 : -1;
+}
+// The header drivers of tpraos.h for every header of a host SoA batch.
+// mode 0 = throughput (one lane, key table shared), 1 = latency (a fresh lane
+// per core, no sharing).  Pointers must be 16-B aligned like device buffers.
+int dh_tpraos_verify(const ouro_tpraos_batch* b, int mode, uint8_t* verdict, uint8_t* beta_eta,
+                     uint8_t* beta_leader) {
+  std::vector<Lane> lanes(kHdrCores);
+  std::vector<int32_t> res(kResWords + 4);
+  int32_t* r = reinterpret_cast<int32_t*>((reinterpret_cast<uintptr_t>(res.data()) + 15) & ~uintptr_t(15));
+  for (size_t i = 0; i < b->n; i++) {
+    memset(r, 0, kResWords * sizeof(int32_t));
+    for (int core = 0; core < kHdrCores; core++)
+      hdr_core(*b, i, core, lanes[mode ? core : 0].w, r, host_btab(), mode == 0);
+    hdr_finish_item(*b, i, r, lanes[0].w, verdict, beta_eta, beta_leader);
+  }
+  return 0;
 }
 }

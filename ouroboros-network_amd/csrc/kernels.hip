@@ -14,13 +14,15 @@
 #include <vector>
 
 #include "../../include/ouro_verify.h"
-#include "verify.h"
+#include "tpraos.h"
 
 using namespace ouro;
 
 namespace {
 
 constexpr int kBlock = 256;
+// throughput header kernel: scratch slot + the per-header result record
+constexpr int kHdrLaneWords = kLaneWords + kResWords;
 
 // message bytes held in registers (the 48-byte OCertSignable); a select chain
 // keeps a dynamic byte index out of scratch
@@ -49,6 +51,7 @@ __device__ __forceinline__ void store_words(uint8_t* p, const uint32_t* w, int n
 }
 
 __device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
+
 
 }  // namespace
 
@@ -106,54 +109,61 @@ __global__ void __launch_bounds__(kBlock, 2) k_sum6kes_verify(
   }
 }
 
+// Throughput mode: one lane per header runs every core of tpraos.h, sharing
+// the VRF key decode and its table, then the single-inversion finish.
 __global__ void __launch_bounds__(kBlock, 2) k_tpraos_verify(ouro_tpraos_batch b,
-                                                          uint8_t* __restrict__ verdict,
-                                                          uint8_t* __restrict__ beta_eta,
-                                                          uint8_t* __restrict__ beta_leader,
-                                                          int32_t* scratch,
-                                                          const int32_t* __restrict__ btab) {
+                                                             uint8_t* __restrict__ verdict,
+                                                             uint8_t* __restrict__ beta_eta,
+                                                             uint8_t* __restrict__ beta_leader,
+                                                             int32_t* scratch,
+                                                             const int32_t* __restrict__ btab) {
+  const size_t tid = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const size_t nth = (size_t)gridDim.x * blockDim.x;
+  int32_t* lane = scratch + tid * kHdrLaneWords;
+  int32_t* res = lane + kLaneWords;
+  for (size_t i = tid; i < b.n; i += nth) {
+    hdr_core(b, i, kCoreOcert, lane, res, btab);
+    hdr_core(b, i, kCoreKes, lane, res, btab);
+    hdr_core(b, i, kCoreUe, lane, res, btab);
+    hdr_core(b, i, kCoreUl, lane, res, btab);
+    hdr_core(b, i, kCoreVe, lane, res, btab);
+    hdr_core(b, i, kCoreVl, lane, res, btab);
+    hdr_finish_item(b, i, res, lane, verdict, beta_eta, beta_leader);
+  }
+}
+
+// Latency mode, launch 1: six lanes per header (work item w = core * n + i,
+// so each wave runs one core type), results to a per-header record.
+// n is read from device memory so a captured graph serves any n <= capacity.
+__global__ void __launch_bounds__(kBlock, 2) k_tpraos_cores(ouro_tpraos_batch b,
+                                                            const uint32_t* __restrict__ d_n,
+                                                            int32_t* res_buf, int32_t* scratch,
+                                                            const int32_t* __restrict__ btab) {
+  const size_t n = *d_n;
   const size_t tid = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   const size_t nth = (size_t)gridDim.x * blockDim.x;
   int32_t* lane = scratch + tid * kLaneWords;
-  for (size_t i = tid; i < b.n; i += nth) {
-    uint32_t v = 0;
-    // OCERT: Ed25519 by the cold key over hotVk || BE64(n) || BE64(c0)
-    {
-      uint32_t s[16], p[8];
-      load_words(s, b.ocert_sigma + 64 * i, 4);
-      load_words(p, b.issuer_vk + 32 * i, 2);
-      RegTail48 m;
-      load_words(m.w, b.hot_vk + 32 * i, 2);
-      const uint64_t ctr = b.ocert_counter[i], c0 = b.ocert_kes_period[i];
-      m.w[8] = bswap32((uint32_t)(ctr >> 32));
-      m.w[9] = bswap32((uint32_t)ctr);
-      m.w[10] = bswap32((uint32_t)(c0 >> 32));
-      m.w[11] = bswap32((uint32_t)c0);
-      if (ed25519_verify_lane(s, p, m, 48, lane, btab)) v |= OURO_HDR_OCERT_OK;
-    }
-    // OCERT: Sum6KES by the hot key over the raw header body
-    {
-      uint32_t hv[8];
-      load_words(hv, b.hot_vk + 32 * i, 2);
-      const uint32_t* sw = reinterpret_cast<const uint32_t*>(b.kes_sig + 448 * i);
-      if (sum6kes_verify_lane(hv, b.kes_t[i], sw, ShaGlobalTail{b.body + b.body_off[i]},
-                              b.body_len[i], lane, btab))
-        v |= OURO_HDR_KES_OK;
-    }
-    // OVERLAY: the two VRF certificates under the same VRF key
-#pragma unroll 1
-    for (int which = 0; which < 2; which++) {
-      uint32_t p[8], pi[20], out[16];
-      load_words(p, b.vrf_vk + 32 * i, 2);
-      load_words(pi, (which ? b.leader_proof : b.eta_proof) + 80 * i, 5);
-      const uint8_t* a = (which ? b.leader_alpha : b.eta_alpha) + 32 * i;
-      const bool ok = vrf03_verify_lane(out, p, pi, ShaGlobalTail{a}, 32, lane, btab);
-      uint8_t* dst = which ? beta_leader : beta_eta;
-      if (dst) store_words(dst + 64 * i, out, 4);
-      if (ok) v |= which ? OURO_HDR_VRF_LEADER_OK : OURO_HDR_VRF_ETA_OK;
-    }
-    verdict[i] = (uint8_t)v;
+  for (size_t w = tid; w < (size_t)kHdrCores * n; w += nth) {
+    const int core = (int)(w / n);
+    const size_t i = w - (size_t)core * n;
+    hdr_core(b, i, core, lane, res_buf + i * kResWords, btab, /*share_key=*/false);
   }
+}
+
+// Latency mode, launch 2: the shared-inversion finish, one lane per header.
+__global__ void __launch_bounds__(kBlock, 2) k_tpraos_finish(ouro_tpraos_batch b,
+                                                             const uint32_t* __restrict__ d_n,
+                                                             const int32_t* res_buf,
+                                                             uint8_t* __restrict__ verdict,
+                                                             uint8_t* __restrict__ beta_eta,
+                                                             uint8_t* __restrict__ beta_leader,
+                                                             int32_t* scratch) {
+  const size_t n = *d_n;
+  const size_t tid = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const size_t nth = (size_t)gridDim.x * blockDim.x;
+  int32_t* lane = scratch + tid * kLaneWords;
+  for (size_t i = tid; i < n; i += nth)
+    hdr_finish_item(b, i, res_buf + i * kResWords, lane, verdict, beta_eta, beta_leader);
 }
 
 // proof_to_hash only (no verification): beta = H(0x04 || 0x03 || [8]Gamma)
@@ -213,13 +223,14 @@ struct DeviceState {
   std::string err_msg;
   int32_t* btab = nullptr;
   int cus = 0;
-  int max_blocks[8] = {0};  // per kernel id
+  int max_blocks[8] = {0};  // per KernelId (kNumKernels <= 8)
 };
 
 std::mutex g_dev_mu;
 std::map<int, DeviceState> g_dev;
 
-enum KernelId { kEd = 0, kVrf = 1, kKes = 2, kHdr = 3, kP2H = 4 };
+enum KernelId { kEd = 0, kVrf = 1, kKes = 2, kHdr = 3, kP2H = 4, kCores = 5, kFinish = 6,
+                kNumKernels = 7 };
 
 const void* kernel_ptr(int id) {
   switch (id) {
@@ -227,6 +238,8 @@ const void* kernel_ptr(int id) {
     case kVrf: return reinterpret_cast<const void*>(&k_vrf03_verify);
     case kKes: return reinterpret_cast<const void*>(&k_sum6kes_verify);
     case kHdr: return reinterpret_cast<const void*>(&k_tpraos_verify);
+    case kCores: return reinterpret_cast<const void*>(&k_tpraos_cores);
+    case kFinish: return reinterpret_cast<const void*>(&k_tpraos_finish);
     default: return reinterpret_cast<const void*>(&k_vrf03_proof_to_hash);
   }
 }
@@ -258,7 +271,7 @@ int device_state(DeviceState** out) {
     build_btab(tab.data());
     OURO_HIP(hipMalloc(&s.btab, sizeof(int32_t) * kBTabWords));
     OURO_HIP(hipMemcpy(s.btab, tab.data(), sizeof(int32_t) * kBTabWords, hipMemcpyHostToDevice));
-    for (int id = 0; id < 5; id++) {
+    for (int id = 0; id < kNumKernels; id++) {
       int per_cu = 0;
       OURO_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel_ptr(id), kBlock, 0));
       s.max_blocks[id] = std::max(1, per_cu) * s.cus;
@@ -309,13 +322,14 @@ int thread_stream(hipStream_t* s) {
 }
 
 // grid for n items of kernel `id`; returns the scratch slot count
-int plan(DeviceState* ds, int id, size_t n, hipStream_t stream, int* grid, int32_t** scratch) {
+int plan(DeviceState* ds, int id, size_t n, hipStream_t stream, int* grid, int32_t** scratch,
+         int lane_words = kLaneWords) {
   size_t blocks = (n + kBlock - 1) / kBlock;
   blocks = std::max<size_t>(1, std::min<size_t>(blocks, (size_t)ds->max_blocks[id]));
   *grid = (int)blocks;
   if (scratch) {
     Buf& b = t_ctx.scratch[stream];
-    int rc = ensure(b, blocks * kBlock * sizeof(int32_t) * kLaneWords);
+    int rc = ensure(b, blocks * kBlock * sizeof(int32_t) * lane_words);
     if (rc) return rc;
     *scratch = static_cast<int32_t*>(b.p);
   }
@@ -375,10 +389,35 @@ int launch_hdr(hipStream_t st, const ouro_tpraos_batch& b, uint8_t* verdict, uin
   if (rc) return rc;
   int grid;
   int32_t* scr;
-  if ((rc = plan(ds, kHdr, b.n, st, &grid, &scr))) return rc;
+  if ((rc = plan(ds, kHdr, b.n, st, &grid, &scr, kHdrLaneWords))) return rc;
   hipLaunchKernelGGL(k_tpraos_verify, dim3(grid), dim3(kBlock), 0, st, b, verdict, be, bl, scr,
                      ds->btab);
   return launch_check();
+}
+
+// latency mode: six lanes per header, then the finish; n read from d_n
+int launch_lowlat(hipStream_t st, const ouro_tpraos_batch& b, const uint32_t* d_n, size_t n_cap,
+                  int32_t* res_buf, int32_t* scratch, uint8_t* verdict, uint8_t* be,
+                  uint8_t* bl) {
+  DeviceState* ds;
+  int rc = device_state(&ds);
+  if (rc) return rc;
+  int g1, g2;
+  if ((rc = plan(ds, kCores, (size_t)kHdrCores * n_cap, st, &g1, nullptr))) return rc;
+  if ((rc = plan(ds, kFinish, n_cap, st, &g2, nullptr))) return rc;
+  hipLaunchKernelGGL(k_tpraos_cores, dim3(g1), dim3(kBlock), 0, st, b, d_n, res_buf, scratch,
+                     ds->btab);
+  if ((rc = launch_check())) return rc;
+  hipLaunchKernelGGL(k_tpraos_finish, dim3(g2), dim3(kBlock), 0, st, b, d_n, res_buf, verdict, be,
+                     bl, scratch);
+  return launch_check();
+}
+
+size_t lowlat_scratch_words(DeviceState* ds, size_t n_cap) {
+  size_t b1 = std::min<size_t>(((size_t)kHdrCores * n_cap + kBlock - 1) / kBlock,
+                               (size_t)ds->max_blocks[kCores]);
+  size_t b2 = std::min<size_t>((n_cap + kBlock - 1) / kBlock, (size_t)ds->max_blocks[kFinish]);
+  return std::max<size_t>(1, std::max(b1, b2)) * kBlock * kLaneWords;
 }
 
 // ---- host-buffer staging ----
@@ -669,5 +708,200 @@ int ouro_tpraos_verify_batch_device(void* stream, const ouro_tpraos_batch* b, ui
   hipStream_t st = static_cast<hipStream_t>(stream);  // NULL = HIP's default stream
   return launch_hdr(st, *b, verdict, beta_eta, beta_leader);
 }
+
+// ---- latency mode (ChainSync windows) ----
+int ouro_tpraos_verify_batch_lowlat(const ouro_tpraos_batch* b, uint8_t* verdict,
+                                    uint8_t* beta_eta, uint8_t* beta_leader) {
+  if (!b) return fail(OURO_EINVAL, "null batch");
+  const size_t n = b->n;
+  if (n == 0) return OURO_OK;
+  if (n > 0xffffffffu) return fail(OURO_EINVAL, "batch too large");
+  if (!b->issuer_vk || !b->vrf_vk || !b->eta_proof || !b->leader_proof || !b->eta_alpha ||
+      !b->leader_alpha || !b->hot_vk || !b->ocert_counter || !b->ocert_kes_period ||
+      !b->ocert_sigma || !b->kes_t || !b->kes_sig || !b->body_off || !b->body_len || !verdict)
+    return fail(OURO_EINVAL, "null argument");
+  hipStream_t st;
+  int rc = thread_stream(&st);
+  if (rc) return rc;
+  DeviceState* ds;
+  if ((rc = device_state(&ds))) return rc;
+  const size_t span = span_of(n, b->body_off, b->body_len);
+  if (span && !b->body) return fail(OURO_EINVAL, "null body buffer");
+  Stager sg{st};
+  ouro_tpraos_batch d;
+  d.n = n;
+  d.issuer_vk = sg.up(b->issuer_vk, 32 * n);
+  d.vrf_vk = sg.up(b->vrf_vk, 32 * n);
+  d.eta_proof = sg.up(b->eta_proof, 80 * n);
+  d.leader_proof = sg.up(b->leader_proof, 80 * n);
+  d.eta_alpha = sg.up(b->eta_alpha, 32 * n);
+  d.leader_alpha = sg.up(b->leader_alpha, 32 * n);
+  d.hot_vk = sg.up(b->hot_vk, 32 * n);
+  d.ocert_counter = sg.up(b->ocert_counter, n);
+  d.ocert_kes_period = sg.up(b->ocert_kes_period, n);
+  d.ocert_sigma = sg.up(b->ocert_sigma, 64 * n);
+  d.kes_t = sg.up(b->kes_t, n);
+  d.kes_sig = sg.up(b->kes_sig, 448 * n);
+  d.body = sg.up(b->body, span);
+  d.body_off = sg.up(b->body_off, n);
+  d.body_len = sg.up(b->body_len, n);
+  const uint32_t n32 = (uint32_t)n;
+  const uint32_t* d_n = sg.up(&n32, 1);
+  int32_t* res = sg.out<int32_t>(n * kResWords);
+  int32_t* scr = sg.out<int32_t>(lowlat_scratch_words(ds, n));
+  uint8_t* dver = sg.out<uint8_t>(n);
+  uint8_t* dbe = sg.out<uint8_t>(64 * n);
+  uint8_t* dbl = sg.out<uint8_t>(64 * n);
+  if (sg.rc) return sg.rc;
+  if ((rc = launch_lowlat(st, d, d_n, n, res, scr, dver, dbe, dbl))) return rc;
+  std::vector<uint8_t> tv(n), te(beta_eta ? 64 * n : 0), tl(beta_leader ? 64 * n : 0);
+  if ((rc = download(st, tv.data(), dver, n))) return rc;
+  if (beta_eta && (rc = download(st, te.data(), dbe, 64 * n))) return rc;
+  if (beta_leader && (rc = download(st, tl.data(), dbl, 64 * n))) return rc;
+  if ((rc = finish(st))) return rc;
+  memcpy(verdict, tv.data(), n);
+  if (beta_eta) memcpy(beta_eta, te.data(), 64 * n);
+  if (beta_leader) memcpy(beta_leader, tl.data(), 64 * n);
+  return OURO_OK;
+}
+
+}  // extern "C"
+
+// ---- captured plans: pinned staging + hipGraph (H2D, 2 kernels, D2H) --------
+struct ouro_tpraos_plan {
+  int dev = -1;
+  size_t cap = 0, body_cap = 0;
+  hipStream_t st = nullptr;
+  hipGraph_t graph = nullptr;
+  hipGraphExec_t exec = nullptr;
+  uint8_t *h_in = nullptr, *d_in = nullptr, *h_out = nullptr, *d_out = nullptr;
+  size_t in_bytes = 0, out_bytes = 0;
+  int32_t *res = nullptr, *scratch = nullptr;
+  size_t off[16] = {0};  // byte offsets of the 15 fields + n in the packed input block
+  ouro_tpraos_batch dev_batch{};
+};
+
+namespace {
+constexpr size_t align16(size_t x) { return (x + 15) & ~(size_t)15; }
+// widths (bytes per header) of the 15 SoA fields, in ouro_tpraos_batch order;
+// 0 marks the body (capacity-sized)
+constexpr size_t kFieldBytes[15] = {32, 32, 80, 80, 32, 32, 32, 8, 8, 64, 4, 448, 0, 8, 4};
+
+void plan_free(ouro_tpraos_plan* p) {
+  if (!p) return;
+  if (p->exec) (void)hipGraphExecDestroy(p->exec);
+  if (p->graph) (void)hipGraphDestroy(p->graph);
+  if (p->h_in) (void)hipHostFree(p->h_in);
+  if (p->h_out) (void)hipHostFree(p->h_out);
+  if (p->d_in) (void)hipFree(p->d_in);
+  if (p->d_out) (void)hipFree(p->d_out);
+  if (p->res) (void)hipFree(p->res);
+  if (p->scratch) (void)hipFree(p->scratch);
+  if (p->st) (void)hipStreamDestroy(p->st);
+  delete p;
+}
+
+int plan_build(ouro_tpraos_plan* p) {
+  DeviceState* ds;
+  int rc = device_state(&ds);
+  if (rc) return rc;
+  if ((rc = current_device(&p->dev))) return rc;
+  OURO_HIP(hipStreamCreateWithFlags(&p->st, hipStreamNonBlocking));
+  size_t o = 16;  // n lives in the first 16 bytes
+  for (int f = 0; f < 15; f++) {
+    p->off[f] = o;
+    o += align16(kFieldBytes[f] ? kFieldBytes[f] * p->cap : p->body_cap);
+  }
+  p->in_bytes = o;
+  p->out_bytes = align16(p->cap) + 128 * p->cap;
+  OURO_HIP(hipHostMalloc(&p->h_in, p->in_bytes, hipHostMallocDefault));
+  OURO_HIP(hipHostMalloc(&p->h_out, p->out_bytes, hipHostMallocDefault));
+  OURO_HIP(hipMalloc(&p->d_in, p->in_bytes));
+  OURO_HIP(hipMalloc(&p->d_out, p->out_bytes));
+  OURO_HIP(hipMalloc(&p->res, sizeof(int32_t) * kResWords * p->cap));
+  OURO_HIP(hipMalloc(&p->scratch, sizeof(int32_t) * lowlat_scratch_words(ds, p->cap)));
+  memset(p->h_in, 0, p->in_bytes);
+  uint8_t* d = p->d_in;
+  ouro_tpraos_batch& b = p->dev_batch;
+  b.n = p->cap;
+  b.issuer_vk = d + p->off[0];
+  b.vrf_vk = d + p->off[1];
+  b.eta_proof = d + p->off[2];
+  b.leader_proof = d + p->off[3];
+  b.eta_alpha = d + p->off[4];
+  b.leader_alpha = d + p->off[5];
+  b.hot_vk = d + p->off[6];
+  b.ocert_counter = reinterpret_cast<const uint64_t*>(d + p->off[7]);
+  b.ocert_kes_period = reinterpret_cast<const uint64_t*>(d + p->off[8]);
+  b.ocert_sigma = d + p->off[9];
+  b.kes_t = reinterpret_cast<const uint32_t*>(d + p->off[10]);
+  b.kes_sig = d + p->off[11];
+  b.body = d + p->off[12];
+  b.body_off = reinterpret_cast<const uint64_t*>(d + p->off[13]);
+  b.body_len = reinterpret_cast<const uint32_t*>(d + p->off[14]);
+  uint8_t* dver = p->d_out;
+  uint8_t* dbe = dver + align16(p->cap);
+  uint8_t* dbl = dbe + 64 * p->cap;
+  OURO_HIP(hipStreamBeginCapture(p->st, hipStreamCaptureModeThreadLocal));
+  OURO_HIP(hipMemcpyAsync(p->d_in, p->h_in, p->in_bytes, hipMemcpyHostToDevice, p->st));
+  rc = launch_lowlat(p->st, b, reinterpret_cast<const uint32_t*>(p->d_in), p->cap, p->res,
+                     p->scratch, dver, dbe, dbl);
+  if (rc) {
+    hipGraph_t g;
+    (void)hipStreamEndCapture(p->st, &g);
+    return rc;
+  }
+  OURO_HIP(hipMemcpyAsync(p->h_out, p->d_out, p->out_bytes, hipMemcpyDeviceToHost, p->st));
+  OURO_HIP(hipStreamEndCapture(p->st, &p->graph));
+  OURO_HIP(hipGraphInstantiate(&p->exec, p->graph, nullptr, nullptr, 0));
+  return OURO_OK;
+}
+}  // namespace
+
+extern "C" {
+
+ouro_tpraos_plan* ouro_tpraos_plan_create(size_t max_headers, size_t max_body_bytes) {
+  if (max_headers == 0 || max_headers > 0xffffffffu) {
+    fail(OURO_EINVAL, "bad plan size");
+    return nullptr;
+  }
+  auto* p = new ouro_tpraos_plan;
+  p->cap = max_headers;
+  p->body_cap = std::max<size_t>(max_body_bytes, 16);
+  if (plan_build(p) != OURO_OK) {
+    plan_free(p);
+    return nullptr;
+  }
+  return p;
+}
+
+int ouro_tpraos_plan_run(ouro_tpraos_plan* p, const ouro_tpraos_batch* b, uint8_t* verdict,
+                         uint8_t* beta_eta, uint8_t* beta_leader) {
+  if (!p || !b || !verdict) return fail(OURO_EINVAL, "null argument");
+  const size_t n = b->n;
+  if (n == 0) return OURO_OK;
+  if (n > p->cap) return fail(OURO_EINVAL, "batch larger than the plan");
+  const size_t span = span_of(n, b->body_off, b->body_len);
+  if (span > p->body_cap) return fail(OURO_EINVAL, "body bytes exceed the plan");
+  const void* src[15] = {b->issuer_vk, b->vrf_vk, b->eta_proof, b->leader_proof, b->eta_alpha,
+                         b->leader_alpha, b->hot_vk, b->ocert_counter, b->ocert_kes_period,
+                         b->ocert_sigma, b->kes_t, b->kes_sig, b->body, b->body_off, b->body_len};
+  for (int f = 0; f < 15; f++) {
+    const size_t bytes = kFieldBytes[f] ? kFieldBytes[f] * n : span;
+    if (bytes && !src[f]) return fail(OURO_EINVAL, "null field");
+    if (bytes) memcpy(p->h_in + p->off[f], src[f], bytes);
+  }
+  const uint32_t n32 = (uint32_t)n;
+  memcpy(p->h_in, &n32, sizeof n32);
+  OURO_HIP(hipSetDevice(p->dev));
+  OURO_HIP(hipGraphLaunch(p->exec, p->st));
+  OURO_HIP(hipStreamSynchronize(p->st));
+  memcpy(verdict, p->h_out, n);
+  if (beta_eta) memcpy(beta_eta, p->h_out + align16(p->cap), 64 * n);
+  if (beta_leader) memcpy(beta_leader, p->h_out + align16(p->cap) + 64 * p->cap, 64 * n);
+  return OURO_OK;
+}
+
+void ouro_tpraos_plan_destroy(ouro_tpraos_plan* p) { plan_free(p); }
 
 }  // extern "C"

@@ -1,0 +1,322 @@
+// tpraos.h -- the TPraos header combiner as phases.
+//
+// The crypto subset of SL.updateChainDepState reached from
+// ouroboros-consensus-shelley/src/Ouroboros/Consensus/Shelley/Protocol.hs:433-442:
+//   OCERT   : Ed25519 by the cold key over hotVk || BE64(n) || BE64(c0),
+//             Sum6KES by hotVk over the raw header body
+//   OVERLAY : draft-03 VRF verify + output for the eta and leader seeds
+// Each check is split into a *core* that ends in projective points and one
+// shared *finish* that inverts all ten Z coordinates with a single field
+// inversion (Montgomery's trick) and then does every encoding, comparison and
+// hash.  The cores are independent, so the same code runs
+//   * throughput mode: one lane runs all six cores of a header, the VRF key is
+//     decoded once and its [1..8](-Y) table serves both U computations;
+//   * latency mode (64-header ChainSync windows): six lanes per header run the
+//     cores concurrently, a second launch finishes.
+// Verdicts and outputs are identical in both modes (tests pin both against
+// the oracle).
+#pragma once
+#include "verify.h"
+#include "../../include/ouro_verify.h"
+
+namespace ouro {
+
+// ---- per-header result record (int32 words) --------------------------------
+enum HdrPoint { kPtR1 = 0, kPtR2, kPtHe, kPtUe, kPtVe, kPtG8e, kPtHl, kPtUl, kPtVl, kPtG8l,
+                kHdrPoints };
+constexpr int kPtWords = 36;                          // X, Y, Z at a 12-word stride
+constexpr int kResFlags = kHdrPoints * kPtWords;      // 6 flag words, one per core
+constexpr int kResWords = kResFlags + 8;              // 368 words (16-B multiple)
+enum HdrCore { kCoreOcert = 0, kCoreKes, kCoreUe, kCoreUl, kCoreVe, kCoreVl, kHdrCores };
+// flag bits
+constexpr int32_t kFlagOk = 1;        // the core's acceptance checks passed
+constexpr int32_t kFlagGammaX0 = 2;   // Gamma decoded with x = 0 (re-encodes with sign 0)
+
+OURO_FI void st_point(int32_t* res, int which, const fe& X, const fe& Y, const fe& Z) {
+  int32_t* p = res + which * kPtWords;
+  st_fe(p, X);
+  st_fe(p + 12, Y);
+  st_fe(p + 24, Z);
+}
+OURO_FI void st_point_from_dsm(int32_t* res, int which, const int32_t* lane) {
+  const ge_p2 r = dsm_result(lane);
+  st_point(res, which, r.X, r.Y, r.Z);
+}
+
+// ---- cores ---------------------------------------------------------------
+// OCERT signature: message hotVk || BE64(counter) || BE64(c0) in registers
+struct OcertMsg {
+  uint32_t w[12];
+  OURO_FI uint32_t tail(uint32_t q) const {
+    uint32_t r = w[0];
+#pragma unroll
+    for (int i = 1; i < 12; i++) r = ((q >> 2) == (uint32_t)i) ? w[i] : r;
+    return (r >> (8 * (q & 3))) & 0xffu;
+  }
+};
+
+OURO_FI uint32_t bswap32_hd(uint32_t x) {
+  return (x >> 24) | ((x >> 8) & 0xff00u) | ((x << 8) & 0xff0000u) | (x << 24);
+}
+
+OURO_HD inline void ocert_msg(OcertMsg& m, const uint32_t hot_vk[8], uint64_t ctr, uint64_t c0) {
+#pragma unroll
+  for (int i = 0; i < 8; i++) m.w[i] = hot_vk[i];
+  m.w[8] = bswap32_hd((uint32_t)(ctr >> 32));
+  m.w[9] = bswap32_hd((uint32_t)ctr);
+  m.w[10] = bswap32_hd((uint32_t)(c0 >> 32));
+  m.w[11] = bswap32_hd((uint32_t)c0);
+}
+
+// U = [s]B - [c]Y.  With build_y the key is validated/decoded and its [1..8](-Y)
+// table written to table slot `yslot`; otherwise a previous call's table is
+// reused (throughput mode: both VRFs of a header share the key).
+OURO_HD inline bool vrf_u_core(const uint32_t pk[8], const uint32_t pi[20], bool build_y,
+                               int yslot, int32_t* lane, const int32_t* btab) {
+  bool ok = true;
+  if (build_y) {
+    ge_p3 Y;
+    ok = !ge_has_small_order(pk) && ge_is_canonical(pk);
+    ok = ge_decode(&Y, pk, false) && ok;
+    build_table(lane + yslot * kTabWords, ge_p3_neg(Y));
+  }
+  uint32_t c[8], s_raw[8], s[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    s_raw[i] = pi[12 + i];
+    c[i] = i < 4 ? pi[8 + i] : 0u;
+  }
+  sc_reduce256(s, s_raw);
+  st_words8(lane + kSlotA1, c);
+  st_words8(lane + kSlotB, s);
+  uint64_t* carr = reinterpret_cast<uint64_t*>(lane + kSlotCarry);
+  carr[0] = sc_recode_carries<4, 33>(c);
+  carr[2] = sc_recode_carries<8, 32>(s);
+  dsm(lane, btab, dsm_cfg(33, 0, true, true, yslot, 1));
+  return ok;
+}
+
+// Gamma checks, H = hash_to_curve(Y, alpha), V = [s]H - [c]Gamma, [8]Gamma.
+// Writes H, V, [8]Gamma into res; returns the flag word.
+template <class Tail>
+OURO_HD inline int32_t vrf_v_core(const uint32_t pk[8], const uint32_t pi[20], const Tail& alpha,
+                                  uint32_t alen, int32_t* lane, const int32_t* btab,
+                                  int32_t* res, int ptH, int ptV, int ptG8) {
+  uint32_t G[8], c[8], s_raw[8], s[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    G[i] = pi[i];
+    s_raw[i] = pi[12 + i];
+    c[i] = i < 4 ? pi[8 + i] : 0u;
+  }
+  ge_p3 Gamma;
+  bool ok = ge_is_canonical(G);
+  ok = ge_decode(&Gamma, G, false) && ok;
+  sc_reduce256(s, s_raw);
+  uint32_t pre[9];
+  pre[0] = 0x04u | (0x01u << 8) | (pk[0] << 16);
+#pragma unroll
+  for (int i = 1; i < 8; i++) pre[i] = (pk[i - 1] >> 16) | (pk[i] << 16);
+  pre[8] = pk[7] >> 16;
+  uint64_t Hs[8];
+  sha512_prefixed<34>(Hs, pre, alpha, alen);
+  uint32_t rw[16];
+  sha512_digest_words(rw, Hs);
+  rw[7] &= 0x7fffffffu;
+  ge_p3 Hp = elligator2_h(rw);
+  st_point(res, ptH, Hp.X, Hp.Y, Hp.Z);
+  build_table(lane + kSlotTab1, Hp);
+  build_table(lane + kSlotTab2, ge_p3_neg(Gamma));
+  st_words8(lane + kSlotA1, s);
+  st_words8(lane + kSlotA2, c);
+  uint64_t* carr = reinterpret_cast<uint64_t*>(lane + kSlotCarry);
+  carr[0] = sc_recode_carries<4, 64>(s);
+  carr[1] = sc_recode_carries<4, 33>(c);
+  dsm(lane, btab, dsm_cfg(64, 33, false, false, 0, 1));
+  st_point_from_dsm(res, ptV, lane);
+  ge_p3 G8 = ge_mul8(Gamma);
+  st_point(res, ptG8, G8.X, G8.Y, G8.Z);
+  return (ok ? kFlagOk : 0) | (fe_iszero(Gamma.X) ? kFlagGammaX0 : 0);
+}
+
+// ---- finish ----------------------------------------------------------------
+OURO_FI void pack_shifted(uint32_t* dst, int word0, const uint32_t p[8]) {
+  // append 32 bytes at byte offset 4*word0 - 2 (the 2-byte suite/tag prefix
+  // shifts every point by 2 bytes); caller seeds dst[word0 - 1] high half
+  dst[word0 - 1] |= p[0] << 16;
+#pragma unroll
+  for (int i = 1; i < 8; i++) dst[word0 - 1 + i] = (p[i - 1] >> 16) | (p[i] << 16);
+  dst[word0 + 7] = p[7] >> 16;
+}
+
+// c' check and beta for one VRF; H/U/V/G8 encodings given
+OURO_HD inline bool vrf_finish(uint32_t beta[16], const uint32_t Henc[8], const uint32_t Genc[8],
+                               const uint32_t Uenc[8], const uint32_t Venc[8],
+                               const uint32_t G8enc[8], const uint32_t c[4]) {
+  uint32_t hp[33];
+  hp[0] = 0x04u | (0x02u << 8);
+  pack_shifted(hp, 1, Henc);
+  pack_shifted(hp, 9, Genc);
+  pack_shifted(hp, 17, Uenc);
+  pack_shifted(hp, 25, Venc);
+  uint64_t Hc[8];
+  sha512_prefixed<130>(Hc, hp, ShaNoTail{}, 0);
+  uint32_t cw[16];
+  sha512_digest_words(cw, Hc);
+  bool ceq = true;
+#pragma unroll
+  for (int i = 0; i < 4; i++) ceq = ceq && cw[i] == c[i];
+  uint32_t bp[9];
+  bp[0] = 0x04u | (0x03u << 8);
+  pack_shifted(bp, 1, G8enc);
+  uint64_t Hb[8];
+  sha512_prefixed<34>(Hb, bp, ShaNoTail{}, 0);
+  sha512_digest_words(beta, Hb);
+  return ceq;
+}
+
+// One inversion for all ten Z; tmp = 10 x 12 scratch words.  Then every
+// comparison and hash.  Returns the OURO_HDR_* verdict bits.
+OURO_HD inline uint32_t hdr_finish(const int32_t* res, int32_t* tmp, const uint32_t R1[8],
+                                   const uint32_t R2[8], const uint32_t pie[20],
+                                   const uint32_t pil[20], uint32_t beta_e[16],
+                                   uint32_t beta_l[16]) {
+  // prefix products P_k = Z_0 ... Z_k
+  fe acc = ld_fe(res + 24);
+  st_fe(tmp, acc);
+#pragma unroll 1
+  for (int k = 1; k < kHdrPoints; k++) {
+    acc = fe_mul(acc, ld_fe(res + k * kPtWords + 24));
+    st_fe(tmp + 12 * k, acc);
+  }
+  fe inv = fe_invert(acc);
+  // walk back: Z_k^-1 = inv * P_{k-1}, inv <- inv * Z_k
+#pragma unroll 1
+  for (int k = kHdrPoints - 1; k > 0; k--) {
+    const fe zk = ld_fe(res + k * kPtWords + 24);
+    st_fe(tmp + 12 * k, fe_mul(inv, ld_fe(tmp + 12 * (k - 1))));
+    inv = fe_mul(inv, zk);
+  }
+  st_fe(tmp, inv);
+  uint32_t enc[kHdrPoints][8];
+#pragma unroll
+  for (int k = 0; k < kHdrPoints; k++)
+    ge_encode_with_inv(enc[k], ld_fe(res + k * kPtWords), ld_fe(res + k * kPtWords + 12),
+                       ld_fe(tmp + 12 * k));
+  const int32_t* fl = res + kResFlags;
+  uint32_t v = 0;
+  bool e1 = true, e2 = true;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    e1 = e1 && enc[kPtR1][i] == R1[i];
+    e2 = e2 && enc[kPtR2][i] == R2[i];
+  }
+  if ((fl[kCoreOcert] & kFlagOk) && e1) v |= 0x01u;
+  if ((fl[kCoreKes] & kFlagOk) && e2) v |= 0x02u;
+#pragma unroll 1
+  for (int which = 0; which < 2; which++) {
+    const uint32_t* pi = which ? pil : pie;
+    const int base = which ? kPtHl : kPtHe;
+    const int32_t fu = fl[which ? kCoreUl : kCoreUe], fv = fl[which ? kCoreVl : kCoreVe];
+    uint32_t Genc[8], c[4], b[16];
+#pragma unroll
+    for (int i = 0; i < 8; i++) Genc[i] = pi[i];
+    if (fv & kFlagGammaX0) Genc[7] &= 0x7fffffffu;
+#pragma unroll
+    for (int i = 0; i < 4; i++) c[i] = pi[8 + i];
+    const bool ceq = vrf_finish(b, enc[base], Genc, enc[base + 1], enc[base + 2], enc[base + 3], c);
+    const bool ok = (fu & kFlagOk) && (fv & kFlagOk) && ceq;
+    uint32_t* dst = which ? beta_l : beta_e;
+#pragma unroll
+    for (int i = 0; i < 16; i++) dst[i] = ok ? b[i] : 0u;
+    if (ok) v |= which ? 0x08u : 0x04u;
+  }
+  return v;
+}
+
+// ---- per-header drivers (the kernels' bodies; host-testable) -------------
+OURO_FI void ld_words(uint32_t* w, const uint8_t* p, int n16) {
+  const uint4* q = reinterpret_cast<const uint4*>(p);
+#pragma unroll
+  for (int i = 0; i < n16; i++) {
+    uint4 v = q[i];
+    w[4 * i] = v.x; w[4 * i + 1] = v.y; w[4 * i + 2] = v.z; w[4 * i + 3] = v.w;
+  }
+}
+OURO_FI void st_words(uint8_t* p, const uint32_t* w, int n16) {
+  uint4* q = reinterpret_cast<uint4*>(p);
+#pragma unroll
+  for (int i = 0; i < n16; i++) q[i] = make_uint4(w[4 * i], w[4 * i + 1], w[4 * i + 2], w[4 * i + 3]);
+}
+
+// One core of header i (tpraos.h); throughput mode reuses the VRF key table
+// built by the eta U core (table slot 2) for the leader U core.
+OURO_HD inline void hdr_core(const ouro_tpraos_batch& b, size_t i, int core,
+                                         int32_t* lane, int32_t* res, const int32_t* btab,
+                                         bool share_key = true) {
+  int32_t flag = 0;
+  switch (core) {
+    case kCoreOcert: {
+      uint32_t s[16], p[8], hv[8];
+      ld_words(s, b.ocert_sigma + 64 * i, 4);
+      ld_words(p, b.issuer_vk + 32 * i, 2);
+      ld_words(hv, b.hot_vk + 32 * i, 2);
+      OcertMsg m;
+      ocert_msg(m, hv, b.ocert_counter[i], b.ocert_kes_period[i]);
+      flag = ed25519_core(s, p, m, 48, lane, btab) ? kFlagOk : 0;
+      st_point_from_dsm(res, kPtR1, lane);
+      break;
+    }
+    case kCoreKes: {
+      uint32_t hv[8];
+      ld_words(hv, b.hot_vk + 32 * i, 2);
+      const uint32_t* sw = reinterpret_cast<const uint32_t*>(b.kes_sig + 448 * i);
+      flag = sum6kes_core(hv, b.kes_t[i], sw, ShaGlobalTail{b.body + b.body_off[i]},
+                          b.body_len[i], lane, btab) ? kFlagOk : 0;
+      st_point_from_dsm(res, kPtR2, lane);
+      break;
+    }
+    case kCoreUe:
+    case kCoreUl: {
+      const bool leader = core == kCoreUl;
+      uint32_t p[8], pi[20];
+      ld_words(p, b.vrf_vk + 32 * i, 2);
+      ld_words(pi, (leader ? b.leader_proof : b.eta_proof) + 80 * i, 5);
+      const bool build = !(share_key && leader);
+      const bool ok = vrf_u_core(p, pi, build, 2, lane, btab);
+      flag = build ? (ok ? kFlagOk : 0) : (res[kResFlags + kCoreUe] & kFlagOk);
+      st_point_from_dsm(res, leader ? kPtUl : kPtUe, lane);
+      break;
+    }
+    default: {  // kCoreVe / kCoreVl
+      const bool leader = core == kCoreVl;
+      uint32_t p[8], pi[20];
+      ld_words(p, b.vrf_vk + 32 * i, 2);
+      ld_words(pi, (leader ? b.leader_proof : b.eta_proof) + 80 * i, 5);
+      const uint8_t* a = (leader ? b.leader_alpha : b.eta_alpha) + 32 * i;
+      flag = vrf_v_core(p, pi, ShaGlobalTail{a}, 32, lane, btab, res,
+                        leader ? kPtHl : kPtHe, leader ? kPtVl : kPtVe,
+                        leader ? kPtG8l : kPtG8e);
+      break;
+    }
+  }
+  res[kResFlags + core] = flag;
+}
+
+OURO_HD inline void hdr_finish_item(const ouro_tpraos_batch& b, size_t i,
+                                                const int32_t* res, int32_t* tmp,
+                                                uint8_t* verdict, uint8_t* beta_eta,
+                                                uint8_t* beta_leader) {
+  uint32_t R1[8], R2[8], pie[20], pil[20], be[16], bl[16];
+  ld_words(R1, b.ocert_sigma + 64 * i, 2);
+  ld_words(R2, b.kes_sig + 448 * i, 2);
+  ld_words(pie, b.eta_proof + 80 * i, 5);
+  ld_words(pil, b.leader_proof + 80 * i, 5);
+  const uint32_t v = hdr_finish(res, tmp, R1, R2, pie, pil, be, bl);
+  if (beta_eta) st_words(beta_eta + 64 * i, be, 4);
+  if (beta_leader) st_words(beta_leader + 64 * i, bl, 4);
+  verdict[i] = (uint8_t)v;
+}
+
+
+}  // namespace ouro

@@ -28,14 +28,15 @@ namespace ouro {
 constexpr int kCachedWords = 40;                  // 4 fe
 constexpr int kTabEntries = 8;                    // [1..8]P
 constexpr int kTabWords = kTabEntries * kCachedWords;
-constexpr int kSlotTab1 = 0;
-constexpr int kSlotTab2 = kTabWords;
-constexpr int kSlotA1 = 2 * kTabWords;            // 8 words
+constexpr int kSlotTab1 = 0;                      // table slot 0
+constexpr int kSlotTab2 = kTabWords;              // table slot 1
+constexpr int kSlotTab3 = 2 * kTabWords;          // table slot 2 (header kernel: -Y)
+constexpr int kSlotA1 = 3 * kTabWords;            // 8 words
 constexpr int kSlotA2 = kSlotA1 + 8;
 constexpr int kSlotB = kSlotA2 + 8;
 constexpr int kSlotCarry = kSlotB + 8;            // 6 words (3 x u64)
 constexpr int kSlotOut = kSlotCarry + 8;          // p2 result: 3 fe at 12-word stride
-constexpr int kLaneWords = kSlotOut + 36;         // 708 words = 2832 B (16-B multiple)
+constexpr int kLaneWords = kSlotOut + 36;         // 1028 words = 4112 B (16-B multiple)
 
 constexpr int kBTabEntries = 128;                 // [1..128]B, then [1..128](2^128 B)
 constexpr int kNielsWords = 32;                   // 30 used, padded for 16-B loads
@@ -137,9 +138,11 @@ OURO_HD inline void build_table(int32_t* tab, const ge_p3& P) {
 // Reads a1/a2/b and their recoding carries from the lane slot, writes the
 // resulting p2 point to lane[kSlotOut..].  Out of line: the header kernel calls
 // it six times per item, and the loop body is the I-cache-critical code.
-constexpr uint32_t dsm_cfg(int nw1, int nw2, bool useB, bool splitB = false) {
+//      bits 20..21 / 22..23 = table slots (0..2) read for a1 / a2.
+constexpr uint32_t dsm_cfg(int nw1, int nw2, bool useB, bool splitB = false, int tab1 = 0,
+                           int tab2 = 1) {
   return (uint32_t)nw1 | ((uint32_t)nw2 << 8) | (useB ? (1u << 16) : 0u) |
-         (splitB ? (1u << 17) : 0u);
+         (splitB ? (1u << 17) : 0u) | ((uint32_t)tab1 << 20) | ((uint32_t)tab2 << 22);
 }
 
 OURO_NI void dsm(int32_t* lane, const int32_t* btab, uint32_t cfg) {
@@ -184,7 +187,8 @@ OURO_NI void dsm(int32_t* lane, const int32_t* btab, uint32_t cfg) {
       const int idx = mag > 0 ? mag - 1 : 0;
       ge_cached q;
       if (src < 2) {
-        q = ld_cached(lane + (src == 0 ? kSlotTab1 : kSlotTab2) + idx * kCachedWords);
+        const int slot = (int)((cfg >> (src == 0 ? 20 : 22)) & 3);
+        q = ld_cached(lane + slot * kTabWords + idx * kCachedWords);
       } else {
         const int base = src == 3 ? kBTabEntries : 0;
         ge_niels nq = ld_niels(btab + (base + idx) * kNielsWords);
@@ -206,10 +210,11 @@ OURO_FI ge_p2 dsm_result(const int32_t* lane) {
 
 // ---- Ed25519 ------------------------------------------------------------------
 // sig = R || S (16 words), pk (8 words), message bytes from global memory.
+// ed25519_core runs the acceptance checks and leaves R' = [h](-A) + [S]B (p2)
+// in lane[kSlotOut]; the verdict is core && encode(R') == R.
 template <class Tail>
-OURO_HD inline bool ed25519_verify_lane(const uint32_t sig[16], const uint32_t pk[8],
-                                        const Tail& msg, uint32_t mlen, int32_t* lane,
-                                        const int32_t* btab) {
+OURO_HD inline bool ed25519_core(const uint32_t sig[16], const uint32_t pk[8], const Tail& msg,
+                                 uint32_t mlen, int32_t* lane, const int32_t* btab) {
   uint32_t R[8], S[8];
 #pragma unroll
   for (int i = 0; i < 8; i++) {
@@ -240,11 +245,19 @@ OURO_HD inline bool ed25519_verify_lane(const uint32_t sig[16], const uint32_t p
   carr[0] = sc_recode_carries<4, 64>(h);
   carr[2] = sc_recode_carries<8, 32>(S);
   dsm(lane, btab, dsm_cfg(64, 0, true));
+  return ok;
+}
+
+template <class Tail>
+OURO_HD inline bool ed25519_verify_lane(const uint32_t sig[16], const uint32_t pk[8],
+                                        const Tail& msg, uint32_t mlen, int32_t* lane,
+                                        const int32_t* btab) {
+  const bool ok = ed25519_core(sig, pk, msg, mlen, lane, btab);
   uint32_t enc[8];
   ge_p2_encode(enc, dsm_result(lane));
   bool eq = true;
 #pragma unroll
-  for (int i = 0; i < 8; i++) eq = eq && enc[i] == R[i];
+  for (int i = 0; i < 8; i++) eq = eq && enc[i] == sig[i];
   return ok && eq;
 }
 
@@ -440,7 +453,7 @@ OURO_HD inline bool vrf03_verify_lane(uint32_t beta[16], const uint32_t pk[8],
 // ---- Sum6KES --------------------------------------------------------------------
 // sig (448 B) is read from global memory: leaf signature, then (vk0, vk1) for
 // levels 1..6 bottom-up; verification walks top-down from the root vk.
-template <class Tail>
+template <class Tail, bool with_compare = true>
 OURO_HD inline bool sum6kes_verify_lane(const uint32_t vk[8], uint32_t t, const uint32_t* sigw,
                                         const Tail& msg, uint32_t mlen, int32_t* lane,
                                         const int32_t* btab) {
@@ -474,8 +487,18 @@ OURO_HD inline bool sum6kes_verify_lane(const uint32_t vk[8], uint32_t t, const 
     uint4 v = s4[i];
     sig[4 * i] = v.x; sig[4 * i + 1] = v.y; sig[4 * i + 2] = v.z; sig[4 * i + 3] = v.w;
   }
+  if (!with_compare) return ed25519_core(sig, cur, msg, mlen, lane, btab) && ok;
   const bool leaf = ed25519_verify_lane(sig, cur, msg, mlen, lane, btab);
   return ok && leaf;
+}
+
+// Merkle walk + the leaf's Ed25519 core (R' left in lane[kSlotOut]); the
+// header kernel compares the encoding after its shared batch inversion.
+template <class Tail>
+OURO_HD inline bool sum6kes_core(const uint32_t vk[8], uint32_t t, const uint32_t* sigw,
+                                 const Tail& msg, uint32_t mlen, int32_t* lane,
+                                 const int32_t* btab) {
+  return sum6kes_verify_lane<Tail, false>(vk, t, sigw, msg, mlen, lane, btab);
 }
 
 // ---- fixed-base tables (host side, computed once per process) ----------------

@@ -108,6 +108,54 @@ def verify_headers(batch: HeaderBatch) -> Tuple[np.ndarray, np.ndarray, np.ndarr
     return verdict, be, bl
 
 
+def verify_headers_lowlat(batch: HeaderBatch) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
+    """Same results as verify_headers; six lanes per header (small batches)."""
+    n = len(batch)
+    verdict = np.zeros(n, dtype=np.uint8)
+    be = np.zeros((n, 64), dtype=np.uint8)
+    bl = np.zeros((n, 64), dtype=np.uint8)
+    if n:
+        s = batch.c_struct()
+        rc = _native.load().ouro_tpraos_verify_batch_lowlat(ctypes.byref(s), ptr(verdict), ptr(be),
+                                                            ptr(bl))
+        _native.check(rc, "ouro_tpraos_verify_batch_lowlat")
+    return verdict, be, bl
+
+
+class HeaderPlan:
+    """A captured hipGraph plan for repeated batches of <= max_headers
+    (the ChainSync small-batch path, BASELINE.json configs[4])."""
+
+    def __init__(self, max_headers: int = 64, max_body_bytes: int = 64 * 1400):
+        self._lib = _native.load()
+        self._p = self._lib.ouro_tpraos_plan_create(max_headers, max_body_bytes)
+        if not self._p:
+            msg = self._lib.ouro_last_error()
+            raise _native.DeviceError(f"plan create failed: {msg.decode() if msg else ''}")
+        self.max_headers = max_headers
+
+    def run(self, batch: HeaderBatch, out=None):
+        n = len(batch)
+        if out is None:
+            out = (np.zeros(n, np.uint8), np.zeros((n, 64), np.uint8), np.zeros((n, 64), np.uint8))
+        s = batch.c_struct()
+        rc = self._lib.ouro_tpraos_plan_run(self._p, ctypes.byref(s), ptr(out[0]), ptr(out[1]),
+                                            ptr(out[2]))
+        _native.check(rc, "ouro_tpraos_plan_run")
+        return out
+
+    def close(self):
+        if self._p:
+            self._lib.ouro_tpraos_plan_destroy(self._p)
+            self._p = None
+
+    def __del__(self):  # pragma: no cover - interpreter teardown order
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 def first_invalid(verdict: np.ndarray, required: int = HDR_ALL_OK) -> Optional[int]:
     """Index of the first header failing any required check -- where the
     reference's sequential HeaderStateHistory fold stops."""

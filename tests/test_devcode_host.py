@@ -140,6 +140,50 @@ def test_kes_lane_golden(dh, kats):
         assert dh.dh_sum6kes_verify(hd.hot_vk, 1, hd.body, len(hd.body), hd.kes_sig) != 0
 
 
+def _hdr_variants(kats, stride):
+    """The golden headers plus single-byte corruptions of the first one (every
+    `stride`-th byte of its body and signature region)."""
+    from ouroboros_network_amd import header as H
+
+    hs = kats["headers"]
+    parsed = [H.parse_header(bytes.fromhex(h["raw"])) for h in hs]
+    ea = [bytes.fromhex(h["eta_alpha"]) for h in hs]
+    la = [bytes.fromhex(h["leader_alpha"]) for h in hs]
+    raw = bytes.fromhex(hs[0]["raw"])
+    for off in range(parsed[0].body_span[0], len(raw), stride):
+        r = bytearray(raw)
+        r[off] = (r[off] + 1) & 0xFF
+        try:
+            parsed.append(H.parse_header(bytes(r)))
+        except Exception:
+            continue
+        ea.append(ea[0])
+        la.append(la[0])
+    return H.pack(parsed, ea, la, slots_per_kes_period=100)
+
+
+@pytest.mark.parametrize("mode", [0, 1], ids=["throughput", "latency"])
+def test_header_drivers(dh, kats, mode):
+    """tpraos.h's cores + single-inversion finish, in the throughput schedule
+    (one lane, VRF key table shared) and the latency schedule (a lane per
+    core), equal the oracle's verdict bits and outputs."""
+    batch = _hdr_variants(kats, stride=7)
+    n = len(batch)
+    s = batch.c_struct()
+    verdict = np.zeros(n, np.uint8)
+    be = np.zeros((n, 64), np.uint8)
+    bl = np.zeros((n, 64), np.uint8)
+    dh.dh_tpraos_verify.argtypes = [ctypes.c_void_p, ctypes.c_int] + [ctypes.c_void_p] * 3
+    assert dh.dh_tpraos_verify(ctypes.addressof(s), mode, O.p(verdict), O.p(be), O.p(bl)) == 0
+    wv, wbe, wbl = O.tpraos_verify_batch(batch)
+    np.testing.assert_array_equal(verdict, wv)
+    np.testing.assert_array_equal(be, wbe)
+    np.testing.assert_array_equal(bl, wbl)
+    for h, v in zip(kats["headers"], verdict):
+        assert int(v) == h["expect_verdict"]
+    assert (verdict != 15).sum() > 10
+
+
 def test_zero_bound_violations(dh):
     """Every multiplier input seen by the tests above stayed inside the limb
     bounds fe25519.h's overflow analysis assumes (run last in this module)."""

@@ -211,3 +211,70 @@ def test_empty_batches(gpu_lib):
     assert Ed25519DSIGN.verify_batch(np.zeros((0, 32), np.uint8), [], np.zeros((0, 64), np.uint8)).size == 0
     ok, beta = PraosVRF.verify_batch(np.zeros((0, 32), np.uint8), [], np.zeros((0, 80), np.uint8))
     assert ok.size == 0 and beta.shape == (0, 64)
+
+
+def _golden_variants(kats):
+    """Golden headers + every decodable single-byte corruption of the first."""
+    from ouroboros_network_amd import header as H
+
+    hs = kats["headers"]
+    parsed = [H.parse_header(bytes.fromhex(h["raw"])) for h in hs]
+    ea = [bytes.fromhex(h["eta_alpha"]) for h in hs]
+    la = [bytes.fromhex(h["leader_alpha"]) for h in hs]
+    raw = bytes.fromhex(hs[0]["raw"])
+    for off in range(parsed[0].body_span[0], len(raw)):
+        r = bytearray(raw)
+        r[off] = (r[off] + 1) & 0xFF
+        try:
+            parsed.append(H.parse_header(bytes(r)))
+        except Exception:
+            continue
+        ea.append(ea[0])
+        la.append(la[0])
+    return H.pack(parsed, ea, la, slots_per_kes_period=100)
+
+
+def test_lowlat_equals_throughput_and_oracle(gpu_lib, kats):
+    """Latency mode (six lanes per header + finish launch) gives the same
+    verdict bits and outputs as the throughput kernel and the oracle."""
+    from ouroboros_network_amd.tpraos import verify_headers, verify_headers_lowlat
+
+    batch = _golden_variants(kats)
+    wv, wbe, wbl = O.tpraos_verify_batch(batch)
+    for fn in (verify_headers, verify_headers_lowlat):
+        v, be, bl = fn(batch)
+        np.testing.assert_array_equal(v, wv)
+        np.testing.assert_array_equal(be, wbe)
+        np.testing.assert_array_equal(bl, wbl)
+    for lo, hi in [(0, 1), (3, 67), (10, 10)]:
+        v, be, bl = verify_headers_lowlat(batch.slice(lo, hi))
+        np.testing.assert_array_equal(v, wv[lo:hi])
+        np.testing.assert_array_equal(bl, wbl[lo:hi])
+
+
+def test_header_plan_replays(gpu_lib, kats):
+    """The captured-graph plan over 64-header windows (BASELINE configs[4]):
+    every window and a ragged tail match the oracle; replays are independent
+    (a window after a different one gives the same answer); oversize batches
+    are rejected, never silently truncated."""
+    from ouroboros_network_amd.tpraos import HeaderPlan
+
+    batch = _golden_variants(kats)
+    n = len(batch)
+    assert n > 128
+    wv, wbe, wbl = O.tpraos_verify_batch(batch)
+    plan = HeaderPlan(max_headers=64, max_body_bytes=int(batch.body.size))
+    try:
+        for lo in list(range(0, n, 64)) + [0]:
+            hi = min(n, lo + 64)
+            v, be, bl = plan.run(batch.slice(lo, hi))
+            np.testing.assert_array_equal(v, wv[lo:hi])
+            np.testing.assert_array_equal(be, wbe[lo:hi])
+            np.testing.assert_array_equal(bl, wbl[lo:hi])
+        v, _, _ = plan.run(batch.slice(5, 6))
+        assert int(v[0]) == int(wv[5])
+        assert plan.run(batch.slice(0, 0))[0].size == 0
+        with pytest.raises(ValueError):
+            plan.run(batch.slice(0, 65))
+    finally:
+        plan.close()
