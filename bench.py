@@ -240,6 +240,52 @@ def cpu_baseline(hb, threads: int):
     return len(hb) / dt, dt, res
 
 
+def latency_leg(hdr, batch: int, iters: int, cpu_threads: int, cpu_iters: int):
+    """configs[4]: ChainSync small-batch path.  `batch` headers from host
+    memory through the captured hipGraph plan (H2D, the six-lanes-per-header
+    core kernel, the finish kernel, D2H), wall-clock per call; next to the CPU
+    oracle on the same batch on 1 core and on `cpu_threads` cores."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_ffi as O
+    from ouroboros_network_amd.tpraos import HeaderPlan
+
+    hb = hdr.host_sample(batch)
+    body_bytes = int(hb.body_len.astype(np.int64).sum())
+    plan = HeaderPlan(batch, body_bytes)
+    try:
+        out = plan.run(hb)
+        for _ in range(min(50, iters)):
+            plan.run(hb, out)
+        lat = np.empty(iters)
+        for k in range(iters):
+            t0 = time.perf_counter()
+            plan.run(hb, out)
+            lat[k] = time.perf_counter() - t0
+    finally:
+        plan.close()
+    cv, cbe, cbl = O.tpraos_verify_batch(hb, threads=1)
+    same = bool((out[0] == cv).all() and (out[1] == cbe).all() and (out[2] == cbl).all())
+
+    def cpu_lat(threads):
+        O.tpraos_verify_batch(hb, threads=threads)
+        t = np.empty(cpu_iters)
+        for k in range(cpu_iters):
+            t0 = time.perf_counter()
+            O.tpraos_verify_batch(hb, threads=threads)
+            t[k] = time.perf_counter() - t0
+        return t
+
+    c1, cn = cpu_lat(1), cpu_lat(cpu_threads)
+    ms = lambda a, q: round(float(np.percentile(a, q)) * 1e3, 3)  # noqa: E731
+    return {"workload": f"configs[4]: {batch}-header batches from host memory, hipGraph plan",
+            "iters": iters, "p50_ms": ms(lat, 50), "p99_ms": ms(lat, 99),
+            "headers_per_s_at_p50": round(batch / (np.percentile(lat, 50)), 1),
+            "all_valid": bool((out[0] == 15).all()), "gpu_equals_cpu": same,
+            "cpu_1core": {"p50_ms": ms(c1, 50), "p99_ms": ms(c1, 99), "iters": cpu_iters},
+            "cpu_ncores": {"cores": cpu_threads, "p50_ms": ms(cn, 50), "p99_ms": ms(cn, 99),
+                           "iters": cpu_iters}}
+
+
 def load_pmc_traffic():
     """HBM bytes per launch of the header kernel from the committed PMC run."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
@@ -258,9 +304,13 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--headers", type=int, default=1 << 20, help="headers per GPU per step")
     ap.add_argument("--pools", type=int, default=1024)
-    ap.add_argument("--cpu-sample", type=int, default=16384)
+    ap.add_argument("--cpu-sample", type=int, default=65536)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-extras", action="store_true")
+    ap.add_argument("--no-latency", action="store_true")
+    ap.add_argument("--lat-iters", type=int, default=2000,
+                    help="configs[4] 64-header plan launches timed for p50/p99")
+    ap.add_argument("--lat-cpu-iters", type=int, default=50)
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (RCCL over xGMI, the real path) or gloo (rehearsal of the "
                          "multi-rank path on fewer GPUs: ranks share devices, gather via host)")
@@ -403,6 +453,12 @@ def main():
                     out[k] = val
             except Exception as e:  # noqa: BLE001
                 out["components_error"] = str(e)
+        if not args.no_latency and world == 1:
+            try:
+                out["latency"] = latency_leg(hdr, 64, args.lat_iters, min(16, os.cpu_count() or 1),
+                                             args.lat_cpu_iters)
+            except Exception as e:  # noqa: BLE001
+                out["latency"] = {"error": str(e)}
         if not args.no_cpu and world == 1:
             threads = min(16, os.cpu_count() or 1)
             m = min(args.cpu_sample, n)
