@@ -62,6 +62,19 @@ const char *ouro_last_error(void);
 int ouro_ed25519_verify(const unsigned char *sig, const unsigned char *m,
                         unsigned long long mlen, const unsigned char *pk);
 
+/* Replaces the donna-derived Ed25519 verify of cardano-crypto
+ * (cardano_crypto_ed25519_sign_open(m, mlen, pk, sig) [recalled], argument
+ * order kept) that ByronDSIGN.verifyDSIGN reaches through verifySignatureRaw
+ * (ouroboros-consensus-byron/src/Ouroboros/Consensus/Byron/Crypto/DSIGN.hs:110-113;
+ * callers ouroboros-consensus/src/Ouroboros/Consensus/Protocol/PBFT.hs:332 and
+ * ouroboros-consensus-byron/src/Ouroboros/Consensus/Byron/Ledger/Integrity.hs:32-35).
+ * pk = the first 32 bytes of the 64-byte XPub; m = signTag || signable bytes.
+ * Acceptance differs from ouro_ed25519_verify: rejects only
+ * sig[63] & 0xE0 and an undecodable A -- no S < L, canonicity or small-order
+ * checks.  0 = valid, -1 = invalid, <= -2 = error. */
+int ouro_byron_ed25519_verify(const unsigned char *m, size_t mlen, const unsigned char *pk,
+                              const unsigned char *sig);
+
 /* Replaces crypto_vrf_ietfdraft03_verify (cardano-crypto-praos, bound by
  * PraosVRF.verifyVRF / verifyCertified; caller: OVERLAY vrfChecks via
  * Shelley/Protocol.hs:435).  On success writes the 64-byte output. */
@@ -88,6 +101,12 @@ int ouro_ed25519_verify_batch(size_t n, const uint8_t *pk /* n x 32 */,
                               const uint8_t *sig /* n x 64 */, const uint8_t *msg,
                               const uint64_t *msg_off, const uint32_t *msg_len,
                               uint8_t *verdict);
+
+/* ByronDSIGN acceptance (see ouro_byron_ed25519_verify), pk = XPub[0:32] */
+int ouro_byron_ed25519_verify_batch(size_t n, const uint8_t *pk /* n x 32 */,
+                                    const uint8_t *sig /* n x 64 */, const uint8_t *msg,
+                                    const uint64_t *msg_off, const uint32_t *msg_len,
+                                    uint8_t *verdict);
 
 /* beta[i] = 64-byte output on success, zeros otherwise */
 int ouro_vrf03_verify_batch(size_t n, const uint8_t *pk /* n x 32 */,
@@ -157,6 +176,10 @@ int ouro_ed25519_verify_batch_device(void *stream, size_t n, const uint8_t *pk,
                                      const uint8_t *sig, const uint8_t *msg,
                                      const uint64_t *msg_off, const uint32_t *msg_len,
                                      uint8_t *verdict);
+int ouro_byron_ed25519_verify_batch_device(void *stream, size_t n, const uint8_t *pk,
+                                           const uint8_t *sig, const uint8_t *msg,
+                                           const uint64_t *msg_off, const uint32_t *msg_len,
+                                           uint8_t *verdict);
 int ouro_vrf03_verify_batch_device(void *stream, size_t n, const uint8_t *pk,
                                    const uint8_t *proof, const uint8_t *alpha,
                                    const uint64_t *alpha_off, const uint32_t *alpha_len,

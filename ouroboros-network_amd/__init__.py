@@ -1,5 +1,6 @@
 """ouroboros-network_amd -- MI355X-native batch verifier for the Ouroboros
-Praos/TPraos header-crypto hot path (Ed25519DSIGN, Sum6KES, PraosVRF draft-03).
+Praos/TPraos header-crypto hot path (Ed25519DSIGN, Sum6KES, PraosVRF draft-03)
+and the Byron PBFT block signature (ByronDSIGN).
 
 Importable as ``ouroboros_network_amd`` (repo-root symlink).  The compute path
 is the gfx950 library ``lib/libouro_verify.so`` behind the C ABI in
@@ -7,12 +8,14 @@ is the gfx950 library ``lib/libouro_verify.so`` behind the C ABI in
 """
 from . import _native
 from ._native import DeviceError, NativeUnavailable
+from .byron import ByronDSIGN, parse_byron_header, verify_byron_headers
 from .dsign import Ed25519DSIGN
 from .kes import Sum6KES, kes_period
 from .tpraos import HeaderBatch, first_invalid, verify_headers
 from .vrf import PraosVRF
 
 __all__ = [
+    "ByronDSIGN",
     "DeviceError",
     "Ed25519DSIGN",
     "HeaderBatch",
@@ -21,6 +24,8 @@ __all__ = [
     "Sum6KES",
     "first_invalid",
     "kes_period",
+    "parse_byron_header",
+    "verify_byron_headers",
     "verify_headers",
 ]
 

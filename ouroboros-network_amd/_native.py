@@ -67,14 +67,17 @@ SIGNATURES = {
     "ouro_set_device": (_I, [_I]),
     "ouro_last_error": (ctypes.c_char_p, []),
     "ouro_ed25519_verify": (_I, [_P, _P, _ULL, _P]),
+    "ouro_byron_ed25519_verify": (_I, [_P, _SZ, _P, _P]),
     "ouro_vrf03_verify": (_I, [_P, _P, _P, _P, _ULL]),
     "ouro_vrf03_proof_to_hash": (_I, [_P, _P]),
     "ouro_sum6kes_verify": (_I, [_P, ctypes.c_uint, _P, _ULL, _P]),
     "ouro_ed25519_verify_batch": (_I, [_SZ, _P, _P, _P, _P, _P, _P]),
+    "ouro_byron_ed25519_verify_batch": (_I, [_SZ, _P, _P, _P, _P, _P, _P]),
     "ouro_vrf03_verify_batch": (_I, [_SZ, _P, _P, _P, _P, _P, _P, _P]),
     "ouro_sum6kes_verify_batch": (_I, [_SZ, _P, _P, _P, _P, _P, _P, _P]),
     "ouro_tpraos_verify_batch": (_I, [ctypes.POINTER(TPraosBatch), _P, _P, _P]),
     "ouro_ed25519_verify_batch_device": (_I, [_P, _SZ, _P, _P, _P, _P, _P, _P]),
+    "ouro_byron_ed25519_verify_batch_device": (_I, [_P, _SZ, _P, _P, _P, _P, _P, _P]),
     "ouro_vrf03_verify_batch_device": (_I, [_P, _SZ, _P, _P, _P, _P, _P, _P, _P]),
     "ouro_sum6kes_verify_batch_device": (_I, [_P, _SZ, _P, _P, _P, _P, _P, _P, _P]),
     "ouro_tpraos_verify_batch_device": (_I, [_P, ctypes.POINTER(TPraosBatch), _P, _P, _P]),

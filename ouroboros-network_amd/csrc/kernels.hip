@@ -61,7 +61,7 @@ __global__ void __launch_bounds__(kBlock, 2) k_ed25519_verify(
     size_t n, const uint8_t* __restrict__ pk, const uint8_t* __restrict__ sig,
     const uint8_t* __restrict__ msg, const uint64_t* __restrict__ msg_off,
     const uint32_t* __restrict__ msg_len, uint8_t* __restrict__ verdict, int32_t* scratch,
-    const int32_t* __restrict__ btab) {
+    const int32_t* __restrict__ btab, uint32_t byron) {
   const size_t tid = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   const size_t nth = (size_t)gridDim.x * blockDim.x;
   int32_t* lane = scratch + tid * kLaneWords;
@@ -69,7 +69,8 @@ __global__ void __launch_bounds__(kBlock, 2) k_ed25519_verify(
     uint32_t s[16], p[8];
     load_words(s, sig + 64 * i, 4);
     load_words(p, pk + 32 * i, 2);
-    const bool ok = ed25519_verify_lane(s, p, ShaGlobalTail{msg + msg_off[i]}, msg_len[i], lane, btab);
+    const bool ok = ed25519_verify_lane(s, p, ShaGlobalTail{msg + msg_off[i]}, msg_len[i], lane,
+                                        btab, byron != 0);
     verdict[i] = ok ? 1 : 0;
   }
 }
@@ -342,8 +343,9 @@ int launch_check() {
 }
 
 // ---- device-pointer launches (shared by the host-buffer and device APIs) ----
+// byron = 1: ByronDSIGN acceptance (cardano-crypto)
 int launch_ed(hipStream_t st, size_t n, const uint8_t* pk, const uint8_t* sig, const uint8_t* msg,
-              const uint64_t* off, const uint32_t* len, uint8_t* verdict) {
+              const uint64_t* off, const uint32_t* len, uint8_t* verdict, uint32_t byron = 0) {
   DeviceState* ds;
   int rc = device_state(&ds);
   if (rc) return rc;
@@ -351,7 +353,7 @@ int launch_ed(hipStream_t st, size_t n, const uint8_t* pk, const uint8_t* sig, c
   int32_t* scr;
   if ((rc = plan(ds, kEd, n, st, &grid, &scr))) return rc;
   hipLaunchKernelGGL(k_ed25519_verify, dim3(grid), dim3(kBlock), 0, st, n, pk, sig, msg, off, len,
-                     verdict, scr, ds->btab);
+                     verdict, scr, ds->btab, byron);
   return launch_check();
 }
 
@@ -479,8 +481,12 @@ int ouro_set_device(int device) {
 
 const char* ouro_last_error(void) { return t_last_error.c_str(); }
 
-int ouro_ed25519_verify_batch(size_t n, const uint8_t* pk, const uint8_t* sig, const uint8_t* msg,
-                              const uint64_t* msg_off, const uint32_t* msg_len, uint8_t* verdict) {
+}  // extern "C"
+
+namespace {
+int ed_batch_host(size_t n, const uint8_t* pk, const uint8_t* sig, const uint8_t* msg,
+                  const uint64_t* msg_off, const uint32_t* msg_len, uint8_t* verdict,
+                  uint32_t byron) {
   if (n == 0) return OURO_OK;
   if (!pk || !sig || !msg_off || !msg_len || !verdict) return fail(OURO_EINVAL, "null argument");
   hipStream_t st;
@@ -496,12 +502,26 @@ int ouro_ed25519_verify_batch(size_t n, const uint8_t* pk, const uint8_t* sig, c
   auto dlen = sg.up(msg_len, n);
   auto dver = sg.out<uint8_t>(n);
   if (sg.rc) return sg.rc;
-  if ((rc = launch_ed(st, n, dpk, dsig, dmsg, doff, dlen, dver))) return rc;
+  if ((rc = launch_ed(st, n, dpk, dsig, dmsg, doff, dlen, dver, byron))) return rc;
   std::vector<uint8_t> tmp(n);
   if ((rc = download(st, tmp.data(), dver, n))) return rc;
   if ((rc = finish(st))) return rc;
   memcpy(verdict, tmp.data(), n);
   return OURO_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int ouro_ed25519_verify_batch(size_t n, const uint8_t* pk, const uint8_t* sig, const uint8_t* msg,
+                              const uint64_t* msg_off, const uint32_t* msg_len, uint8_t* verdict) {
+  return ed_batch_host(n, pk, sig, msg, msg_off, msg_len, verdict, 0);
+}
+
+int ouro_byron_ed25519_verify_batch(size_t n, const uint8_t* pk, const uint8_t* sig,
+                                    const uint8_t* msg, const uint64_t* msg_off,
+                                    const uint32_t* msg_len, uint8_t* verdict) {
+  return ed_batch_host(n, pk, sig, msg, msg_off, msg_len, verdict, 1);
 }
 
 int ouro_vrf03_verify_batch(size_t n, const uint8_t* pk, const uint8_t* proof, const uint8_t* alpha,
@@ -622,6 +642,19 @@ int ouro_ed25519_verify(const unsigned char* sig, const unsigned char* m, unsign
   return v ? OURO_OK : OURO_INVALID;
 }
 
+int ouro_byron_ed25519_verify(const unsigned char* m, size_t mlen, const unsigned char* pk,
+                              const unsigned char* sig) {
+  if (!sig || !pk || (mlen && !m)) return OURO_INVALID;
+  const uint64_t off = 0;
+  const uint32_t len = (uint32_t)mlen;
+  if ((size_t)len != mlen) return fail(OURO_EINVAL, "message too long");
+  uint8_t v = 0;
+  static const uint8_t empty[1] = {0};
+  int rc = ouro_byron_ed25519_verify_batch(1, pk, sig, mlen ? m : empty, &off, &len, &v);
+  if (rc) return rc;
+  return v ? OURO_OK : OURO_INVALID;
+}
+
 int ouro_vrf03_verify(unsigned char* output, const unsigned char* pk, const unsigned char* proof,
                       const unsigned char* msg, unsigned long long msglen) {
   if (!pk || !proof || (msglen && !msg)) return OURO_INVALID;
@@ -681,6 +714,15 @@ int ouro_ed25519_verify_batch_device(void* stream, size_t n, const uint8_t* pk, 
   if (n == 0) return OURO_OK;
   hipStream_t st = static_cast<hipStream_t>(stream);  // NULL = HIP's default stream
   return launch_ed(st, n, pk, sig, msg, msg_off, msg_len, verdict);
+}
+
+int ouro_byron_ed25519_verify_batch_device(void* stream, size_t n, const uint8_t* pk,
+                                           const uint8_t* sig, const uint8_t* msg,
+                                           const uint64_t* msg_off, const uint32_t* msg_len,
+                                           uint8_t* verdict) {
+  if (n == 0) return OURO_OK;
+  hipStream_t st = static_cast<hipStream_t>(stream);  // NULL = HIP's default stream
+  return launch_ed(st, n, pk, sig, msg, msg_off, msg_len, verdict, 1);
 }
 
 int ouro_vrf03_verify_batch_device(void* stream, size_t n, const uint8_t* pk, const uint8_t* proof,

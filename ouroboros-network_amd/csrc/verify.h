@@ -214,15 +214,23 @@ OURO_FI ge_p2 dsm_result(const int32_t* lane) {
 // in lane[kSlotOut]; the verdict is core && encode(R') == R.
 template <class Tail>
 OURO_HD inline bool ed25519_core(const uint32_t sig[16], const uint32_t pk[8], const Tail& msg,
-                                 uint32_t mlen, int32_t* lane, const int32_t* btab) {
+                                 uint32_t mlen, int32_t* lane, const int32_t* btab,
+                                 bool byron = false) {
   uint32_t R[8], S[8];
 #pragma unroll
   for (int i = 0; i < 8; i++) {
     R[i] = sig[i];
     S[i] = sig[8 + i];
   }
-  bool ok = sc_is_canonical(S) && !ge_has_small_order(R);
-  ok = ok && ge_is_canonical(pk) && !ge_has_small_order(pk);
+  // libsodium 1.0.18 (App. B.1) or, for ByronDSIGN, the donna-derived
+  // cardano-crypto rule (App. B.5): only the top three bits of S are checked
+  bool ok;
+  if (byron) {
+    ok = (S[7] >> 29) == 0;
+  } else {
+    ok = sc_is_canonical(S) && !ge_has_small_order(R);
+    ok = ok && ge_is_canonical(pk) && !ge_has_small_order(pk);
+  }
   ge_p3 negA;
   ok = ge_decode(&negA, pk, true) && ok;
   // h = SHA-512(R || A || M) mod L
@@ -251,8 +259,8 @@ OURO_HD inline bool ed25519_core(const uint32_t sig[16], const uint32_t pk[8], c
 template <class Tail>
 OURO_HD inline bool ed25519_verify_lane(const uint32_t sig[16], const uint32_t pk[8],
                                         const Tail& msg, uint32_t mlen, int32_t* lane,
-                                        const int32_t* btab) {
-  const bool ok = ed25519_core(sig, pk, msg, mlen, lane, btab);
+                                        const int32_t* btab, bool byron = false) {
+  const bool ok = ed25519_core(sig, pk, msg, mlen, lane, btab, byron);
   uint32_t enc[8];
   ge_p2_encode(enc, dsm_result(lane));
   bool eq = true;

@@ -10,6 +10,7 @@ import numpy as np
 import pytest
 
 import oracle_ffi as O
+from edge_cases import L as edge_L
 from edge_cases import ed25519_edge_cases, vrf_edge_cases
 
 pytestmark = pytest.mark.gpu
@@ -278,3 +279,43 @@ def test_header_plan_replays(gpu_lib, kats):
             plan.run(batch.slice(0, 65))
     finally:
         plan.close()
+
+
+# ---- ByronDSIGN ------------------------------
+
+def test_byron_golden_header(gpu_lib, kats):
+    from ouroboros_network_amd import ByronDSIGN, parse_byron_header, verify_byron_headers
+
+    b = kats["byron"]
+    h = parse_byron_header(bytes.fromhex(b["raw"]))
+    ctx = (h.magic, h.issuer_xpub)
+    assert ByronDSIGN.verify_dsign(ctx, h.delegate_xpub, h.to_sign, h.sig) is None
+    assert ByronDSIGN.verify_dsign(ctx, h.delegate_xpub, h.to_sign[:-1] + b"\x00", h.sig) \
+        == "Verification failed"
+    assert ByronDSIGN.verify_dsign((h.magic + 1, h.issuer_xpub), h.delegate_xpub, h.to_sign,
+                                   h.sig) == "Verification failed"
+    assert verify_byron_headers([h, h]).tolist() == [True, True]
+
+
+def test_byron_batch_matches_oracle(gpu_lib):
+    """Synthetic signatures with 1/8 corrupted, the Ed25519 edge-case set and
+    the Byron-specific corners (S + L < 2^253 accepted, top bits of S set):
+    verdicts bit-exact with the oracle's donna-style rule."""
+    from ouroboros_network_amd import ByronDSIGN
+
+    rng = np.random.default_rng(11)
+    pk, sig, msg = O.synth_ed25519(1024, first=5000)
+    corrupt_rows(rng, [pk, sig, msg])
+    # S -> S + L on every 5th row (valid under Byron rules, invalid under libsodium's)
+    for i in range(0, 1024, 5):
+        s = int.from_bytes(sig[i, 32:].tobytes(), "little") + edge_L
+        if s < 2**253:
+            sig[i, 32:] = np.frombuffer(s.to_bytes(32, "little"), np.uint8)
+    sig[3::97, 63] |= 0x20  # a top bit of S set
+    cases = [(bytes(pk[i]), bytes(sig[i]), bytes(msg[i])) for i in range(1024)]
+    cases += ed25519_edge_cases()
+    got = ByronDSIGN.verify_batch([c[0] for c in cases], [c[2] for c in cases],
+                                  [c[1] for c in cases])
+    want = np.array([O.ed25519_verify_byron(c[1], c[2], c[0]) for c in cases])
+    np.testing.assert_array_equal(got, want)
+    assert want.sum() > 700
