@@ -100,14 +100,26 @@ OURO_FI fe fe_select(const fe& a, const fe& b, bool c) {
   return h;
 }
 
+// signed bit-field extract of the low `bits` bits (v_bfe_i32)
+OURO_FI int32_t sbfe(int32_t x, int bits) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_sbfe(x, 0, bits);
+#else
+  return (int32_t)((uint32_t)x << (32 - bits)) >> (32 - bits);
+#endif
+}
+
 // Balanced (rounding) carry of a 10-column int64 accumulator into a reduced fe.
 // Two interleaved chains (0..4 and 4..9) for ILP, then the 2^255 = 19 wrap.
+// Per step: c = (t + 2^(b-1)) >> b, and the limb t - c 2^b is the b-bit
+// signed field of t's low word (the representative of t mod 2^b in
+// [-2^(b-1), 2^(b-1))), one v_bfe_i32.
 OURO_FI fe fe_carry64(int64_t t[10]) {
   int64_t c;
 #define OURO_CARRY(i, j, bits)                           \
   c = (t[i] + ((int64_t)1 << (bits - 1))) >> bits;        \
   t[j] += c;                                             \
-  t[i] -= c * ((int64_t)1 << bits);
+  t[i] = sbfe((int32_t)t[i], bits);
   OURO_CARRY(0, 1, 26)
   OURO_CARRY(4, 5, 26)
   OURO_CARRY(1, 2, 25)
@@ -120,12 +132,19 @@ OURO_FI fe fe_carry64(int64_t t[10]) {
   OURO_CARRY(8, 9, 26)
   c = (t[9] + ((int64_t)1 << 24)) >> 25;
   t[0] += c * 19;
-  t[9] -= c * ((int64_t)1 << 25);
+  t[9] = sbfe((int32_t)t[9], 25);
   OURO_CARRY(0, 1, 26)
 #undef OURO_CARRY
   fe h;
 #pragma unroll
-  for (int i = 0; i < 10; i++) h.v[i] = (int32_t)t[i];
+  for (int i = 0; i < 10; i++) {
+    h.v[i] = (int32_t)t[i];
+#if defined(__HIP_DEVICE_COMPILE__)
+    // hide the limb ranges: with them known, LLVM narrows the next multiply's
+    // 64-bit MACs into 32-bit pieces and triples its instruction count
+    asm("" : "+v"(h.v[i]));
+#endif
+  }
   return h;
 }
 
