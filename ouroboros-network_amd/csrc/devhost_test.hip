@@ -15,6 +15,35 @@ using namespace ouro;
 
 #if defined(OURO_COUNT_OPS)
 thread_local unsigned long long g_ouro_nmul = 0, g_ouro_nsq = 0, g_ouro_bound_violations = 0;
+
+// bound tracker hooks (fe25519.h): shadow bounds of elements stored in memory
+#include <array>
+#include <unordered_map>
+namespace {
+thread_local std::unordered_map<const void*, std::array<uint64_t, 10>> g_shadow;
+thread_local unsigned long long g_untracked_loads = 0;
+}
+void ouro_trk_violation() {
+  ++g_ouro_bound_violations;
+  static const bool do_abort = getenv("OURO_TRK_ABORT") != nullptr;
+  if (do_abort) abort();
+}
+void ouro_trk_store(const void* p, const uint64_t b[10]) {
+  std::array<uint64_t, 10> a;
+  for (int i = 0; i < 10; i++) a[i] = b[i];
+  g_shadow[p] = a;
+}
+void ouro_trk_load(const void* p, uint64_t b[10]) {
+  auto it = g_shadow.find(p);
+  if (it == g_shadow.end()) {
+    // never stored through st_fe/st_cached: only possible for memory the
+    // tracker did not see being written -- assume the worst 32-bit value
+    ++g_untracked_loads;
+    for (int i = 0; i < 10; i++) b[i] = 0xffffffffu;
+    return;
+  }
+  for (int i = 0; i < 10; i++) b[i] = it->second[i];
+}
 #endif
 
 namespace {
@@ -76,11 +105,18 @@ void dh_fe_sub(uint8_t* out, const uint8_t* a, const uint8_t* b) {
 void dh_fe_invert(uint8_t* out, const uint8_t* a) {
   fe_to_bytes(out, fe_invert(fe_from_bytes(a)));
 }
-// raw-limb round trip: limbs given as 10 int32, canonical encoding out
-void dh_fe_limbs_tobytes(uint8_t* out, const int32_t* limbs) {
-  fe f;
-  for (int i = 0; i < 10; i++) f.v[i] = limbs[i];
+// raw-limb round trip: limbs given as 10 uint32 (< 2^31), canonical encoding out
+void dh_fe_limbs_tobytes(uint8_t* out, const uint32_t* limbs) {
+  fe f = fe_make(limbs[0], limbs[1], limbs[2], limbs[3], limbs[4], limbs[5], limbs[6], limbs[7],
+                 limbs[8], limbs[9]);
   fe_to_bytes(out, f);
+}
+unsigned long long dh_untracked_loads(void) {
+#if defined(OURO_COUNT_OPS)
+  return g_untracked_loads;
+#else
+  return 0;
+#endif
 }
 void dh_sc_reduce64(uint8_t* out, const uint8_t* in64) {
   uint32_t w[16], r[8];

@@ -1,144 +1,186 @@
 // fe25519.h -- GF(2^255 - 19) for gfx950, one field element per lane.
 //
-// Representation: 10 signed 32-bit limbs, radix 2^25.5 (limb i weighs
+// Representation: 10 UNSIGNED 32-bit limbs, radix 2^25.5 (limb i weighs
 // 2^ceil(25.5 i): 26-bit even limbs, 25-bit odd limbs).  Products accumulate
-// in signed 64-bit, which hipcc lowers to v_mad_i64_i32 -- measured on MI355X
-// at ~46.7 lane-ops/CU/clk, i.e. the 64-bit MAC path, see
-// tools/microbench/int_rates.hip and DESIGN.md.  Signed limbs make subtraction
-// free of 2p offsets.
+// in unsigned 64-bit, which hipcc lowers to v_mad_u64_u32.  The signed form
+// (v_mad_i64_i32) issues slower on MI355X: the same multiply runs 14 % faster
+// unsigned although it executes more instructions (profiles/r01c/
+// fe_mul_variants.json; tools/microbench/fe_mul_variants.hip).
 //
-// Bound discipline ("reduced" = what fe_mul/fe_sq/fe_carry return):
-//   |even limb| <= 2^25, |odd limb| <= 2^24 (+ a few units).
-// fe_mul / fe_sq inputs may be any sum/difference of at most three reduced
-// elements (|limb| < 1.68 * 2^26 keeps 19*g in int32 and every column sum in
-// int64).  The group formulas in ge25519.h respect this.
+// Unsigned limbs mean subtraction adds a multiple of p first:
+//   fe_sub(f, g)  = f + 2p - g      (g <= 2p limbwise)
+//   fe_sub4(f, g) = f + 4p - g      (g <= 4p limbwise)
+// and every operand of a multiplication must keep its column sums below 2^64
+// and 19 * (its second operand) below 2^32.  The group formulas in ge25519.h
+// are arranged for that.  Rather than a hand proof per formula, the host test
+// build (OURO_COUNT_OPS) carries a worst-case upper bound for every limb next
+// to its value -- constants exact, loads/stores through a shadow table,
+// add/sub/select/mul/carry propagating maxima independent of the data -- and
+// counts every operation whose worst case could overflow
+// (tests/test_devcode_host.py::test_zero_bound_violations).  Because the
+// arithmetic's control flow does not depend on the values, one pass through a
+// routine covers all of its inputs.
+//
+// "Reduced" = what fe_mul/fe_sq/fe_carry64 return: limb i <= mask_i (2^26 - 1
+// even, 2^25 - 1 odd), except limb 1 <= 2^25 + 2^18.
 #pragma once
 #include "common.h"
 
-// Operation counting for the host test build only (tools/count_ops.py): the
-// device code never defines OURO_COUNT_OPS.
-// The same build also checks the bound discipline below on every multiplier
-// input (tests assert zero violations over all vectors).
 #if defined(OURO_COUNT_OPS) && !defined(__HIP_DEVICE_COMPILE__)
+#define OURO_TRACK_BOUNDS 1
 extern thread_local unsigned long long g_ouro_nmul, g_ouro_nsq, g_ouro_bound_violations;
 #define OURO_COUNT_MUL() (++g_ouro_nmul)
 #define OURO_COUNT_SQ() (++g_ouro_nsq)
-#define OURO_CHECK_BOUNDS(f)                                                  \
-  do {                                                                        \
-    for (int i_ = 0; i_ < 10; i_++)                                           \
-      if ((f).v[i_] > 113025455 || (f).v[i_] < -113025455) ++g_ouro_bound_violations; \
-  } while (0)
+#define OURO_TRK(...) __VA_ARGS__
+// shadow table for bounds of elements kept in memory (devhost_test.hip)
+void ouro_trk_store(const void* p, const uint64_t b[10]);
+void ouro_trk_load(const void* p, uint64_t b[10]);
+void ouro_trk_violation();  // counts; aborts under OURO_TRK_ABORT=1 (for gdb)
 #else
 #define OURO_COUNT_MUL() ((void)0)
 #define OURO_COUNT_SQ() ((void)0)
-#define OURO_CHECK_BOUNDS(f) ((void)0)
+#define OURO_TRK(...)
 #endif
 
 namespace ouro {
 
 struct fe {
-  int32_t v[10];
+  uint32_t v[10];
+#if defined(OURO_TRACK_BOUNDS)
+  uint64_t b[10];  // host bound tracker: worst-case value of each limb
+#endif
 };
 
-// ---- constants (balanced limbs; generated from the integers) ----
-#define OURO_FE(a0, a1, a2, a3, a4, a5, a6, a7, a8, a9) \
-  { { a0, a1, a2, a3, a4, a5, a6, a7, a8, a9 } }
-// d = -121665/121666
-OURO_FI fe fe_d() {
-  fe r = OURO_FE(-10913610, 13857413, -15372611, 6949391, 114729, -8787816, -6275908, -3247719,
-                 -18696448, -12055116);
-  return r;
+OURO_FI constexpr uint32_t limb_bits(int i) { return (i & 1) ? 25u : 26u; }
+OURO_FI constexpr uint32_t limb_mask(int i) { return (1u << limb_bits(i)) - 1u; }
+// limb i of K*p in the canonical split (limb 0 = K (2^26 - 19))
+OURO_FI constexpr uint32_t kp_limb(uint32_t K, int i) {
+  return i == 0 ? K * ((1u << 26) - 19u) : K * limb_mask(i);
 }
-OURO_FI fe fe_d2() {
-  fe r = OURO_FE(-21827239, -5839606, -30745221, 13898782, 229458, 15978800, -12551817, -6495438,
-                 29715968, 9444199);
-  return r;
+
+#if defined(OURO_TRACK_BOUNDS)
+inline void trk_check(bool ok) {
+  if (!ok) ouro_trk_violation();
 }
-OURO_FI fe fe_sqrtm1() {
-  fe r = OURO_FE(-32595792, -7943725, 9377950, 3500415, 12389472, -272473, -25146209, -2005654,
-                 326686, 11406482);
-  return r;
+inline void trk_exact(fe& f) {
+  for (int i = 0; i < 10; i++) f.b[i] = f.v[i];
 }
-// Montgomery A = 486662 (curve25519), used by Elligator2
-OURO_FI fe fe_mont_a() {
-  fe r = OURO_FE(486662, 0, 0, 0, 0, 0, 0, 0, 0, 0);
+// upper bounds after a floor carry chain over column bounds T (checked < 2^64)
+inline void trk_carry(fe& h, const unsigned __int128 T[10], unsigned __int128 lim) {
+  unsigned __int128 t[10];
+  for (int i = 0; i < 10; i++) {
+    t[i] = T[i];
+    trk_check(t[i] < lim);
+  }
+  auto step = [&](int i, int j) {
+    t[j] += t[i] >> limb_bits(i);
+    if (t[i] > limb_mask(i)) t[i] = limb_mask(i);
+    trk_check(t[j] < lim);
+  };
+  step(0, 1); step(4, 5); step(1, 2); step(5, 6); step(2, 3);
+  step(6, 7); step(3, 4); step(7, 8); step(4, 5); step(8, 9);
+  t[0] += 19 * (t[9] >> 25);
+  if (t[9] > limb_mask(9)) t[9] = limb_mask(9);
+  trk_check(t[0] < lim);
+  step(0, 1);
+  for (int i = 0; i < 10; i++) h.b[i] = (uint64_t)t[i];
+}
+#endif
+
+OURO_FI fe fe_make(uint32_t a0, uint32_t a1, uint32_t a2, uint32_t a3, uint32_t a4, uint32_t a5,
+                   uint32_t a6, uint32_t a7, uint32_t a8, uint32_t a9) {
+  fe r;
+  r.v[0] = a0; r.v[1] = a1; r.v[2] = a2; r.v[3] = a3; r.v[4] = a4;
+  r.v[5] = a5; r.v[6] = a6; r.v[7] = a7; r.v[8] = a8; r.v[9] = a9;
+  OURO_TRK(trk_exact(r));
   return r;
 }
 
-OURO_FI fe fe_zero() {
-  fe r = OURO_FE(0, 0, 0, 0, 0, 0, 0, 0, 0, 0);
-  return r;
+// ---- constants (canonical limbs; tools/check_fe_constants.py) ---------------
+// d = -121665/121666
+OURO_FI fe fe_d() {
+  return fe_make(56195235, 13857412, 51736253, 6949390, 114729, 24766616, 60832955, 30306712,
+                 48412415, 21499315);
 }
-OURO_FI fe fe_one() {
-  fe r = OURO_FE(1, 0, 0, 0, 0, 0, 0, 0, 0, 0);
-  return r;
+OURO_FI fe fe_d2() {
+  return fe_make(45281625, 27714825, 36363642, 13898781, 229458, 15978800, 54557047, 27058993,
+                 29715967, 9444199);
 }
+// sqrt(-1) = 2^((p-1)/4), libsodium's fe25519_sqrtm1
+OURO_FI fe fe_sqrtm1() {
+  return fe_make(34513072, 25610706, 9377949, 3500415, 12389472, 33281959, 41962654, 31548777,
+                 326685, 11406482);
+}
+// Montgomery A = 486662 (curve25519), used by Elligator2
+OURO_FI fe fe_mont_a() { return fe_make(486662, 0, 0, 0, 0, 0, 0, 0, 0, 0); }
+OURO_FI fe fe_zero() { return fe_make(0, 0, 0, 0, 0, 0, 0, 0, 0, 0); }
+OURO_FI fe fe_one() { return fe_make(1, 0, 0, 0, 0, 0, 0, 0, 0, 0); }
+OURO_FI fe fe_two() { return fe_make(2, 0, 0, 0, 0, 0, 0, 0, 0, 0); }
 
 OURO_FI fe fe_add(const fe& f, const fe& g) {
   fe h;
 #pragma unroll
   for (int i = 0; i < 10; i++) h.v[i] = f.v[i] + g.v[i];
+  OURO_TRK(for (int i = 0; i < 10; i++) {
+    h.b[i] = f.b[i] + g.b[i];
+    trk_check(h.b[i] < (1ull << 32));
+  })
   return h;
 }
-OURO_FI fe fe_sub(const fe& f, const fe& g) {
+// f + K p - g
+template <uint32_t K>
+OURO_FI fe fe_subk(const fe& f, const fe& g) {
   fe h;
 #pragma unroll
-  for (int i = 0; i < 10; i++) h.v[i] = f.v[i] - g.v[i];
+  for (int i = 0; i < 10; i++) h.v[i] = (f.v[i] + kp_limb(K, i)) - g.v[i];
+  OURO_TRK(for (int i = 0; i < 10; i++) {
+    trk_check(g.b[i] <= kp_limb(K, i));
+    h.b[i] = f.b[i] + kp_limb(K, i);
+    trk_check(h.b[i] < (1ull << 32));
+  })
   return h;
 }
-OURO_FI fe fe_neg(const fe& f) {
-  fe h;
-#pragma unroll
-  for (int i = 0; i < 10; i++) h.v[i] = -f.v[i];
-  return h;
-}
+OURO_FI fe fe_sub(const fe& f, const fe& g) { return fe_subk<2>(f, g); }
+OURO_FI fe fe_sub4(const fe& f, const fe& g) { return fe_subk<4>(f, g); }
+OURO_FI fe fe_neg(const fe& f) { return fe_subk<2>(fe_zero(), f); }
+OURO_FI fe fe_neg4(const fe& f) { return fe_subk<4>(fe_zero(), f); }
+
 // c ? a : b, per lane
 OURO_FI fe fe_select(const fe& a, const fe& b, bool c) {
   fe h;
 #pragma unroll
   for (int i = 0; i < 10; i++) h.v[i] = c ? a.v[i] : b.v[i];
+  OURO_TRK(for (int i = 0; i < 10; i++) h.b[i] = a.b[i] > b.b[i] ? a.b[i] : b.b[i];)
   return h;
 }
 
-// signed bit-field extract of the low `bits` bits (v_bfe_i32)
-OURO_FI int32_t sbfe(int32_t x, int bits) {
-#if defined(__HIP_DEVICE_COMPILE__)
-  return __builtin_amdgcn_sbfe(x, 0, bits);
-#else
-  return (int32_t)((uint32_t)x << (32 - bits)) >> (32 - bits);
-#endif
-}
-
-// Balanced (rounding) carry of a 10-column int64 accumulator into a reduced fe.
-// Two interleaved chains (0..4 and 4..9) for ILP, then the 2^255 = 19 wrap.
-// Per step: c = (t + 2^(b-1)) >> b, and the limb t - c 2^b is the b-bit
-// signed field of t's low word (the representative of t mod 2^b in
-// [-2^(b-1), 2^(b-1))), one v_bfe_i32.
-OURO_FI fe fe_carry64(int64_t t[10]) {
-  int64_t c;
-#define OURO_CARRY(i, j, bits)                           \
-  c = (t[i] + ((int64_t)1 << (bits - 1))) >> bits;        \
-  t[j] += c;                                             \
-  t[i] = sbfe((int32_t)t[i], bits);
-  OURO_CARRY(0, 1, 26)
-  OURO_CARRY(4, 5, 26)
-  OURO_CARRY(1, 2, 25)
-  OURO_CARRY(5, 6, 25)
-  OURO_CARRY(2, 3, 26)
-  OURO_CARRY(6, 7, 26)
-  OURO_CARRY(3, 4, 25)
-  OURO_CARRY(7, 8, 25)
-  OURO_CARRY(4, 5, 26)
-  OURO_CARRY(8, 9, 26)
-  c = (t[9] + ((int64_t)1 << 24)) >> 25;
+// Floor carry of a 10-column accumulator into a reduced element.  Two
+// interleaved chains (0..4 and 4..9) for ILP, then the 2^255 = 19 wrap.
+OURO_FI fe fe_carry64(uint64_t t[10]) {
+  uint64_t c;
+#define OURO_CARRY(i, j)          \
+  c = t[i] >> limb_bits(i);       \
+  t[j] += c;                      \
+  t[i] &= limb_mask(i);
+  OURO_CARRY(0, 1)
+  OURO_CARRY(4, 5)
+  OURO_CARRY(1, 2)
+  OURO_CARRY(5, 6)
+  OURO_CARRY(2, 3)
+  OURO_CARRY(6, 7)
+  OURO_CARRY(3, 4)
+  OURO_CARRY(7, 8)
+  OURO_CARRY(4, 5)
+  OURO_CARRY(8, 9)
+  c = t[9] >> 25;
+  t[9] &= limb_mask(9);
   t[0] += c * 19;
-  t[9] = sbfe((int32_t)t[9], 25);
-  OURO_CARRY(0, 1, 26)
+  OURO_CARRY(0, 1)
 #undef OURO_CARRY
   fe h;
 #pragma unroll
   for (int i = 0; i < 10; i++) {
-    h.v[i] = (int32_t)t[i];
+    h.v[i] = (uint32_t)t[i];
 #if defined(__HIP_DEVICE_COMPILE__)
     // hide the limb ranges: with them known, LLVM narrows the next multiply's
     // 64-bit MACs into 32-bit pieces and triples its instruction count
@@ -148,28 +190,44 @@ OURO_FI fe fe_carry64(int64_t t[10]) {
   return h;
 }
 
-// Re-balance an element whose limbs grew through additions.
+// Cheap 32-bit re-normalisation of an element whose limbs grew through
+// additions (one sequential pass; limb 0 may keep a small excess).
 OURO_FI fe fe_carry(const fe& f) {
-  int64_t t[10];
+  fe h;
+  uint32_t c = 0;
 #pragma unroll
-  for (int i = 0; i < 10; i++) t[i] = f.v[i];
-  return fe_carry64(t);
+  for (int i = 0; i < 10; i++) {
+    const uint32_t t = f.v[i] + c;
+    c = t >> limb_bits(i);
+    h.v[i] = t & limb_mask(i);
+  }
+  h.v[0] += 19 * c;
+  OURO_TRK({
+    uint64_t cb = 0;
+    for (int i = 0; i < 10; i++) {
+      const uint64_t t = f.b[i] + cb;
+      trk_check(t < (1ull << 32));
+      cb = t >> limb_bits(i);
+      h.b[i] = t < limb_mask(i) ? t : limb_mask(i);
+    }
+    h.b[0] += 19 * cb;
+  })
+  return h;
 }
 
 // h = f * g.  Column k collects f_i g_j with i + j = k (mod 10); odd*odd
 // terms carry a factor 2 (2^ceil(25.5 i) 2^ceil(25.5 j) = 2 * 2^ceil(25.5 (i+j)))
-// and wrapped terms a factor 19 (2^255 = 19).
+// and wrapped terms a factor 19 (2^255 = 19), applied to g.  Needs
+// 19 g_j < 2^32: g is the operand with the smaller bound.
 OURO_FI fe fe_mul(const fe& f, const fe& g) {
   OURO_COUNT_MUL();
-  OURO_CHECK_BOUNDS(f);
-  OURO_CHECK_BOUNDS(g);
-  int32_t g19[10], f2[10];
+  uint32_t g19[10], f2[10];
 #pragma unroll
   for (int i = 0; i < 10; i++) {
-    g19[i] = 19 * g.v[i];
-    f2[i] = (i & 1) ? 2 * f.v[i] : f.v[i];
+    g19[i] = 19u * g.v[i];
+    f2[i] = (i & 1) ? 2u * f.v[i] : f.v[i];
   }
-  int64_t t[10];
+  uint64_t t[10];
 #pragma unroll
   for (int k = 0; k < 10; k++) t[k] = 0;
 #pragma unroll
@@ -177,24 +235,80 @@ OURO_FI fe fe_mul(const fe& f, const fe& g) {
 #pragma unroll
     for (int j = 0; j < 10; j++) {
       const int k = i + j;
-      const int32_t a = ((i & 1) && (j & 1)) ? f2[i] : f.v[i];
-      const int32_t b = (k >= 10) ? g19[j] : g.v[j];
-      t[k >= 10 ? k - 10 : k] += (int64_t)a * b;
+      const uint32_t a = ((i & 1) && (j & 1)) ? f2[i] : f.v[i];
+      const uint32_t b = (k >= 10) ? g19[j] : g.v[j];
+      t[k >= 10 ? k - 10 : k] += (uint64_t)a * b;
     }
   }
-  return fe_carry64(t);
+  fe h = fe_carry64(t);
+  OURO_TRK({
+    unsigned __int128 T[10] = {0};
+    for (int i = 0; i < 10; i++) {
+      if (i & 1) trk_check(2 * f.b[i] < (1ull << 32));
+      if (i >= 1) trk_check(19 * g.b[i] < (1ull << 32));
+      for (int j = 0; j < 10; j++) {
+        const int k = i + j;
+        unsigned __int128 x = (unsigned __int128)f.b[i] * g.b[j];
+        if ((i & 1) && (j & 1)) x *= 2;
+        if (k >= 10) x *= 19;
+        T[k % 10] += x;
+      }
+    }
+    trk_carry(h, T, (unsigned __int128)1 << 64);
+  })
+  return h;
+}
+
+// f * g with the factor 19 applied per column after accumulation: no bound on
+// 19 g, for the few products whose operands are both wide (slower: ~9 % per
+// multiply on MI355X, profiles/r01c/fe_mul_variants.json "fe10d_mul").
+OURO_FI fe fe_mul_wide(const fe& f, const fe& g) {
+  OURO_COUNT_MUL();
+  uint32_t f2[10];
+#pragma unroll
+  for (int i = 0; i < 10; i++) f2[i] = (i & 1) ? 2u * f.v[i] : f.v[i];
+  uint64_t lo[10], hi[10];
+#pragma unroll
+  for (int k = 0; k < 10; k++) lo[k] = hi[k] = 0;
+#pragma unroll
+  for (int i = 0; i < 10; i++) {
+#pragma unroll
+    for (int j = 0; j < 10; j++) {
+      const int k = i + j;
+      const uint32_t a = ((i & 1) && (j & 1)) ? f2[i] : f.v[i];
+      if (k < 10) lo[k] += (uint64_t)a * g.v[j];
+      else hi[k - 10] += (uint64_t)a * g.v[j];
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 9; k++) lo[k] += 19ull * hi[k];
+  fe h = fe_carry64(lo);
+  OURO_TRK({
+    unsigned __int128 T[10] = {0};
+    for (int i = 0; i < 10; i++) {
+      if (i & 1) trk_check(2 * f.b[i] < (1ull << 32));
+      for (int j = 0; j < 10; j++) {
+        const int k = i + j;
+        unsigned __int128 x = (unsigned __int128)f.b[i] * g.b[j];
+        if ((i & 1) && (j & 1)) x *= 2;
+        if (k >= 10) x *= 19;
+        T[k % 10] += x;
+      }
+    }
+    trk_carry(h, T, (unsigned __int128)1 << 64);
+  })
+  return h;
 }
 
 // Column sums of f^2 (before carry); shared by fe_sq and fe_sq2.
-OURO_FI void fe_sq_cols(int64_t t[10], const fe& f) {
+OURO_FI void fe_sq_cols(uint64_t t[10], const fe& f) {
   OURO_COUNT_SQ();
-  OURO_CHECK_BOUNDS(f);
-  int32_t f2[10], f4[10], f19[10];
+  uint32_t f2[10], f4[10], f19[10];
 #pragma unroll
   for (int i = 0; i < 10; i++) {
-    f2[i] = 2 * f.v[i];
-    f4[i] = 4 * f.v[i];
-    f19[i] = 19 * f.v[i];
+    f2[i] = 2u * f.v[i];
+    f4[i] = 4u * f.v[i];
+    f19[i] = 19u * f.v[i];
   }
 #pragma unroll
   for (int k = 0; k < 10; k++) t[k] = 0;
@@ -203,96 +317,117 @@ OURO_FI void fe_sq_cols(int64_t t[10], const fe& f) {
     // diagonal: f_i^2 * (2 if i odd) * (19 if 2i >= 10)
     {
       const int k = 2 * i;
-      const int32_t a = (i & 1) ? f2[i] : f.v[i];
-      const int32_t b = (k >= 10) ? f19[i] : f.v[i];
-      t[k >= 10 ? k - 10 : k] += (int64_t)a * b;
+      const uint32_t a = (i & 1) ? f2[i] : f.v[i];
+      const uint32_t b = (k >= 10) ? f19[i] : f.v[i];
+      t[k >= 10 ? k - 10 : k] += (uint64_t)a * b;
     }
 #pragma unroll
     for (int j = i + 1; j < 10; j++) {
       // cross terms counted twice: 2 f_i f_j * (2 if both odd) * (19 if wrap)
       const int k = i + j;
-      const int32_t a = ((i & 1) && (j & 1)) ? f4[i] : f2[i];
-      const int32_t b = (k >= 10) ? f19[j] : f.v[j];
-      t[k >= 10 ? k - 10 : k] += (int64_t)a * b;
+      const uint32_t a = ((i & 1) && (j & 1)) ? f4[i] : f2[i];
+      const uint32_t b = (k >= 10) ? f19[j] : f.v[j];
+      t[k >= 10 ? k - 10 : k] += (uint64_t)a * b;
     }
   }
 }
 
+#if defined(OURO_TRACK_BOUNDS)
+inline void trk_sq(fe& h, const fe& f, unsigned scale) {
+  unsigned __int128 T[10] = {0};
+  for (int i = 0; i < 10; i++) {
+    trk_check(((i & 1) ? 4 : 2) * f.b[i] < (1ull << 32));
+    if (i >= 5) trk_check(19 * f.b[i] < (1ull << 32));
+    for (int j = 0; j < 10; j++) {
+      const int k = i + j;
+      unsigned __int128 x = (unsigned __int128)f.b[i] * f.b[j];
+      if ((i & 1) && (j & 1)) x *= 2;
+      if (k >= 10) x *= 19;
+      T[k % 10] += x * scale;
+    }
+  }
+  trk_carry(h, T, (unsigned __int128)1 << 64);
+}
+#endif
+
 OURO_FI fe fe_sq(const fe& f) {
-  int64_t t[10];
+  uint64_t t[10];
   fe_sq_cols(t, f);
-  return fe_carry64(t);
+  fe h = fe_carry64(t);
+  OURO_TRK(trk_sq(h, f, 1));
+  return h;
 }
 
 // 2 f^2
 OURO_FI fe fe_sq2(const fe& f) {
-  int64_t t[10];
+  uint64_t t[10];
   fe_sq_cols(t, f);
 #pragma unroll
   for (int k = 0; k < 10; k++) t[k] += t[k];
-  return fe_carry64(t);
+  fe h = fe_carry64(t);
+  OURO_TRK(trk_sq(h, f, 2));
+  return h;
 }
 
 // ---- encoding -------------------------------------------------------------
 // 256-bit little-endian words -> fe (bit 255 ignored, like fe25519_frombytes)
 OURO_FI fe fe_from_words(const uint32_t w[8]) {
   fe h;
-  h.v[0] = (int32_t)(w[0] & 0x3ffffff);
-  h.v[1] = (int32_t)(((w[0] >> 26) | (w[1] << 6)) & 0x1ffffff);
-  h.v[2] = (int32_t)(((w[1] >> 19) | (w[2] << 13)) & 0x3ffffff);
-  h.v[3] = (int32_t)(((w[2] >> 13) | (w[3] << 19)) & 0x1ffffff);
-  h.v[4] = (int32_t)((w[3] >> 6) & 0x3ffffff);
-  h.v[5] = (int32_t)(w[4] & 0x1ffffff);
-  h.v[6] = (int32_t)(((w[4] >> 25) | (w[5] << 7)) & 0x3ffffff);
-  h.v[7] = (int32_t)(((w[5] >> 19) | (w[6] << 13)) & 0x1ffffff);
-  h.v[8] = (int32_t)(((w[6] >> 12) | (w[7] << 20)) & 0x3ffffff);
-  h.v[9] = (int32_t)((w[7] >> 6) & 0x1ffffff);
-  return fe_carry(h);  // unsigned 26-bit limbs -> balanced
+  h.v[0] = w[0] & 0x3ffffff;
+  h.v[1] = ((w[0] >> 26) | (w[1] << 6)) & 0x1ffffff;
+  h.v[2] = ((w[1] >> 19) | (w[2] << 13)) & 0x3ffffff;
+  h.v[3] = ((w[2] >> 13) | (w[3] << 19)) & 0x1ffffff;
+  h.v[4] = (w[3] >> 6) & 0x3ffffff;
+  h.v[5] = w[4] & 0x1ffffff;
+  h.v[6] = ((w[4] >> 25) | (w[5] << 7)) & 0x3ffffff;
+  h.v[7] = ((w[5] >> 19) | (w[6] << 13)) & 0x1ffffff;
+  h.v[8] = ((w[6] >> 12) | (w[7] << 20)) & 0x3ffffff;
+  h.v[9] = (w[7] >> 6) & 0x1ffffff;
+  OURO_TRK(for (int i = 0; i < 10; i++) h.b[i] = limb_mask(i);)
+  return h;
 }
 
-// canonical little-endian encoding of f mod p as 8 words
+// canonical little-endian encoding of f mod p as 8 words (limbs < 2^31)
 OURO_FI void fe_to_words(uint32_t w[8], const fe& f) {
-  int32_t h[10];
+  OURO_TRK(for (int i = 0; i < 10; i++) trk_check(f.b[i] < (1ull << 31));)
+  uint32_t h[10];
 #pragma unroll
   for (int i = 0; i < 10; i++) h[i] = f.v[i];
-  // three floor-carry passes leave every limb in [0, 2^bits) with the value
-  // in [0, 2^255); the first pass absorbs any sign.
+  // three floor-carry passes leave limbs 1..9 within their masks and the
+  // value below 2^255 + 2^26
 #pragma unroll
   for (int pass = 0; pass < 3; pass++) {
-    int32_t c;
+    uint32_t c;
 #pragma unroll
     for (int i = 0; i < 9; i++) {
-      const int bits = (i & 1) ? 25 : 26;
-      c = h[i] >> bits;
-      h[i] -= c * (1 << bits);
+      c = h[i] >> limb_bits(i);
+      h[i] &= limb_mask(i);
       h[i + 1] += c;
     }
     c = h[9] >> 25;
-    h[9] -= c * (1 << 25);
+    h[9] &= limb_mask(9);
     h[0] += 19 * c;
   }
-  // subtract p if value >= p: q = (value + 19) >> 255
-  int32_t q = (h[0] + 19) >> 26;
+  // subtract p if value >= p: q = (value + 19) >> 255 (exact carry chain)
+  uint32_t q = (h[0] + 19) >> 26;
 #pragma unroll
-  for (int i = 1; i < 10; i++) q = (h[i] + q) >> ((i & 1) ? 25 : 26);
+  for (int i = 1; i < 10; i++) q = (h[i] + q) >> limb_bits(i);
   h[0] += 19 * q;
 #pragma unroll
   for (int i = 0; i < 9; i++) {
-    const int bits = (i & 1) ? 25 : 26;
-    int32_t c = h[i] >> bits;
-    h[i] -= c * (1 << bits);
+    const uint32_t c = h[i] >> limb_bits(i);
+    h[i] &= limb_mask(i);
     h[i + 1] += c;
   }
-  h[9] &= 0x1ffffff;
-  const uint32_t* u = reinterpret_cast<const uint32_t*>(h);
-  w[0] = u[0] | (u[1] << 26);
-  w[1] = (u[1] >> 6) | (u[2] << 19);
-  w[2] = (u[2] >> 13) | (u[3] << 13);
-  w[3] = (u[3] >> 19) | (u[4] << 6);
-  w[4] = u[5] | (u[6] << 25);
-  w[5] = (u[6] >> 7) | (u[7] << 19);
-  w[6] = (u[7] >> 13) | (u[8] << 12);
-  w[7] = (u[8] >> 20) | (u[9] << 6);
+  h[9] &= limb_mask(9);
+  w[0] = h[0] | (h[1] << 26);
+  w[1] = (h[1] >> 6) | (h[2] << 19);
+  w[2] = (h[2] >> 13) | (h[3] << 13);
+  w[3] = (h[3] >> 19) | (h[4] << 6);
+  w[4] = h[5] | (h[6] << 25);
+  w[5] = (h[6] >> 7) | (h[7] << 19);
+  w[6] = (h[7] >> 13) | (h[8] << 12);
+  w[7] = (h[8] >> 20) | (h[9] << 6);
 }
 
 OURO_FI bool fe_iszero(const fe& f) {

@@ -19,38 +19,46 @@ namespace ouro {
 struct ge_p2 { fe X, Y, Z; };
 struct ge_p3 { fe X, Y, Z, T; };
 struct ge_p1p1 { fe X, Y, Z, T; };
-struct ge_cached { fe YplusX, YminusX, Z, T2d; };
+struct ge_cached { fe YplusX, YminusX, Z2, T2d; };  // Z2 = 2Z
 struct ge_niels { fe yplusx, yminusx, xy2d; };
+
+// Limb-bound profile the formulas keep (unit = one reduced element, see
+// fe25519.h; the host bound tracker checks every case):
+//   p2 / p3 inputs: X <= 2, Y, Z, T <= 1 (X may be a negation)
+//   p1p1 outputs:   X <= 3, Y <= 2, Z <= 3, T <= 4
+//   cached:         Y+X <= 3, Y-X <= 3, Z2 <= 2, 2dT <= 1
+// and every product puts the narrower operand second (fe_mul's 19 g < 2^32).
 
 OURO_FI ge_p3 ge_p3_identity() { return ge_p3{fe_zero(), fe_one(), fe_one(), fe_zero()}; }
 OURO_FI ge_p2 ge_p2_identity() { return ge_p2{fe_zero(), fe_one(), fe_one()}; }
 OURO_FI ge_cached ge_cached_identity() {
-  return ge_cached{fe_one(), fe_one(), fe_one(), fe_zero()};
+  return ge_cached{fe_one(), fe_one(), fe_two(), fe_zero()};
 }
 OURO_FI ge_niels ge_niels_identity() { return ge_niels{fe_one(), fe_one(), fe_zero()}; }
 
 OURO_FI ge_p2 ge_p1p1_to_p2(const ge_p1p1& p) {
-  return ge_p2{fe_mul(p.X, p.T), fe_mul(p.Y, p.Z), fe_mul(p.Z, p.T)};
+  return ge_p2{fe_mul(p.T, p.X), fe_mul(p.Z, p.Y), fe_mul(p.T, p.Z)};
 }
 OURO_FI ge_p3 ge_p1p1_to_p3(const ge_p1p1& p) {
-  return ge_p3{fe_mul(p.X, p.T), fe_mul(p.Y, p.Z), fe_mul(p.Z, p.T), fe_mul(p.X, p.Y)};
+  return ge_p3{fe_mul(p.T, p.X), fe_mul(p.Z, p.Y), fe_mul(p.T, p.Z), fe_mul(p.X, p.Y)};
 }
 OURO_FI ge_p2 ge_p3_to_p2(const ge_p3& p) { return ge_p2{p.X, p.Y, p.Z}; }
 OURO_FI ge_cached ge_p3_to_cached(const ge_p3& p) {
-  return ge_cached{fe_add(p.Y, p.X), fe_sub(p.Y, p.X), p.Z, fe_mul(p.T, fe_d2())};
+  return ge_cached{fe_add(p.Y, p.X), fe_sub(p.Y, p.X), fe_add(p.Z, p.Z), fe_mul(p.T, fe_d2())};
 }
 
-// 2P: A = X^2, B = Y^2, C = 2Z^2; x' = 2XY / (B - A), y' = (A + B) / (C - (B - A))
+// 2P: A = X^2, B = Y^2, C = 2Z^2; x' = 2XY / (B - A), y' = (A + B) / (C - (B - A)).
+// A + B is re-normalised (fe_carry) so that X' = (X+Y)^2 - (A+B) stays within 3.
 OURO_FI ge_p1p1 ge_p2_dbl(const ge_p2& p) {
   fe A = fe_sq(p.X);
   fe B = fe_sq(p.Y);
   fe C = fe_sq2(p.Z);
   fe S = fe_sq(fe_add(p.X, p.Y));
   ge_p1p1 r;
-  r.Y = fe_add(B, A);
+  r.Y = fe_carry(fe_add(B, A));
   r.Z = fe_sub(B, A);
   r.X = fe_sub(S, r.Y);
-  r.T = fe_sub(C, r.Z);
+  r.T = fe_sub(fe_add(C, A), B);
   return r;
 }
 OURO_FI ge_p1p1 ge_p3_dbl(const ge_p3& p) { return ge_p2_dbl(ge_p3_to_p2(p)); }
@@ -62,26 +70,8 @@ OURO_FI ge_p1p1 ge_add_cached(const ge_p3& p, const ge_cached& q, bool neg) {
   fe qb = fe_select(q.YplusX, q.YminusX, neg);
   fe A = fe_mul(fe_add(p.Y, p.X), qa);
   fe B = fe_mul(fe_sub(p.Y, p.X), qb);
-  fe C = fe_mul(q.T2d, p.T);
-  fe ZZ = fe_mul(p.Z, q.Z);
-  fe D = fe_add(ZZ, ZZ);
-  fe Dp = fe_add(D, C), Dm = fe_sub(D, C);
-  ge_p1p1 r;
-  r.X = fe_sub(A, B);
-  r.Y = fe_add(A, B);
-  r.Z = fe_select(Dm, Dp, neg);
-  r.T = fe_select(Dp, Dm, neg);
-  return r;
-}
-
-// P +- Q with Q affine (niels form): the fixed-base table path
-OURO_FI ge_p1p1 ge_add_niels(const ge_p3& p, const ge_niels& q, bool neg) {
-  fe qa = fe_select(q.yminusx, q.yplusx, neg);
-  fe qb = fe_select(q.yplusx, q.yminusx, neg);
-  fe A = fe_mul(fe_add(p.Y, p.X), qa);
-  fe B = fe_mul(fe_sub(p.Y, p.X), qb);
-  fe C = fe_mul(q.xy2d, p.T);
-  fe D = fe_add(p.Z, p.Z);
+  fe C = fe_mul(p.T, q.T2d);
+  fe D = fe_mul(p.Z, q.Z2);
   fe Dp = fe_add(D, C), Dm = fe_sub(D, C);
   ge_p1p1 r;
   r.X = fe_sub(A, B);
@@ -135,7 +125,7 @@ OURO_FI bool ge_decode(ge_p3* h, const uint32_t s[8], bool negate) {
   x = fe_pow22523(x);
   x = fe_mul(fe_mul(x, v3), u);  // u v^3 (u v^7)^((p-5)/8)
   fe vxx = fe_mul(fe_sq(x), v);
-  bool m_root = fe_iszero(fe_sub(vxx, u));
+  bool m_root = fe_iszero(fe_sub4(vxx, u));
   bool p_root = fe_iszero(fe_add(vxx, u));
   x = fe_select(x, fe_mul(x, fe_sqrtm1()), m_root);
   const bool sign = (s[7] >> 31) != 0;

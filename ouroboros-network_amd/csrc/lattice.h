@@ -1,0 +1,276 @@
+// lattice.h -- half-size scalars for the Ed25519 verification equation.
+//
+// libsodium 1.0.18 accepts iff encode([S]B - [h]A) == R_bytes (SURVEY.md App.
+// B.1).  With R_bytes canonical and decodable to a point R (otherwise no
+// encoding can equal it), that is Q = [S]B - [h]A - R == O.  For any odd c1
+// with 0 < c1 < L and c0 = c1 h (mod 8L):
+//   [c1]Q = [c1 S mod L]B - [c0]A - [c1]R,
+// because B has order L and every curve point is killed by 8L; and
+// [c1]Q == O  <=>  Q == O, because ord(Q) divides 8L, L does not divide c1 and
+// no power of two divides an odd c1.  A short (c0, c1) -- about 2^127 each --
+// halves the doubling chain of the double-scalar multiplication (Pornin,
+// "Optimized lattice basis reduction in dimension 2, and fast Schnorr and
+// EdDSA signature verification", 2020, whose equation this is, extended here
+// to cofactorless verification of mixed-order keys by working modulo 8L).
+//
+// The short vector comes from a Lehmer-style half extended Euclid on
+// (8L, h): rows (r, t) with r = t h (mod 8L) are combined by exact integer
+// 2x2 steps, each derived from the leading 64 bits, so the lattice relation
+// holds by construction whatever the approximation does.  Correctness needs
+// nothing from the reduction but that relation and an odd c1, and both are
+// re-checked at the end; a candidate that fails (never seen) or is not
+// shorter than 2^250 is replaced by (h, 1), i.e. the classic full-length
+// equation.
+#pragma once
+#include "sc25519.h"
+
+namespace ouro {
+
+// 288-bit two's complement integers, little-endian words
+struct i288 {
+  uint32_t w[9];
+};
+
+OURO_FI bool i288_is_neg(const i288& a) { return (a.w[8] >> 31) != 0; }
+
+OURO_FI void i288_negate(i288& a) {
+  uint32_t c = 1;
+#pragma unroll
+  for (int i = 0; i < 9; i++) {
+    const uint32_t x = ~a.w[i];
+    a.w[i] = x + c;
+    c = (a.w[i] < x) ? 1u : 0u;
+  }
+}
+
+// a (signed 32-bit) * x  (mod 2^288)
+OURO_FI i288 i288_mul_s32(const i288& x, int32_t a) {
+  const uint32_t m = a < 0 ? (uint32_t)(-(int64_t)a) : (uint32_t)a;
+  i288 r;
+  uint64_t carry = 0;
+#pragma unroll
+  for (int i = 0; i < 9; i++) {
+    const uint64_t t = (uint64_t)x.w[i] * m + carry;
+    r.w[i] = (uint32_t)t;
+    carry = t >> 32;
+  }
+  if (a < 0) i288_negate(r);
+  return r;
+}
+
+OURO_FI i288 i288_add(const i288& x, const i288& y) {
+  i288 r;
+  uint32_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 9; i++) {
+    const uint64_t t = (uint64_t)x.w[i] + y.w[i] + c;
+    r.w[i] = (uint32_t)t;
+    c = (uint32_t)(t >> 32);
+  }
+  return r;
+}
+
+OURO_FI i288 i288_sub(const i288& x, const i288& y) {
+  i288 r;
+  uint32_t b = 0;
+#pragma unroll
+  for (int i = 0; i < 9; i++) {
+    const uint64_t t = (uint64_t)x.w[i] - y.w[i] - b;
+    r.w[i] = (uint32_t)t;
+    b = (uint32_t)(t >> 63);
+  }
+  return r;
+}
+
+// bit length of a non-negative value
+OURO_FI int i288_bitlen(const i288& a) {
+  int len = 0;
+#pragma unroll
+  for (int i = 0; i < 9; i++)
+    if (a.w[i]) len = 32 * i + 32 - __builtin_clz(a.w[i]);
+  return len;
+}
+
+// bit length of |a|
+OURO_FI int i288_abs_bitlen(const i288& a) {
+  i288 m = a;
+  if (i288_is_neg(m)) i288_negate(m);
+  return i288_bitlen(m);
+}
+
+// word i (0 <= i, wave-divergent) of a non-negative value, 0 beyond the top
+OURO_FI uint32_t i288_word(const i288& a, int i) {
+  uint32_t r = 0;
+#pragma unroll
+  for (int k = 0; k < 9; k++) r = (i == k) ? a.w[k] : r;
+  return r;
+}
+
+// bits [sh, sh + 64) of a non-negative value
+OURO_FI uint64_t i288_bits64(const i288& a, int sh) {
+  const int ws = sh >> 5, bs = sh & 31;
+  const uint32_t w0 = i288_word(a, ws), w1 = i288_word(a, ws + 1), w2 = i288_word(a, ws + 2);
+  const uint64_t lo = bs ? ((w0 >> bs) | (w1 << (32 - bs))) : w0;
+  const uint64_t hi = bs ? ((w1 >> bs) | (w2 << (32 - bs))) : w1;
+  return lo | (hi << 32);
+}
+
+OURO_FI int clz64(uint64_t x) { return __builtin_clzll(x); }
+
+OURO_FI void i288_cswap(i288& a, i288& b, bool c) {
+#pragma unroll
+  for (int i = 0; i < 9; i++) {
+    const uint32_t x = a.w[i], y = b.w[i];
+    a.w[i] = c ? y : x;
+    b.w[i] = c ? x : y;
+  }
+}
+
+// a < b for non-negative a, b
+OURO_FI bool i288_lt(const i288& a, const i288& b) { return i288_is_neg(i288_sub(a, b)); }
+
+// 8L = 2^255 + 8 (L - 2^252)
+OURO_FI i288 i288_8L() {
+  i288 r;
+  r.w[0] = 0xe7ae9f68u; r.w[1] = 0xc09318d2u; r.w[2] = 0x17bce6b2u; r.w[3] = 0xa6f7cef5u;
+  r.w[4] = 0; r.w[5] = 0; r.w[6] = 0; r.w[7] = 0x80000000u; r.w[8] = 0;
+  return r;
+}
+
+struct HalfScalars {
+  uint32_t c0[8];  // |c0|
+  uint32_t c1[8];  // c1 > 0, odd
+  bool c0_neg;
+  int bits;        // max(bitlen |c0|, bitlen c1)
+};
+
+// (c0, c1) for h < 2^253: c0 = c1 h (mod 8L), c1 odd, both short.
+OURO_HD inline void ed25519_half_scalars(HalfScalars& out, const uint32_t h[8]) {
+  i288 ru = i288_8L(), rv, tu, tv;
+#pragma unroll
+  for (int i = 0; i < 9; i++) {
+    rv.w[i] = i < 8 ? h[i] : 0u;
+    tu.w[i] = 0;
+    tv.w[i] = i == 0 ? 1u : 0u;
+  }
+  // invariant: ru >= rv >= 0, r = t h (mod 8L) for both rows
+#pragma unroll 1
+  for (int outer = 0; outer < 12; outer++) {
+    if (i288_bitlen(rv) <= 128) break;
+    const int len = i288_bitlen(ru);
+    const int sh = len > 64 ? len - 64 : 0;
+    uint64_t x = i288_bits64(ru, sh), y = i288_bits64(rv, sh);
+    // rows of the step matrix: u' = m00 u + m01 v, v' = m10 u + m11 v
+    int64_t m00 = 1, m01 = 0, m10 = 0, m11 = 1;
+    bool moved = false;
+#pragma unroll 1
+    for (int it = 0; it < 96; it++) {
+      if (y < (1ull << 32)) break;  // the leading bits are used up
+      int s = clz64(y) - clz64(x);
+      if ((y << s) > x) s--;
+      const int64_t a10 = m10 < 0 ? -m10 : m10, a11 = m11 < 0 ? -m11 : m11;
+      const int64_t a00 = m00 < 0 ? -m00 : m00, a01 = m01 < 0 ? -m01 : m01;
+      const int64_t big1 = a10 > a11 ? a10 : a11, big0 = a00 > a01 ? a00 : a01;
+      if ((big1 << s) + big0 >= (1ll << 31)) break;  // keep |m| < 2^31
+      x -= y << s;
+      m00 -= m10 * ((int64_t)1 << s);
+      m01 -= m11 * ((int64_t)1 << s);
+      moved = true;
+      if (x < y) {
+        const uint64_t tx = x; x = y; y = tx;
+        int64_t q = m00; m00 = m10; m10 = q;
+        q = m01; m01 = m11; m11 = q;
+      }
+    }
+    if (!moved) break;
+    i288 nu = i288_add(i288_mul_s32(ru, (int32_t)m00), i288_mul_s32(rv, (int32_t)m01));
+    i288 nv = i288_add(i288_mul_s32(ru, (int32_t)m10), i288_mul_s32(rv, (int32_t)m11));
+    i288 ntu = i288_add(i288_mul_s32(tu, (int32_t)m00), i288_mul_s32(tv, (int32_t)m01));
+    i288 ntv = i288_add(i288_mul_s32(tu, (int32_t)m10), i288_mul_s32(tv, (int32_t)m11));
+    // the approximation may overshoot: (-r, -t) is the same lattice vector's negative
+    if (i288_is_neg(nu)) { i288_negate(nu); i288_negate(ntu); }
+    if (i288_is_neg(nv)) { i288_negate(nv); i288_negate(ntv); }
+    const bool sw = i288_lt(nu, nv);
+    i288_cswap(nu, nv, sw);
+    i288_cswap(ntu, ntv, sw);
+    ru = nu; rv = nv; tu = ntu; tv = ntv;
+  }
+  // candidates with odd t: v, u, u + v, u - v; keep the shortest
+  i288 best_r, best_t;
+  int best = 1 << 20;
+#pragma unroll 1
+  for (int k = 0; k < 4; k++) {
+    i288 r = k == 0 ? rv : ru, t = k == 0 ? tv : tu;
+    if (k == 2) { r = i288_add(ru, rv); t = i288_add(tu, tv); }
+    if (k == 3) { r = i288_sub(ru, rv); t = i288_sub(tu, tv); }
+    if ((t.w[0] & 1u) == 0) continue;
+    const int br = i288_abs_bitlen(r), bt = i288_abs_bitlen(t);
+    const int b = br > bt ? br : bt;
+    if (b < best) { best = b; best_r = r; best_t = t; }
+  }
+  // c1 > 0
+  if (i288_is_neg(best_t)) { i288_negate(best_t); i288_negate(best_r); }
+  const bool c0_neg = i288_is_neg(best_r);
+  if (c0_neg) i288_negate(best_r);
+  // re-check c1 h = c0 (mod 8L): mod 8 on the low bits, mod L by reduction
+  bool good = best <= 250;
+  {
+    uint32_t prod[16];
+#pragma unroll
+    for (int i = 0; i < 16; i++) prod[i] = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      uint64_t carry = 0;
+#pragma unroll
+      for (int j = 0; j < 8; j++) {
+        const uint64_t t = (uint64_t)best_t.w[i] * h[j] + prod[i + j] + carry;
+        prod[i + j] = (uint32_t)t;
+        carry = t >> 32;
+      }
+      prod[i + 8] = (uint32_t)carry;
+    }
+    uint32_t a[8], b[8], c0w[8];
+#pragma unroll
+    for (int i = 0; i < 8; i++) c0w[i] = best_r.w[i];
+    sc_reduce512(a, prod);
+    sc_reduce256(b, c0w);
+    if (c0_neg) {
+      // b = L - b (or 0)
+      uint32_t l[8];
+      sc_L(l);
+      bool z = true;
+#pragma unroll
+      for (int i = 0; i < 8; i++) z = z && b[i] == 0;
+      uint32_t br = 0;
+#pragma unroll
+      for (int i = 0; i < 8; i++) {
+        const uint64_t t = (uint64_t)l[i] - b[i] - br;
+        b[i] = z ? 0u : (uint32_t)t;
+        br = (uint32_t)(t >> 63);
+      }
+    }
+    bool eq = true;
+#pragma unroll
+    for (int i = 0; i < 8; i++) eq = eq && a[i] == b[i];
+    const uint32_t low = best_t.w[0] * h[0] - (c0_neg ? (0u - best_r.w[0]) : best_r.w[0]);
+    good = good && eq && (low & 7u) == 0 && best_t.w[8] == 0 && best_r.w[8] == 0;
+  }
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    out.c0[i] = good ? best_r.w[i] : h[i];
+    out.c1[i] = good ? best_t.w[i] : (i == 0 ? 1u : 0u);
+  }
+  out.c0_neg = good && c0_neg;
+  if (!good) {
+    uint32_t hh[8];
+#pragma unroll
+    for (int i = 0; i < 8; i++) hh[i] = h[i];
+    i288 hv;
+#pragma unroll
+    for (int i = 0; i < 9; i++) hv.w[i] = i < 8 ? hh[i] : 0u;
+    best = i288_bitlen(hv);
+  }
+  out.bits = best;
+}
+
+}  // namespace ouro

@@ -43,24 +43,27 @@ constexpr int kNielsWords = 32;                   // 30 used, padded for 16-B lo
 constexpr int kBTabWords = 2 * kBTabEntries * kNielsWords;
 
 // ---- vector load/store helpers ---------------------------------------------
+// (the host bound tracker of fe25519.h follows elements through memory)
 OURO_FI void st_fe(int32_t* p, const fe& f) {
   int4* q = reinterpret_cast<int4*>(p);
   // 10 words: store as 2 x int4 + int2
   q[0] = make_int4(f.v[0], f.v[1], f.v[2], f.v[3]);
   q[1] = make_int4(f.v[4], f.v[5], f.v[6], f.v[7]);
   reinterpret_cast<int2*>(p + 8)[0] = make_int2(f.v[8], f.v[9]);
+  OURO_TRK(ouro_trk_store(p, f.b));
 }
 OURO_FI fe ld_fe(const int32_t* p) {
   const int4* q = reinterpret_cast<const int4*>(p);
   int4 a = q[0], b = q[1];
   int2 c = reinterpret_cast<const int2*>(p + 8)[0];
-  fe f = OURO_FE(a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w, c.x, c.y);
+  fe f = fe_make(a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w, c.x, c.y);
+  OURO_TRK(ouro_trk_load(p, f.b));
   return f;
 }
 // cached point: 40 words = 10 x int4, fe k at words [10k, 10k+10)
 OURO_FI void st_cached(int32_t* p, const ge_cached& c) {
   int4* q = reinterpret_cast<int4*>(p);
-  const int32_t* s[4] = {c.YplusX.v, c.YminusX.v, c.Z.v, c.T2d.v};
+  const uint32_t* s[4] = {c.YplusX.v, c.YminusX.v, c.Z2.v, c.T2d.v};
   int32_t w[40];
 #pragma unroll
   for (int k = 0; k < 4; k++)
@@ -68,6 +71,8 @@ OURO_FI void st_cached(int32_t* p, const ge_cached& c) {
     for (int i = 0; i < 10; i++) w[10 * k + i] = s[k][i];
 #pragma unroll
   for (int i = 0; i < 10; i++) q[i] = make_int4(w[4 * i], w[4 * i + 1], w[4 * i + 2], w[4 * i + 3]);
+  OURO_TRK(ouro_trk_store(p, c.YplusX.b); ouro_trk_store(p + 10, c.YminusX.b);
+           ouro_trk_store(p + 20, c.Z2.b); ouro_trk_store(p + 30, c.T2d.b);)
 }
 OURO_FI ge_cached ld_cached(const int32_t* p) {
   const int4* q = reinterpret_cast<const int4*>(p);
@@ -82,9 +87,11 @@ OURO_FI ge_cached ld_cached(const int32_t* p) {
   for (int i = 0; i < 10; i++) {
     c.YplusX.v[i] = w[i];
     c.YminusX.v[i] = w[10 + i];
-    c.Z.v[i] = w[20 + i];
+    c.Z2.v[i] = w[20 + i];
     c.T2d.v[i] = w[30 + i];
   }
+  OURO_TRK(ouro_trk_load(p, c.YplusX.b); ouro_trk_load(p + 10, c.YminusX.b);
+           ouro_trk_load(p + 20, c.Z2.b); ouro_trk_load(p + 30, c.T2d.b);)
   return c;
 }
 OURO_FI ge_niels ld_niels(const int32_t* p) {
@@ -102,6 +109,8 @@ OURO_FI ge_niels ld_niels(const int32_t* p) {
     n.yminusx.v[i] = w[10 + i];
     n.xy2d.v[i] = w[20 + i];
   }
+  OURO_TRK(ouro_trk_load(p, n.yplusx.b); ouro_trk_load(p + 10, n.yminusx.b);
+           ouro_trk_load(p + 20, n.xy2d.b);)
   return n;
 }
 OURO_FI void st_words8(int32_t* p, const uint32_t w[8]) {
@@ -192,7 +201,7 @@ OURO_NI void dsm(int32_t* lane, const int32_t* btab, uint32_t cfg) {
       } else {
         const int base = src == 3 ? kBTabEntries : 0;
         ge_niels nq = ld_niels(btab + (base + idx) * kNielsWords);
-        q = ge_cached{nq.yplusx, nq.yminusx, fe_one(), nq.xy2d};
+        q = ge_cached{nq.yplusx, nq.yminusx, fe_two(), nq.xy2d};
       }
       if (mag == 0) q = ge_cached_identity();
       t = ge_add_cached(ge_p1p1_to_p3(t), q, neg);
@@ -294,14 +303,14 @@ OURO_HD inline ge_p3 elligator2_h(const uint32_t r[8]) {
   fe D = fe_carry(fe_add(fe_add(r2, r2), one));         // 1 + 2 r^2 (re-balanced:
                                                         // n = Xn - D below sums 4 terms)
   fe A2r2 = fe_mul(fe_mul(A, A), r2);                   // A^2 r^2
-  fe W = fe_sub(fe_sq(D), fe_add(A2r2, A2r2));          // D^2 - 2 A^2 r^2
-  fe e = fe_neg(fe_mul(fe_mul(A, W), D));               // -A W D
+  fe W = fe_sub4(fe_sq(D), fe_add(A2r2, A2r2));         // D^2 - 2 A^2 r^2
+  fe e = fe_neg(fe_mul(fe_mul(W, A), D));               // -A W D
   fe chi = fe_mul(fe_sq(fe_sq(fe_pow22523(e))), fe_sq(e));  // e^((p-1)/2)
   uint32_t cw[8];
   fe_to_words(cw, chi);
   const bool e_is_minus_1 = (cw[0] >> 8) & 1;  // libsodium's byte-1 test
   fe Ar2 = fe_mul(A, r2);
-  fe Xn = fe_carry(fe_select(fe_neg(fe_add(Ar2, Ar2)), fe_neg(A), e_is_minus_1));
+  fe Xn = fe_carry(fe_select(fe_neg4(fe_add(Ar2, Ar2)), fe_neg(A), e_is_minus_1));
   fe n = fe_sub(Xn, D), m = fe_add(Xn, D);
   // x = sqrt(u / v), u = n^2 - m^2, v = d n^2 + m^2
   fe n2 = fe_sq(n), m2 = fe_sq(m);
@@ -310,10 +319,11 @@ OURO_HD inline ge_p3 elligator2_h(const uint32_t r[8]) {
   fe v3 = fe_mul(fe_sq(v), v);
   fe x = fe_mul(fe_mul(u, v3), fe_pow22523(fe_mul(fe_mul(fe_sq(v3), v), u)));
   fe vxx = fe_mul(fe_sq(x), v);
-  const bool m_root = fe_iszero(fe_sub(vxx, u));
+  const bool m_root = fe_iszero(fe_sub4(vxx, u));
   x = fe_select(x, fe_mul(x, fe_sqrtm1()), m_root);
   x = fe_select(fe_neg(x), x, fe_isnegative(x));  // sign bit 0: even x
-  ge_p3 P{fe_mul(x, m), n, m, fe_mul(x, n)};
+  const fe nc = fe_carry(n);
+  ge_p3 P{fe_mul(x, m), nc, m, fe_mul(x, nc)};
   return ge_mul8(P);
 }
 
@@ -326,13 +336,13 @@ OURO_HD inline ge_p3 elligator2_h_ref(const uint32_t r[8]) {
   fe den = fe_add(fe_sq2(rr), one);          // 1 + 2 r^2
   fe x = fe_neg(fe_mul(A, fe_invert(den)));  // -A / (1 + 2 r^2)
   fe x2 = fe_sq(x);
-  fe e = fe_add(fe_add(fe_mul(x, x2), x), fe_mul(x2, A));  // x^3 + A x^2 + x
+  fe e = fe_carry(fe_add(fe_add(fe_mul(x, x2), x), fe_mul(x2, A)));  // x^3 + A x^2 + x
   // chi(e) = e^((p-1)/2) = (e^(2^252-3))^4 e^2
   fe chi = fe_mul(fe_sq(fe_sq(fe_pow22523(e))), fe_sq(e));
   uint32_t cw[8];
   fe_to_words(cw, chi);
   const bool e_is_minus_1 = (cw[0] >> 8) & 1;  // byte 1, bit 0 (libsodium's test)
-  x = fe_select(fe_sub(fe_neg(x), A), x, e_is_minus_1);
+  x = fe_carry(fe_select(fe_sub(fe_neg(x), A), x, e_is_minus_1));
   // y_ed = (x - 1) / (x + 1), decoded with sign 0, then cleared of the cofactor
   fe yed = fe_mul(fe_sub(x, one), fe_invert(fe_add(x, one)));
   uint32_t yw[8];
@@ -526,6 +536,7 @@ OURO_HD inline void build_btab_one(int32_t* out, const ge_p3& G) {
       e[10 + i] = ym.v[i];
       e[20 + i] = xy2d.v[i];
     }
+    OURO_TRK(ouro_trk_store(e, yp.b); ouro_trk_store(e + 10, ym.b); ouro_trk_store(e + 20, xy2d.b);)
     e[30] = 0;
     e[31] = 0;
   }

@@ -56,13 +56,15 @@ def test_field_ops(dh):
 
 
 def test_tobytes_canonicalises_unreduced_limbs(dh):
-    """fe_to_words on limb vectors at and beyond the 'reduced' bounds."""
+    """fe_to_words on unsigned limb vectors at and beyond the 'reduced' bounds
+    (anything below 2^31 per limb)."""
     rng = np.random.default_rng(1)
     E = [0, 26, 51, 77, 102, 128, 153, 179, 204, 230]
     out = ctypes.create_string_buffer(32)
     for _ in range(500):
-        limbs = [int(rng.integers(-(3 << 25), 3 << 25)) for _ in range(10)]
-        arr = (ctypes.c_int32 * 10)(*limbs)
+        top = int(rng.choice([1 << 26, 1 << 28, 1 << 31]))
+        limbs = [int(rng.integers(0, top)) for _ in range(10)]
+        arr = (ctypes.c_uint32 * 10)(*limbs)
         dh.dh_fe_limbs_tobytes(out, arr)
         want = sum(l << E[i] for i, l in enumerate(limbs)) % P
         assert dec(out.raw) == want

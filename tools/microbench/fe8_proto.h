@@ -351,6 +351,62 @@ F8I fe10u sq10u(const fe10u& f) {
   return carry64u(t);
 }
 
+// Deferred-19 variants: wrapped columns (i + j >= 10) accumulate unscaled in
+// hi[], then lo[k] += 19 hi[k] once per column.  No operand is pre-multiplied
+// by 19, so the only input constraint is the column sum (< 2^64).
+F8I fe10u mul10d(const fe10u& f, const fe10u& g) {
+  uint32_t f2[10];
+#pragma unroll
+  for (int i = 0; i < 10; i++) f2[i] = (i & 1) ? 2u * f.v[i] : f.v[i];
+  uint64_t lo[10], hi[10];
+#pragma unroll
+  for (int k = 0; k < 10; k++) lo[k] = hi[k] = 0;
+#pragma unroll
+  for (int i = 0; i < 10; i++) {
+#pragma unroll
+    for (int j = 0; j < 10; j++) {
+      const int k = i + j;
+      const uint32_t a = ((i & 1) && (j & 1)) ? f2[i] : f.v[i];
+      if (k < 10) lo[k] += (uint64_t)a * g.v[j];
+      else hi[k - 10] += (uint64_t)a * g.v[j];
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 9; k++) lo[k] += 19ull * hi[k];
+  return carry64u(lo);
+}
+
+F8I fe10u sq10d(const fe10u& f) {
+  uint32_t f2[10], f4[10];
+#pragma unroll
+  for (int i = 0; i < 10; i++) {
+    f2[i] = 2u * f.v[i];
+    f4[i] = 4u * f.v[i];
+  }
+  uint64_t lo[10], hi[10];
+#pragma unroll
+  for (int k = 0; k < 10; k++) lo[k] = hi[k] = 0;
+#pragma unroll
+  for (int i = 0; i < 10; i++) {
+    {
+      const int k = 2 * i;
+      const uint32_t a = (i & 1) ? f2[i] : f.v[i];
+      if (k < 10) lo[k] += (uint64_t)a * f.v[i];
+      else hi[k - 10] += (uint64_t)a * f.v[i];
+    }
+#pragma unroll
+    for (int j = i + 1; j < 10; j++) {
+      const int k = i + j;
+      const uint32_t a = ((i & 1) && (j & 1)) ? f4[i] : f2[i];
+      if (k < 10) lo[k] += (uint64_t)a * f.v[j];
+      else hi[k - 10] += (uint64_t)a * f.v[j];
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 9; k++) lo[k] += 19ull * hi[k];
+  return carry64u(lo);
+}
+
 F8I fe10u from_words10u(const uint32_t w[8]) {
   ouro::fe s = ouro::fe_from_words(w);  // balanced -> carry to unsigned
   uint64_t t[10];

@@ -54,7 +54,7 @@ __global__ void __launch_bounds__(256, 2) kvar(const uint32_t* in, uint32_t* out
     }
     ouro::fe_to_words(w1, x);
     ouro::fe_to_words(w2, z);
-  } else if constexpr (V == 7 || V == 8) {
+  } else if constexpr (V == 7 || V == 8 || V == 9 || V == 10) {
     fe8p::fe10u x = fe8p::from_words10u(a), y = fe8p::from_words10u(b), z = fe8p::from_words10u(c);
     fe8p::fe10u w = y;
 #pragma unroll 1
@@ -62,6 +62,12 @@ __global__ void __launch_bounds__(256, 2) kvar(const uint32_t* in, uint32_t* out
       if constexpr (V == 7) {
         fe8p::fe10u t = fe8p::mul10u(x, y), u = fe8p::mul10u(z, w);
         x = y; y = t; z = w; w = u;
+      } else if constexpr (V == 9) {
+        fe8p::fe10u t = fe8p::mul10d(x, y), u = fe8p::mul10d(z, w);
+        x = y; y = t; z = w; w = u;
+      } else if constexpr (V == 10) {
+        x = fe8p::sq10d(x);
+        z = fe8p::sq10d(z);
       } else {
         x = fe8p::sq10u(x);
         z = fe8p::sq10u(z);
@@ -135,10 +141,11 @@ int main(int argc, char** argv) {
   CHECK(hipMalloc(&din, h.size() * 4));
   CHECK(hipMalloc(&dout, 16 * n * 4));
   CHECK(hipMemcpy(din, h.data(), h.size() * 4, hipMemcpyHostToDevice));
-  const char* names[9] = {"fe10_mul", "fe8_mul_asm", "fe8_mul_c", "fe10_sq", "fe8_sq_asm",
-                          "fe8_mul_opscan", "fe8_mul_opscan_c", "fe10u_mul", "fe10u_sq"};
-  std::vector<std::vector<uint32_t>> res(9, std::vector<uint32_t>(16 * n));
-  float ms[9];
+  const char* names[11] = {"fe10_mul", "fe8_mul_asm", "fe8_mul_c", "fe10_sq", "fe8_sq_asm",
+                           "fe8_mul_opscan", "fe8_mul_opscan_c", "fe10u_mul", "fe10u_sq",
+                           "fe10d_mul", "fe10d_sq"};
+  std::vector<std::vector<uint32_t>> res(11, std::vector<uint32_t>(16 * n));
+  float ms[11];
   for (int round = 0; round < 2; round++) {
     ms[0] = run<0>(din, dout, n, 3);
     CHECK(hipMemcpy(res[0].data(), dout, 16 * n * 4, hipMemcpyDeviceToHost));
@@ -158,13 +165,18 @@ int main(int argc, char** argv) {
     CHECK(hipMemcpy(res[7].data(), dout, 16 * n * 4, hipMemcpyDeviceToHost));
     ms[8] = run<8>(din, dout, n, 3);
     CHECK(hipMemcpy(res[8].data(), dout, 16 * n * 4, hipMemcpyDeviceToHost));
+    ms[9] = run<9>(din, dout, n, 3);
+    CHECK(hipMemcpy(res[9].data(), dout, 16 * n * 4, hipMemcpyDeviceToHost));
+    ms[10] = run<10>(din, dout, n, 3);
+    CHECK(hipMemcpy(res[10].data(), dout, 16 * n * 4, hipMemcpyDeviceToHost));
   }
-  const bool mul_eq = res[0] == res[1] && res[0] == res[2] && res[0] == res[5] && res[0] == res[6] && res[0] == res[7];
-  const bool sq_eq = res[3] == res[4] && res[3] == res[8];
+  const bool mul_eq = res[0] == res[1] && res[0] == res[2] && res[0] == res[5] && res[0] == res[6] && res[0] == res[7] &&
+                      res[0] == res[9];
+  const bool sq_eq = res[3] == res[4] && res[3] == res[8] && res[3] == res[10];
   const double ops = 2.0 * ITERS * n;
   printf("{\"lanes\": %zu, \"iters\": %d, \"mul_equal\": %s, \"sq_equal\": %s", n, ITERS,
          mul_eq ? "true" : "false", sq_eq ? "true" : "false");
-  for (int v = 0; v < 9; v++)
+  for (int v = 0; v < 11; v++)
     printf(", \"%s\": {\"ms\": %.3f, \"Gops\": %.2f}", names[v], ms[v], ops / (ms[v] * 1e-3) / 1e9);
   printf("}\n");
   return (mul_eq && sq_eq) ? 0 : 1;
