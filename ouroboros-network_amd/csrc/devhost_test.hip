@@ -158,6 +158,17 @@ void dh_elligator2_ref(uint8_t* out, const uint8_t* r32) {
   ge_encode_with_inv(enc, H.X, H.Y, fe_invert(H.Z));
   memcpy(out, enc, 32);
 }
+// lattice.h: (|c0|, c1, sign of c0) for h (32 bytes, < 2^253); returns the bit size
+int dh_half_scalars(const uint8_t* h32, uint8_t* c0, uint8_t* c1, int* c0_neg) {
+  uint32_t h[8];
+  bytes_to_words8(h, h32);
+  HalfScalars hs;
+  ed25519_half_scalars(hs, h);
+  memcpy(c0, hs.c0, 32);
+  memcpy(c1, hs.c1, 32);
+  *c0_neg = hs.c0_neg ? 1 : 0;
+  return hs.bits;
+}
 int dh_ed25519_verify(const uint8_t* sig, const uint8_t* m, uint32_t mlen, const uint8_t* pk) {
   uint32_t s[16], p[8];
   for (int i = 0; i < 16; i++) s[i] = ld_le32(sig + 4 * i);

@@ -163,9 +163,13 @@ OURO_HD inline void ed25519_half_scalars(HalfScalars& out, const uint32_t h[8]) 
     // rows of the step matrix: u' = m00 u + m01 v, v' = m10 u + m11 v
     int64_t m00 = 1, m01 = 0, m10 = 0, m11 = 1;
     bool moved = false;
+    // stop when the leading bits are used up (y < 2^32) or when r_v crosses
+    // 2^128 (y < 2^(128 - sh)), so that u stays the last remainder above it
+    // (sh >= 65 here: r_u > r_v > 2^128)
+    const int ybits = 128 - sh > 32 ? 128 - sh : 32;
 #pragma unroll 1
     for (int it = 0; it < 96; it++) {
-      if (y < (1ull << 32)) break;  // the leading bits are used up
+      if (y < (1ull << ybits)) break;
       int s = clz64(y) - clz64(x);
       if ((y << s) > x) s--;
       const int64_t a10 = m10 < 0 ? -m10 : m10, a11 = m11 < 0 ? -m11 : m11;

@@ -5,10 +5,11 @@
 //   OCERT   : Ed25519 by the cold key over hotVk || BE64(n) || BE64(c0),
 //             Sum6KES by hotVk over the raw header body
 //   OVERLAY : draft-03 VRF verify + output for the eta and leader seeds
-// Each check is split into a *core* that ends in projective points and one
-// shared *finish* that inverts all ten Z coordinates with a single field
-// inversion (Montgomery's trick) and then does every encoding, comparison and
-// hash.  The cores are independent, so the same code runs
+// Each check is a *core*: the two Ed25519 checks end in their verdict (the
+// half-size equation of lattice.h compares with the identity projectively);
+// the VRF cores end in projective points, and one shared *finish* inverts all
+// eight Z coordinates with a single field inversion (Montgomery's trick) and
+// then does every encoding, comparison and hash.  The cores are independent, so the same code runs
 //   * throughput mode: one lane runs all six cores of a header, the VRF key is
 //     decoded once and its [1..8](-Y) table serves both U computations;
 //   * latency mode (64-header ChainSync windows): six lanes per header run the
@@ -22,11 +23,10 @@
 namespace ouro {
 
 // ---- per-header result record (int32 words) --------------------------------
-enum HdrPoint { kPtR1 = 0, kPtR2, kPtHe, kPtUe, kPtVe, kPtG8e, kPtHl, kPtUl, kPtVl, kPtG8l,
-                kHdrPoints };
+enum HdrPoint { kPtHe = 0, kPtUe, kPtVe, kPtG8e, kPtHl, kPtUl, kPtVl, kPtG8l, kHdrPoints };
 constexpr int kPtWords = 36;                          // X, Y, Z at a 12-word stride
 constexpr int kResFlags = kHdrPoints * kPtWords;      // 6 flag words, one per core
-constexpr int kResWords = kResFlags + 8;              // 368 words (16-B multiple)
+constexpr int kResWords = kResFlags + 8;              // 296 words (16-B multiple)
 enum HdrCore { kCoreOcert = 0, kCoreKes, kCoreUe, kCoreUl, kCoreVe, kCoreVl, kHdrCores };
 // flag bits
 constexpr int32_t kFlagOk = 1;        // the core's acceptance checks passed
@@ -175,10 +175,9 @@ OURO_HD inline bool vrf_finish(uint32_t beta[16], const uint32_t Henc[8], const 
   return ceq;
 }
 
-// One inversion for all ten Z; tmp = 10 x 12 scratch words.  Then every
+// One inversion for all eight Z; tmp = 8 x 12 scratch words.  Then every
 // comparison and hash.  Returns the OURO_HDR_* verdict bits.
-OURO_HD inline uint32_t hdr_finish(const int32_t* res, int32_t* tmp, const uint32_t R1[8],
-                                   const uint32_t R2[8], const uint32_t pie[20],
+OURO_HD inline uint32_t hdr_finish(const int32_t* res, int32_t* tmp, const uint32_t pie[20],
                                    const uint32_t pil[20], uint32_t beta_e[16],
                                    uint32_t beta_l[16]) {
   // prefix products P_k = Z_0 ... Z_k
@@ -205,14 +204,8 @@ OURO_HD inline uint32_t hdr_finish(const int32_t* res, int32_t* tmp, const uint3
                        ld_fe(tmp + 12 * k));
   const int32_t* fl = res + kResFlags;
   uint32_t v = 0;
-  bool e1 = true, e2 = true;
-#pragma unroll
-  for (int i = 0; i < 8; i++) {
-    e1 = e1 && enc[kPtR1][i] == R1[i];
-    e2 = e2 && enc[kPtR2][i] == R2[i];
-  }
-  if ((fl[kCoreOcert] & kFlagOk) && e1) v |= 0x01u;
-  if ((fl[kCoreKes] & kFlagOk) && e2) v |= 0x02u;
+  if (fl[kCoreOcert] & kFlagOk) v |= 0x01u;
+  if (fl[kCoreKes] & kFlagOk) v |= 0x02u;
 #pragma unroll 1
   for (int which = 0; which < 2; which++) {
     const uint32_t* pi = which ? pil : pie;
@@ -263,17 +256,15 @@ OURO_HD inline void hdr_core(const ouro_tpraos_batch& b, size_t i, int core,
       ld_words(hv, b.hot_vk + 32 * i, 2);
       OcertMsg m;
       ocert_msg(m, hv, b.ocert_counter[i], b.ocert_kes_period[i]);
-      flag = ed25519_core(s, p, m, 48, lane, btab) ? kFlagOk : 0;
-      st_point_from_dsm(res, kPtR1, lane);
+      flag = ed25519_verify_lane(s, p, m, 48, lane, btab) ? kFlagOk : 0;
       break;
     }
     case kCoreKes: {
       uint32_t hv[8];
       ld_words(hv, b.hot_vk + 32 * i, 2);
       const uint32_t* sw = reinterpret_cast<const uint32_t*>(b.kes_sig + 448 * i);
-      flag = sum6kes_core(hv, b.kes_t[i], sw, ShaGlobalTail{b.body + b.body_off[i]},
-                          b.body_len[i], lane, btab) ? kFlagOk : 0;
-      st_point_from_dsm(res, kPtR2, lane);
+      flag = sum6kes_verify_lane(hv, b.kes_t[i], sw, ShaGlobalTail{b.body + b.body_off[i]},
+                                 b.body_len[i], lane, btab) ? kFlagOk : 0;
       break;
     }
     case kCoreUe:
@@ -307,12 +298,10 @@ OURO_HD inline void hdr_finish_item(const ouro_tpraos_batch& b, size_t i,
                                                 const int32_t* res, int32_t* tmp,
                                                 uint8_t* verdict, uint8_t* beta_eta,
                                                 uint8_t* beta_leader) {
-  uint32_t R1[8], R2[8], pie[20], pil[20], be[16], bl[16];
-  ld_words(R1, b.ocert_sigma + 64 * i, 2);
-  ld_words(R2, b.kes_sig + 448 * i, 2);
+  uint32_t pie[20], pil[20], be[16], bl[16];
   ld_words(pie, b.eta_proof + 80 * i, 5);
   ld_words(pil, b.leader_proof + 80 * i, 5);
-  const uint32_t v = hdr_finish(res, tmp, R1, R2, pie, pil, be, bl);
+  const uint32_t v = hdr_finish(res, tmp, pie, pil, be, bl);
   if (beta_eta) st_words(beta_eta + 64 * i, be, 4);
   if (beta_leader) st_words(beta_leader + 64 * i, bl, 4);
   verdict[i] = (uint8_t)v;

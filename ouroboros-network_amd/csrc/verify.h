@@ -19,6 +19,7 @@
 #pragma once
 #include "blake2b.h"
 #include "ge25519.h"
+#include "lattice.h"
 #include "sc25519.h"
 #include "sha512.h"
 
@@ -218,30 +219,54 @@ OURO_FI ge_p2 dsm_result(const int32_t* lane) {
 }
 
 // ---- Ed25519 ------------------------------------------------------------------
+// Largest x over the wave's active lanes (ballots honour EXEC, so lanes that
+// left the grid-stride loop do not contribute); identity on the host.
+OURO_FI int wave_max_small(int x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  int m = 0;
+#pragma unroll
+  for (int b = 6; b >= 0; b--) {
+    const int trial = m | (1 << b);
+    if (__ballot(x >= trial) != 0) m = trial;
+  }
+  return m;
+#else
+  return x;
+#endif
+}
+
 // sig = R || S (16 words), pk (8 words), message bytes from global memory.
-// ed25519_core runs the acceptance checks and leaves R' = [h](-A) + [S]B (p2)
-// in lane[kSlotOut]; the verdict is core && encode(R') == R.
+// Accepts iff libsodium 1.0.18 does (App. B.1) -- or, for ByronDSIGN, the
+// donna-derived cardano-crypto rule (App. B.5) -- through the equivalent
+// half-size equation of lattice.h:
+//   R_bytes canonical, decodable, x = 0 only with sign 0, and
+//   [c1 S mod L]B + [c0](-A) + [c1](-R) == O,  c0 = c1 h (mod 8L), c1 odd,
+// with h = SHA-512(R || A || M) mod L.  The doubling chain is ~130 bits
+// instead of 253, and no inversion is needed: the result is compared to the
+// identity projectively.
 template <class Tail>
-OURO_HD inline bool ed25519_core(const uint32_t sig[16], const uint32_t pk[8], const Tail& msg,
-                                 uint32_t mlen, int32_t* lane, const int32_t* btab,
-                                 bool byron = false) {
+OURO_HD inline bool ed25519_verify_lane(const uint32_t sig[16], const uint32_t pk[8],
+                                        const Tail& msg, uint32_t mlen, int32_t* lane,
+                                        const int32_t* btab, bool byron = false) {
   uint32_t R[8], S[8];
 #pragma unroll
   for (int i = 0; i < 8; i++) {
     R[i] = sig[i];
     S[i] = sig[8 + i];
   }
-  // libsodium 1.0.18 (App. B.1) or, for ByronDSIGN, the donna-derived
-  // cardano-crypto rule (App. B.5): only the top three bits of S are checked
   bool ok;
   if (byron) {
-    ok = (S[7] >> 29) == 0;
+    ok = (S[7] >> 29) == 0;  // only the top three bits of S
   } else {
     ok = sc_is_canonical(S) && !ge_has_small_order(R);
     ok = ok && ge_is_canonical(pk) && !ge_has_small_order(pk);
   }
-  ge_p3 negA;
+  ge_p3 negA, negR;
   ok = ge_decode(&negA, pk, true) && ok;
+  // encode(R') == R_bytes  <=>  R_bytes is the canonical encoding of R' (a point)
+  ok = ge_is_canonical(R) && ok;
+  ok = ge_decode(&negR, R, true) && ok;
+  ok = ok && !(fe_iszero(negR.X) && (R[7] >> 31) != 0);
   // h = SHA-512(R || A || M) mod L
   uint32_t pre[16];
 #pragma unroll
@@ -254,28 +279,41 @@ OURO_HD inline bool ed25519_core(const uint32_t sig[16], const uint32_t pk[8], c
   uint32_t hw[16], h[8];
   sha512_digest_words(hw, H);
   sc_reduce512(h, hw);
-  // R' = [h](-A) + [S]B
-  build_table(lane + kSlotTab1, negA);
-  st_words8(lane + kSlotA1, h);
-  st_words8(lane + kSlotB, S);
-  uint64_t* carr = reinterpret_cast<uint64_t*>(lane + kSlotCarry);
-  carr[0] = sc_recode_carries<4, 64>(h);
-  carr[2] = sc_recode_carries<8, 32>(S);
-  dsm(lane, btab, dsm_cfg(64, 0, true));
-  return ok;
-}
-
-template <class Tail>
-OURO_HD inline bool ed25519_verify_lane(const uint32_t sig[16], const uint32_t pk[8],
-                                        const Tail& msg, uint32_t mlen, int32_t* lane,
-                                        const int32_t* btab, bool byron = false) {
-  const bool ok = ed25519_core(sig, pk, msg, mlen, lane, btab, byron);
-  uint32_t enc[8];
-  ge_p2_encode(enc, dsm_result(lane));
-  bool eq = true;
+  HalfScalars hs;
+  ed25519_half_scalars(hs, h);
+  // b = c1 S mod L
+  uint32_t prod[16], b[8];
 #pragma unroll
-  for (int i = 0; i < 8; i++) eq = eq && enc[i] == sig[i];
-  return ok && eq;
+  for (int i = 0; i < 16; i++) prod[i] = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    uint64_t carry = 0;
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+      const uint64_t t = (uint64_t)hs.c1[i] * S[j] + prod[i + j] + carry;
+      prod[i + j] = (uint32_t)t;
+      carry = t >> 32;
+    }
+    prod[i + 8] = (uint32_t)carry;
+  }
+  sc_reduce512(b, prod);
+  // [|c0|](+-A) + [c1](-R) + [b]B, one ~130-bit doubling chain
+  build_table(lane + kSlotTab1, hs.c0_neg ? ge_p3_neg(negA) : negA);
+  build_table(lane + kSlotTab2, negR);
+  st_words8(lane + kSlotA1, hs.c0);
+  st_words8(lane + kSlotA2, hs.c1);
+  st_words8(lane + kSlotB, b);
+  uint64_t* carr = reinterpret_cast<uint64_t*>(lane + kSlotCarry);
+  carr[0] = sc_recode_carries<4, 64>(hs.c0);
+  carr[1] = sc_recode_carries<4, 64>(hs.c1);
+  carr[2] = sc_recode_carries<8, 32>(b);
+  // windows so that every scalar is < 2^(4 nw - 1) (top carry zero), <= 64
+  int nw = wave_max_small((hs.bits + 4) >> 2);
+  nw = nw < 1 ? 1 : (nw > 64 ? 64 : nw);
+  dsm(lane, btab, dsm_cfg(nw, nw, true, true, 0, 1));
+  const ge_p2 Q = dsm_result(lane);
+  const bool ident = fe_iszero(Q.X) && fe_iszero(fe_sub(Q.Y, Q.Z));
+  return ok && ident;
 }
 
 // ---- ECVRF-ED25519-SHA512-Elligator2 (draft-03) -------------------------------
@@ -471,7 +509,7 @@ OURO_HD inline bool vrf03_verify_lane(uint32_t beta[16], const uint32_t pk[8],
 // ---- Sum6KES --------------------------------------------------------------------
 // sig (448 B) is read from global memory: leaf signature, then (vk0, vk1) for
 // levels 1..6 bottom-up; verification walks top-down from the root vk.
-template <class Tail, bool with_compare = true>
+template <class Tail>
 OURO_HD inline bool sum6kes_verify_lane(const uint32_t vk[8], uint32_t t, const uint32_t* sigw,
                                         const Tail& msg, uint32_t mlen, int32_t* lane,
                                         const int32_t* btab) {
@@ -505,18 +543,8 @@ OURO_HD inline bool sum6kes_verify_lane(const uint32_t vk[8], uint32_t t, const 
     uint4 v = s4[i];
     sig[4 * i] = v.x; sig[4 * i + 1] = v.y; sig[4 * i + 2] = v.z; sig[4 * i + 3] = v.w;
   }
-  if (!with_compare) return ed25519_core(sig, cur, msg, mlen, lane, btab) && ok;
   const bool leaf = ed25519_verify_lane(sig, cur, msg, mlen, lane, btab);
   return ok && leaf;
-}
-
-// Merkle walk + the leaf's Ed25519 core (R' left in lane[kSlotOut]); the
-// header kernel compares the encoding after its shared batch inversion.
-template <class Tail>
-OURO_HD inline bool sum6kes_core(const uint32_t vk[8], uint32_t t, const uint32_t* sigw,
-                                 const Tail& msg, uint32_t mlen, int32_t* lane,
-                                 const int32_t* btab) {
-  return sum6kes_verify_lane<Tail, false>(vk, t, sigw, msg, mlen, lane, btab);
 }
 
 // ---- fixed-base tables (host side, computed once per process) ----------------

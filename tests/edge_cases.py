@@ -58,6 +58,57 @@ SMALL_Y = [0, 1, Y8, P - Y8, P - 1, P, P + 1]
 T8 = (recover_x(Y8, 0), Y8)  # an order-8 point
 
 
+def smul(k: int, pt):
+    """[k]pt by double-and-add (exact, slow; test data only)."""
+    acc = (0, 1)
+    while k:
+        if k & 1:
+            acc = add(acc, pt)
+        pt = add(pt, pt)
+        k >>= 1
+    return acc
+
+
+BASE = (recover_x(4 * pow(5, P - 2, P) % P, 0), 4 * pow(5, P - 2, P) % P)
+
+
+def torsion_consistent_cases(per_order: int = 2):
+    """Signatures over a mixed-order key A = aB + T_A whose R carries exactly
+    the torsion -[h]T_A, so that [S]B - [h]A == R holds exactly: cofactorless
+    verification (libsodium 1.0.18) accepts them, and a verifier that reduced
+    the coefficient of A modulo L instead of 8L would not.  Also the same
+    signatures with R's torsion off by one step (rejected).  T_A of order 2, 4
+    and 8.  [(pk, sig, msg)]"""
+    out = []
+    rng_seed = 0
+    for k in (4, 2, 1):  # [k]T8 has order 8 / k
+        TA = smul(k, T8)
+        made = 0
+        while made < per_order:
+            rng_seed += 1
+            a = int.from_bytes(hashlib.sha512(b"tors-a%d" % rng_seed).digest(), "little") % L
+            r = int.from_bytes(hashlib.sha512(b"tors-r%d" % rng_seed).digest(), "little") % L
+            A = add(smul(a, BASE), TA)
+            pk = enc_pt(A)
+            msg = b"torsion %d" % rng_seed
+            rB = smul(r, BASE)
+            for j in range(8):
+                R = add(rB, smul(j, T8))
+                Rb = enc_pt(R)
+                h = int.from_bytes(hashlib.sha512(Rb + pk + msg).digest(), "little") % L
+                # [j]T8 == -[h k]T8  <=>  j = -h k (mod 8)
+                if (j + h * k) % 8 == 0:
+                    S = (r + h * a) % L
+                    out.append((pk, Rb + S.to_bytes(32, "little"), msg))
+                    Rw = enc_pt(add(R, T8))
+                    hw = int.from_bytes(hashlib.sha512(Rw + pk + msg).digest(), "little") % L
+                    Sw = (r + hw * a) % L
+                    out.append((pk, Rw + Sw.to_bytes(32, "little"), msg))
+                    made += 1
+                    break
+    return out
+
+
 def small_order_encodings():
     out = []
     for y in SMALL_Y:
@@ -120,6 +171,8 @@ def ed25519_edge_cases():
     b = bytearray(pk)
     b[31] ^= 0x80
     cases.append((bytes(b), sig, msg))
+    # mixed-order keys with torsion-consistent R (accepted) and off-by-one R
+    cases += torsion_consistent_cases()
     return cases
 
 

@@ -79,6 +79,37 @@ def test_scalar_reduce(dh):
         assert dec(out.raw) == dec(v) % L
 
 
+def _half(dh, h):
+    c0 = ctypes.create_string_buffer(32)
+    c1 = ctypes.create_string_buffer(32)
+    neg = ctypes.c_int(0)
+    bits = dh.dh_half_scalars(h.to_bytes(32, "little"), c0, c1, ctypes.byref(neg))
+    a, b = dec(c0.raw), dec(c1.raw)
+    return (-a if neg.value else a), b, bits
+
+
+def test_half_scalars(dh):
+    """lattice.h: c0 = c1 h (mod 8L), c1 odd, and both about half size -- the
+    conditions under which the half-size Ed25519 equation is equivalent to
+    libsodium's (the relation and parity are what correctness rests on; the
+    size only decides speed)."""
+    rng = np.random.default_rng(5)
+    hs = [0, 1, 2, 3, 8, L - 1, L - 2, 2**252, 2**128, 2**128 + 1, 2**127, (L - 1) // 2,
+          8 * 3**80 % L, 2**200 + 7]
+    rand = [int.from_bytes(rng.bytes(64), "little") % L for _ in range(3000)]
+    sizes = []
+    for k, h in enumerate(hs + rand):
+        c0, c1, bits = _half(dh, h)
+        assert c1 % 2 == 1 and 0 < c1 < L
+        assert (c0 - c1 * h) % (8 * L) == 0
+        assert max(abs(c0).bit_length(), c1.bit_length()) == bits
+        if k >= len(hs):
+            sizes.append(bits)
+    # structured h (L - 1, 2^252, ...) have no short odd vector and use (h, 1);
+    # hash outputs do: about half size
+    assert max(sizes) <= 142 and np.median(sizes) <= 128, (max(sizes), np.median(sizes))
+
+
 def test_hashes(dh):
     import hashlib
 
