@@ -64,14 +64,16 @@ OURO_FI ge_p1p1 ge_p2_dbl(const ge_p2& p) {
 OURO_FI ge_p1p1 ge_p3_dbl(const ge_p3& p) { return ge_p2_dbl(ge_p3_to_p2(p)); }
 
 // P + Q (neg = false) or P - Q (neg = true), Q cached.  The sign is a per-lane
-// select so a wave stays convergent whatever the digits are.
-OURO_FI ge_p1p1 ge_add_cached(const ge_p3& p, const ge_cached& q, bool neg) {
+// select so a wave stays convergent whatever the digits are.  affine_q (wave-
+// uniform): Q has Z = 1 (Z2 = 2), so 2 Z_P Z_Q is a re-normalised addition.
+OURO_FI ge_p1p1 ge_add_cached(const ge_p3& p, const ge_cached& q, bool neg,
+                              bool affine_q = false) {
   fe qa = fe_select(q.YminusX, q.YplusX, neg);
   fe qb = fe_select(q.YplusX, q.YminusX, neg);
   fe A = fe_mul(fe_add(p.Y, p.X), qa);
   fe B = fe_mul(fe_sub(p.Y, p.X), qb);
   fe C = fe_mul(p.T, q.T2d);
-  fe D = fe_mul(p.Z, q.Z2);
+  fe D = affine_q ? fe_carry(fe_add(p.Z, p.Z)) : fe_mul(p.Z, q.Z2);
   fe Dp = fe_add(D, C), Dm = fe_sub(D, C);
   ge_p1p1 r;
   r.X = fe_sub(A, B);

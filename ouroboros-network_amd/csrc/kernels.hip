@@ -21,6 +21,10 @@ using namespace ouro;
 namespace {
 
 constexpr int kBlock = 256;
+// resident waves per SIMD the kernels are compiled for (VGPR budget 512 / W)
+#ifndef OURO_WAVES
+#define OURO_WAVES 2
+#endif
 // throughput header kernel: scratch slot + the per-header result record
 constexpr int kHdrLaneWords = kLaneWords + kResWords;
 
@@ -57,7 +61,7 @@ __device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap
 
 // ---------------------------------------------------------------- kernels ----
 
-__global__ void __launch_bounds__(kBlock, 2) k_ed25519_verify(
+__global__ void __launch_bounds__(kBlock, OURO_WAVES) k_ed25519_verify(
     size_t n, const uint8_t* __restrict__ pk, const uint8_t* __restrict__ sig,
     const uint8_t* __restrict__ msg, const uint64_t* __restrict__ msg_off,
     const uint32_t* __restrict__ msg_len, uint8_t* __restrict__ verdict, int32_t* scratch,
@@ -75,7 +79,7 @@ __global__ void __launch_bounds__(kBlock, 2) k_ed25519_verify(
   }
 }
 
-__global__ void __launch_bounds__(kBlock, 2) k_vrf03_verify(
+__global__ void __launch_bounds__(kBlock, OURO_WAVES) k_vrf03_verify(
     size_t n, const uint8_t* __restrict__ pk, const uint8_t* __restrict__ proof,
     const uint8_t* __restrict__ alpha, const uint64_t* __restrict__ alpha_off,
     const uint32_t* __restrict__ alpha_len, uint8_t* __restrict__ beta,
@@ -93,7 +97,7 @@ __global__ void __launch_bounds__(kBlock, 2) k_vrf03_verify(
   }
 }
 
-__global__ void __launch_bounds__(kBlock, 2) k_sum6kes_verify(
+__global__ void __launch_bounds__(kBlock, OURO_WAVES) k_sum6kes_verify(
     size_t n, const uint8_t* __restrict__ vk, const uint32_t* __restrict__ t,
     const uint8_t* __restrict__ msg, const uint64_t* __restrict__ msg_off,
     const uint32_t* __restrict__ msg_len, const uint8_t* __restrict__ sig,
@@ -112,7 +116,7 @@ __global__ void __launch_bounds__(kBlock, 2) k_sum6kes_verify(
 
 // Throughput mode: one lane per header runs every core of tpraos.h, sharing
 // the VRF key decode and its table, then the single-inversion finish.
-__global__ void __launch_bounds__(kBlock, 2) k_tpraos_verify(ouro_tpraos_batch b,
+__global__ void __launch_bounds__(kBlock, OURO_WAVES) k_tpraos_verify(ouro_tpraos_batch b,
                                                              uint8_t* __restrict__ verdict,
                                                              uint8_t* __restrict__ beta_eta,
                                                              uint8_t* __restrict__ beta_leader,
@@ -136,7 +140,7 @@ __global__ void __launch_bounds__(kBlock, 2) k_tpraos_verify(ouro_tpraos_batch b
 // Latency mode, launch 1: six lanes per header (work item w = core * n + i,
 // so each wave runs one core type), results to a per-header record.
 // n is read from device memory so a captured graph serves any n <= capacity.
-__global__ void __launch_bounds__(kBlock, 2) k_tpraos_cores(ouro_tpraos_batch b,
+__global__ void __launch_bounds__(kBlock, OURO_WAVES) k_tpraos_cores(ouro_tpraos_batch b,
                                                             const uint32_t* __restrict__ d_n,
                                                             int32_t* res_buf, int32_t* scratch,
                                                             const int32_t* __restrict__ btab) {
@@ -152,7 +156,7 @@ __global__ void __launch_bounds__(kBlock, 2) k_tpraos_cores(ouro_tpraos_batch b,
 }
 
 // Latency mode, launch 2: the shared-inversion finish, one lane per header.
-__global__ void __launch_bounds__(kBlock, 2) k_tpraos_finish(ouro_tpraos_batch b,
+__global__ void __launch_bounds__(kBlock, OURO_WAVES) k_tpraos_finish(ouro_tpraos_batch b,
                                                              const uint32_t* __restrict__ d_n,
                                                              const int32_t* res_buf,
                                                              uint8_t* __restrict__ verdict,
@@ -168,7 +172,7 @@ __global__ void __launch_bounds__(kBlock, 2) k_tpraos_finish(ouro_tpraos_batch b
 }
 
 // proof_to_hash only (no verification): beta = H(0x04 || 0x03 || [8]Gamma)
-__global__ void __launch_bounds__(kBlock, 2) k_vrf03_proof_to_hash(size_t n,
+__global__ void __launch_bounds__(kBlock, OURO_WAVES) k_vrf03_proof_to_hash(size_t n,
                                                                 const uint8_t* __restrict__ proof,
                                                                 uint8_t* __restrict__ beta,
                                                                 uint8_t* __restrict__ verdict) {

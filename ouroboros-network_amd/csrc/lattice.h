@@ -199,14 +199,33 @@ OURO_HD inline void ed25519_half_scalars(HalfScalars& out, const uint32_t h[8]) 
     i288_cswap(ntu, ntv, sw);
     ru = nu; rv = nv; tu = ntu; tv = ntv;
   }
-  // candidates with odd t: v, u, u + v, u - v; keep the shortest
-  i288 best_r, best_t;
+  // one Euclid step past v: w = u - q v, q from the leading bits (any integer
+  // q keeps w in the lattice; the right one makes it the next remainder)
+  i288 rw = rv, tw = tv;
+  {
+    const int lu = i288_bitlen(ru), lv = i288_bitlen(rv);
+    if (lv > 0 && lu - lv < 30) {
+      const int sh = lu > 64 ? lu - 64 : 0;
+      const double x = (double)i288_bits64(ru, sh), y = (double)i288_bits64(rv, sh);
+      const int32_t q = (int32_t)(x / y);
+      rw = i288_add(ru, i288_mul_s32(rv, -q));
+      tw = i288_add(tu, i288_mul_s32(tv, -q));
+      if (i288_is_neg(rw)) { i288_negate(rw); i288_negate(tw); }
+    }
+  }
+  // candidates with odd t among the remainders around 2^128 and their
+  // neighbour sums: v, u, u + v, u - v, w, v + w, v - w; keep the shortest
+  // (tests/test_devcode_host.py pins the size distribution)
+  i288 best_r = rv, best_t = tv;
   int best = 1 << 20;
 #pragma unroll 1
-  for (int k = 0; k < 4; k++) {
+  for (int k = 0; k < 7; k++) {
     i288 r = k == 0 ? rv : ru, t = k == 0 ? tv : tu;
     if (k == 2) { r = i288_add(ru, rv); t = i288_add(tu, tv); }
     if (k == 3) { r = i288_sub(ru, rv); t = i288_sub(tu, tv); }
+    if (k == 4) { r = rw; t = tw; }
+    if (k == 5) { r = i288_add(rv, rw); t = i288_add(tv, tw); }
+    if (k == 6) { r = i288_sub(rv, rw); t = i288_sub(tv, tw); }
     if ((t.w[0] & 1u) == 0) continue;
     const int br = i288_abs_bitlen(r), bt = i288_abs_bitlen(t);
     const int b = br > bt ? br : bt;

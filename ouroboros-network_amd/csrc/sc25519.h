@@ -130,23 +130,23 @@ OURO_FI uint64_t sc_recode_carries(const uint32_t s[8]) {
   return mask;
 }
 
-// 32-bit word `idx` of s for a wave-uniform idx (a select chain, no scratch)
-OURO_FI uint32_t sc_word(const uint32_t s[8], int idx) {
-  uint32_t r = s[0];
+// ---- digit streams for the double-scalar multiplication ---------------------
+// A scalar consumed from its most significant window down: the next window
+// sits in the top bits of w[N-1] and each step shifts the array left, so no
+// register array is ever indexed dynamically (which the compiler would move
+// to scratch memory).
+template <int N>
+OURO_FI void ss_shl(uint32_t w[N], int bits) {
 #pragma unroll
-  for (int i = 1; i < 8; i++) r = (idx == i) ? s[i] : r;
-  return r;
+  for (int i = N - 1; i > 0; i--) w[i] = (w[i] << bits) | (w[i - 1] >> (32 - bits));
+  w[0] <<= bits;
 }
-
-// digit j (wave-uniform j) of the W-bit recoding; W divides 32
+// signed digit from the window value v (top bits of the stream) and the
+// recoding carries into this window (cin) and out of it (cout)
 template <int W>
-OURO_FI int32_t sc_digit(const uint32_t s[8], uint64_t carries, int j) {
-  const int bit = W * j;
-  const uint32_t v = (sc_word(s, bit >> 5) >> (bit & 31)) & ((1u << W) - 1);
+OURO_FI int32_t sc_digit_from(uint32_t v, uint64_t carries, int j, int jmax) {
   const uint32_t cin = (uint32_t)(carries >> j) & 1u;
-  // the carry out of the top window is zero for every scalar fed here
-  // (h, S, s < L; c < 2^128), so bit 64 is never needed
-  const uint32_t cout = (j + 1 < 64) ? (uint32_t)(carries >> (j + 1)) & 1u : 0u;
+  const uint32_t cout = (j + 1 < jmax) ? (uint32_t)(carries >> (j + 1)) & 1u : 0u;
   return (int32_t)(v + cin) - (int32_t)(cout << W);
 }
 

@@ -13,6 +13,8 @@
 // (tests/test_synth.py).
 #include <hip/hip_runtime.h>
 
+#include <vector>
+
 #include "synth.h"
 
 using namespace ouro;
@@ -283,10 +285,11 @@ int grid_for(size_t items) {
 }
 int prepare(size_t items) {
   if (!g_ctx.btab) {
-    int32_t tab[kBTabWords];
-    build_btab(tab);
-    if (hipMalloc(&g_ctx.btab, sizeof tab) != hipSuccess) return -2;
-    if (hipMemcpy(g_ctx.btab, tab, sizeof tab, hipMemcpyHostToDevice) != hipSuccess) return -2;
+    std::vector<int32_t> tab(kBTabWords);
+    build_btab(tab.data());
+    const size_t bytes = tab.size() * sizeof(int32_t);
+    if (hipMalloc(&g_ctx.btab, bytes) != hipSuccess) return -2;
+    if (hipMemcpy(g_ctx.btab, tab.data(), bytes, hipMemcpyHostToDevice) != hipSuccess) return -2;
   }
   size_t lanes = (size_t)grid_for(items) * kBlock;
   if (lanes > g_ctx.lanes) {

@@ -17,6 +17,8 @@
 // tables of [1..8]P in cached form live in a per-lane global scratch slot;
 // the [1..128]B niels table is shared (global, L1/L2 resident).
 #pragma once
+#include <vector>
+
 #include "blake2b.h"
 #include "ge25519.h"
 #include "lattice.h"
@@ -39,9 +41,16 @@ constexpr int kSlotCarry = kSlotB + 8;            // 6 words (3 x u64)
 constexpr int kSlotOut = kSlotCarry + 8;          // p2 result: 3 fe at 12-word stride
 constexpr int kLaneWords = kSlotOut + 36;         // 1028 words = 4112 B (16-B multiple)
 
-constexpr int kBTabEntries = 128;                 // [1..128]B, then [1..128](2^128 B)
-constexpr int kNielsWords = 32;                   // 30 used, padded for 16-B loads
-constexpr int kBTabWords = 2 * kBTabEntries * kNielsWords;
+// Fixed base B: the scalar is split at bit 128 (halves with B and 2^128 B, so
+// the doubling chain spans 128 bits) and each half is cut into signed digits
+// of kBW bits, one every kBW / 4 windows of the chain.  kBW = 16: 8 additions
+// per half from tables of 2^15 affine points (2 x 4 MiB, MALL/L2-resident).
+constexpr int kBW = 16;
+constexpr int kBStride = kBW / 4;                 // chain windows per B digit
+constexpr int kBDigitsHalf = 128 / kBW;           // digits per 128-bit half
+constexpr int kBTabEntries = 1 << (kBW - 1);      // [1..2^15]B, then [1..2^15](2^128 B)
+constexpr int kNielsWords = 32;                   // 30 used, padded to 128 B
+constexpr size_t kBTabWords = 2 * (size_t)kBTabEntries * kNielsWords;
 
 // ---- vector load/store helpers ---------------------------------------------
 // (the host bound tracker of fe25519.h follows elements through memory)
@@ -141,14 +150,14 @@ OURO_HD inline void build_table(int32_t* tab, const ge_p3& P) {
 
 // ---- the double-scalar multiplication ---------------------------------------
 // cfg: bits 0..6 = number of active width-4 windows of scalar a1 (table 1),
-//      bits 8..14 = same for a2 (table 2, 0 = unused), bit 16 = add [b]B,
-//      bit 17 = split b: its width-8 digits 0..15 go with B and digits 16..31
-//      with B' = 2^128 B, so the doubling chain only spans 128 bits
-//      (U = [s]B - [c]Y in the VRF, where c has 128 bits).
+//      bits 8..14 = same for a2 (table 2, 0 = unused), bit 16 = add [b]B with
+//      b split at bit 128: its kBW-bit digits 0..7 go with B and 8..15 with
+//      B' = 2^128 B, so the doubling chain only spans 128 bits (bit 17, the
+//      split flag of earlier layouts, is implied and ignored),
+//      bits 20..21 / 22..23 = table slots (0..2) read for a1 / a2.
 // Reads a1/a2/b and their recoding carries from the lane slot, writes the
 // resulting p2 point to lane[kSlotOut..].  Out of line: the header kernel calls
 // it six times per item, and the loop body is the I-cache-critical code.
-//      bits 20..21 / 22..23 = table slots (0..2) read for a1 / a2.
 constexpr uint32_t dsm_cfg(int nw1, int nw2, bool useB, bool splitB = false, int tab1 = 0,
                            int tab2 = 1) {
   return (uint32_t)nw1 | ((uint32_t)nw2 << 8) | (useB ? (1u << 16) : 0u) |
@@ -158,7 +167,8 @@ constexpr uint32_t dsm_cfg(int nw1, int nw2, bool useB, bool splitB = false, int
 OURO_NI void dsm(int32_t* lane, const int32_t* btab, uint32_t cfg) {
   const int nw1 = (int)(cfg & 0x7f), nw2 = (int)((cfg >> 8) & 0x7f);
   const bool useB = (cfg >> 16) & 1;
-  const bool splitB = (cfg >> 17) & 1;
+  const int32_t* tab1 = lane + (int)((cfg >> 20) & 3) * kTabWords;
+  const int32_t* tab2 = lane + (int)((cfg >> 22) & 3) * kTabWords;
   uint32_t a1[8], a2[8], b[8];
   ld_words8(a1, lane + kSlotA1);
   ld_words8(a2, lane + kSlotA2);
@@ -166,52 +176,81 @@ OURO_NI void dsm(int32_t* lane, const int32_t* btab, uint32_t cfg) {
   const uint64_t* carr = reinterpret_cast<const uint64_t*>(lane + kSlotCarry);
   const uint64_t c1 = carr[0], c2 = carr[1], cb = carr[2];
   int top = nw1 > nw2 ? nw1 : nw2;
-  if (useB) top = splitB ? (top > 32 ? top : 32) : 64;
+  if (useB && top < 32) top = 32;
+  // digit streams: window top-1 of a1/a2 at the top of the array
+#pragma unroll 1
+  for (int s = top; s < 64; s++) {
+    ss_shl<8>(a1, 4);
+    ss_shl<8>(a2, 4);
+  }
+  // b: two 128-bit streams (its low and high halves), kBW bits per B window
+  uint32_t blo[4] = {b[0], b[1], b[2], b[3]};
+  uint32_t bhi[4] = {b[4], b[5], b[6], b[7]};
+  uint32_t prefetch = 0;
   // t starts as the identity in p1p1 form (X/Z = 0, Y/T = 1)
   ge_p1p1 t{fe_zero(), fe_one(), fe_one(), fe_one()};
 #pragma unroll 1
   for (int j = top - 1; j >= 0; j--) {
+    // this window's digits (wave-uniform activity, per-lane values)
+    const bool act1 = j < nw1, act2 = j < nw2;
+    const bool actB = useB && (j % kBStride) == 0 && j < 32;
+    const bool actB2 = actB;
+    int32_t d1 = 0, d2 = 0, d3 = 0, d4 = 0;
+    if (act1) d1 = sc_digit_from<4>(a1[7] >> 28, c1, j, 64);
+    if (act2) d2 = sc_digit_from<4>(a2[7] >> 28, c2, j, 64);
+    ss_shl<8>(a1, 4);
+    ss_shl<8>(a2, 4);
+    if (actB) {
+      const int k = j / kBStride;
+      d3 = sc_digit_from<kBW>(blo[3] >> (32 - kBW), cb, k, 2 * kBDigitsHalf);
+      d4 = sc_digit_from<kBW>(bhi[3] >> (32 - kBW), cb, k + kBDigitsHalf, 2 * kBDigitsHalf);
+      ss_shl<4>(blo, kBW);
+      ss_shl<4>(bhi, kBW);
+    }
+    // touch this window's per-lane table entries now, so that the loads
+    // after the four doublings hit L2 instead of waiting on HBM
+    const int i1 = (d1 < 0 ? -d1 : d1) - 1, i2 = (d2 < 0 ? -d2 : d2) - 1;
+    const int32_t* e1 = tab1 + (i1 > 0 ? i1 : 0) * kCachedWords;
+    const int32_t* e2 = tab2 + (i2 > 0 ? i2 : 0) * kCachedWords;
+    uint32_t pf1 = 0, pf2 = 0, pf3 = 0, pf4 = 0, pf5 = 0, pf6 = 0;
+    if (act1) { pf1 = (uint32_t)e1[0]; pf2 = (uint32_t)e1[kCachedWords - 1]; }
+    if (act2) { pf3 = (uint32_t)e2[0]; pf4 = (uint32_t)e2[kCachedWords - 1]; }
+    if (actB) {
+      // the B entries (one 128-B line each) come from the 8 MiB tables
+      const int i3 = (d3 < 0 ? -d3 : d3) - 1, i4 = (d4 < 0 ? -d4 : d4) - 1;
+      pf5 = (uint32_t)btab[(size_t)(i3 > 0 ? i3 : 0) * kNielsWords];
+      pf6 = (uint32_t)btab[((size_t)kBTabEntries + (i4 > 0 ? i4 : 0)) * kNielsWords];
+    }
 #pragma unroll 1
     for (int k = 0; k < 4; k++) t = ge_p2_dbl(ge_p1p1_to_p2(t));
+    prefetch ^= pf1 ^ pf2 ^ pf3 ^ pf4 ^ pf5 ^ pf6;
     // up to four additions, each from a wave-uniform source
 #pragma unroll 1
     for (int src = 0; src < 4; src++) {
-      bool active;
-      int32_t d;
-      if (src == 0) {
-        active = j < nw1;
-        d = active ? sc_digit<4>(a1, c1, j) : 0;
-      } else if (src == 1) {
-        active = j < nw2;
-        d = active ? sc_digit<4>(a2, c2, j) : 0;
-      } else if (src == 2) {
-        active = useB && (j & 1) == 0 && (!splitB || j < 32);
-        d = active ? sc_digit<8>(b, cb, j >> 1) : 0;
-      } else {
-        active = splitB && (j & 1) == 0 && j < 32;
-        d = active ? sc_digit<8>(b, cb, (j >> 1) + 16) : 0;
-      }
+      const bool active = src == 0 ? act1 : src == 1 ? act2 : src == 2 ? actB : actB2;
       if (!active) continue;
+      const int32_t d = src == 0 ? d1 : src == 1 ? d2 : src == 2 ? d3 : d4;
       const bool neg = d < 0;
       const int32_t mag = neg ? -d : d;
       const int idx = mag > 0 ? mag - 1 : 0;
       ge_cached q;
       if (src < 2) {
-        const int slot = (int)((cfg >> (src == 0 ? 20 : 22)) & 3);
-        q = ld_cached(lane + slot * kTabWords + idx * kCachedWords);
+        q = ld_cached((src == 0 ? tab1 : tab2) + idx * kCachedWords);
       } else {
-        const int base = src == 3 ? kBTabEntries : 0;
+        const size_t base = src == 3 ? kBTabEntries : 0;
         ge_niels nq = ld_niels(btab + (base + idx) * kNielsWords);
         q = ge_cached{nq.yplusx, nq.yminusx, fe_two(), nq.xy2d};
       }
       if (mag == 0) q = ge_cached_identity();
-      t = ge_add_cached(ge_p1p1_to_p3(t), q, neg);
+      t = ge_add_cached(ge_p1p1_to_p3(t), q, neg, src >= 2);
     }
   }
   ge_p2 r = ge_p1p1_to_p2(t);
   st_fe(lane + kSlotOut, r.X);
   st_fe(lane + kSlotOut + 12, r.Y);
   st_fe(lane + kSlotOut + 24, r.Z);
+  // keeps the prefetch loads alive; limbs are < 2^27, so this never stores
+  if (prefetch == 0xffffffffu) lane[kSlotOut + 35] = (int32_t)prefetch;
 }
 
 OURO_FI ge_p2 dsm_result(const int32_t* lane) {
@@ -306,7 +345,7 @@ OURO_HD inline bool ed25519_verify_lane(const uint32_t sig[16], const uint32_t p
   uint64_t* carr = reinterpret_cast<uint64_t*>(lane + kSlotCarry);
   carr[0] = sc_recode_carries<4, 64>(hs.c0);
   carr[1] = sc_recode_carries<4, 64>(hs.c1);
-  carr[2] = sc_recode_carries<8, 32>(b);
+  carr[2] = sc_recode_carries<kBW, 2 * kBDigitsHalf>(b);
   // windows so that every scalar is < 2^(4 nw - 1) (top carry zero), <= 64
   int nw = wave_max_small((hs.bits + 4) >> 2);
   nw = nw < 1 ? 1 : (nw > 64 ? 64 : nw);
@@ -443,7 +482,7 @@ OURO_HD inline bool vrf03_verify_lane(uint32_t beta[16], const uint32_t pk[8],
   st_words8(lane + kSlotB, s);
   uint64_t* carr = reinterpret_cast<uint64_t*>(lane + kSlotCarry);
   carr[0] = sc_recode_carries<4, 33>(c);
-  carr[2] = sc_recode_carries<8, 32>(s);
+  carr[2] = sc_recode_carries<kBW, 2 * kBDigitsHalf>(s);
   dsm(lane, btab, dsm_cfg(33, 0, true, true));
   ge_p2 U = dsm_result(lane);
   // V = [s]H - [c]Gamma
@@ -548,29 +587,43 @@ OURO_HD inline bool sum6kes_verify_lane(const uint32_t vk[8], uint32_t t, const 
 }
 
 // ---- fixed-base tables (host side, computed once per process) ----------------
-// [k]G for k = 1..128 as (y + x, y - x, 2 d x y), affine, reduced limbs, for
-// G = B and G = 2^128 B (the split-scalar table of dsm_cfg bit 17).
-OURO_HD inline void build_btab_one(int32_t* out, const ge_p3& G) {
+// [k]G for k = 1..kBTabEntries as (y + x, y - x, 2 d x y), affine, reduced
+// limbs, for G = B and G = 2^128 B (the two halves of the split scalar).  The
+// affine conversion inverts the Z coordinates in chunks with one inversion each
+// (Montgomery's trick); 2 x 32768 entries take a few tens of ms on the host.
+inline void build_btab_one(int32_t* out, const ge_p3& G) {
+  constexpr int kChunk = 256;
+  std::vector<ge_p3> pts(kChunk);
+  std::vector<fe> pre(kChunk);
   ge_p3 P = G;
-  for (int k = 0; k < kBTabEntries; k++) {
-    if (k > 0) P = ge_p3_add(P, G);
-    fe zi = fe_invert(P.Z);
-    fe x = fe_mul(P.X, zi), y = fe_mul(P.Y, zi);
-    fe yp = fe_carry(fe_add(y, x)), ym = fe_carry(fe_sub(y, x));
-    fe xy2d = fe_mul(fe_mul(x, y), fe_d2());
-    int32_t* e = out + k * kNielsWords;
-    for (int i = 0; i < 10; i++) {
-      e[i] = yp.v[i];
-      e[10 + i] = ym.v[i];
-      e[20 + i] = xy2d.v[i];
+  for (int k0 = 0; k0 < kBTabEntries; k0 += kChunk) {
+    const int n = kBTabEntries - k0 < kChunk ? kBTabEntries - k0 : kChunk;
+    for (int i = 0; i < n; i++) {
+      if (k0 + i > 0) P = ge_p3_add(P, G);
+      pts[i] = P;
+      pre[i] = i ? fe_mul(pre[i - 1], P.Z) : P.Z;
     }
-    OURO_TRK(ouro_trk_store(e, yp.b); ouro_trk_store(e + 10, ym.b); ouro_trk_store(e + 20, xy2d.b);)
-    e[30] = 0;
-    e[31] = 0;
+    fe inv = fe_invert(pre[n - 1]);
+    for (int i = n - 1; i >= 0; i--) {
+      const fe zi = i ? fe_mul(inv, pre[i - 1]) : inv;
+      if (i) inv = fe_mul(inv, pts[i].Z);
+      fe x = fe_mul(pts[i].X, zi), y = fe_mul(pts[i].Y, zi);
+      fe yp = fe_carry(fe_add(y, x)), ym = fe_carry(fe_sub(y, x));
+      fe xy2d = fe_mul(fe_mul(x, y), fe_d2());
+      int32_t* e = out + (size_t)(k0 + i) * kNielsWords;
+      for (int l = 0; l < 10; l++) {
+        e[l] = yp.v[l];
+        e[10 + l] = ym.v[l];
+        e[20 + l] = xy2d.v[l];
+      }
+      OURO_TRK(ouro_trk_store(e, yp.b); ouro_trk_store(e + 10, ym.b); ouro_trk_store(e + 20, xy2d.b);)
+      e[30] = 0;
+      e[31] = 0;
+    }
   }
 }
 
-OURO_HD inline void build_btab(int32_t* out) {
+inline void build_btab(int32_t* out) {
   // B = (x, 4/5) with x even: encoding 0x5866...66 (little-endian)
   uint32_t by[8];
   for (int i = 0; i < 8; i++) by[i] = 0x66666666u;
@@ -580,7 +633,7 @@ OURO_HD inline void build_btab(int32_t* out) {
   build_btab_one(out, B);
   ge_p3 B128 = B;
   for (int i = 0; i < 128; i++) B128 = ge_p1p1_to_p3(ge_p3_dbl(B128));
-  build_btab_one(out + kBTabEntries * kNielsWords, B128);
+  build_btab_one(out + (size_t)kBTabEntries * kNielsWords, B128);
 }
 
 }  // namespace ouro

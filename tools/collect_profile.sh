@@ -12,5 +12,8 @@ cp "$G/prof_$TAG.bench.json" "$D/bench_under_rocprof.json"
 cp "$G/pmc_fetch_$TAG/run_counter_collection.csv" "$D/pmc_fetch_size.csv"
 cp "$G/pmc_write_$TAG/run_counter_collection.csv" "$D/pmc_write_size.csv"
 cp "$G/pmc_sq_$TAG/run_counter_collection.csv" "$D/pmc_sq.csv"
+if [ -f "$G/pmc_wait_$TAG/run_counter_collection.csv" ]; then
+  cp "$G/pmc_wait_$TAG/run_counter_collection.csv" "$D/pmc_wait.csv"
+fi
 python3 tools/summarize_profile.py "$TAG" ${PMC_HEADERS:+--pmc-headers $PMC_HEADERS} > /dev/null
 echo "profiles/$TAG: $(ls "$D" | tr '\n' ' ')"

@@ -38,7 +38,17 @@ __global__ void __launch_bounds__(256, 2) kvar(const uint32_t* in, uint32_t* out
     c[k] = in[24 * i + 16 + k];
   }
   uint32_t w1[8], w2[8];
-  if constexpr (V == 0 || V == 3) {
+  if constexpr (V == 11 || V == 12) {
+    // production fe25519.h, one dependent chain per lane (V 11: sq, V 12: mul)
+    ouro::fe x = ouro::fe_from_words(a), y = ouro::fe_from_words(b);
+#pragma unroll 1
+    for (int it = 0; it < ITERS; it++) {
+      if constexpr (V == 11) x = ouro::fe_sq(x);
+      else x = ouro::fe_mul(x, y);
+    }
+    ouro::fe_to_words(w1, x);
+    ouro::fe_to_words(w2, y);
+  } else if constexpr (V == 0 || V == 3) {
     ouro::fe x = ouro::fe_from_words(a), y = ouro::fe_from_words(b), z = ouro::fe_from_words(c);
     ouro::fe w = y;
 #pragma unroll 1
@@ -141,11 +151,11 @@ int main(int argc, char** argv) {
   CHECK(hipMalloc(&din, h.size() * 4));
   CHECK(hipMalloc(&dout, 16 * n * 4));
   CHECK(hipMemcpy(din, h.data(), h.size() * 4, hipMemcpyHostToDevice));
-  const char* names[11] = {"fe10_mul", "fe8_mul_asm", "fe8_mul_c", "fe10_sq", "fe8_sq_asm",
+  const char* names[13] = {"fe10_mul", "fe8_mul_asm", "fe8_mul_c", "fe10_sq", "fe8_sq_asm",
                            "fe8_mul_opscan", "fe8_mul_opscan_c", "fe10u_mul", "fe10u_sq",
-                           "fe10d_mul", "fe10d_sq"};
-  std::vector<std::vector<uint32_t>> res(11, std::vector<uint32_t>(16 * n));
-  float ms[11];
+                           "fe10d_mul", "fe10d_sq", "fe_sq_1chain", "fe_mul_1chain"};
+  std::vector<std::vector<uint32_t>> res(13, std::vector<uint32_t>(16 * n));
+  float ms[13];
   for (int round = 0; round < 2; round++) {
     ms[0] = run<0>(din, dout, n, 3);
     CHECK(hipMemcpy(res[0].data(), dout, 16 * n * 4, hipMemcpyDeviceToHost));
@@ -169,6 +179,10 @@ int main(int argc, char** argv) {
     CHECK(hipMemcpy(res[9].data(), dout, 16 * n * 4, hipMemcpyDeviceToHost));
     ms[10] = run<10>(din, dout, n, 3);
     CHECK(hipMemcpy(res[10].data(), dout, 16 * n * 4, hipMemcpyDeviceToHost));
+    ms[11] = run<11>(din, dout, n, 3);
+    CHECK(hipMemcpy(res[11].data(), dout, 16 * n * 4, hipMemcpyDeviceToHost));
+    ms[12] = run<12>(din, dout, n, 3);
+    CHECK(hipMemcpy(res[12].data(), dout, 16 * n * 4, hipMemcpyDeviceToHost));
   }
   const bool mul_eq = res[0] == res[1] && res[0] == res[2] && res[0] == res[5] && res[0] == res[6] && res[0] == res[7] &&
                       res[0] == res[9];
@@ -176,8 +190,9 @@ int main(int argc, char** argv) {
   const double ops = 2.0 * ITERS * n;
   printf("{\"lanes\": %zu, \"iters\": %d, \"mul_equal\": %s, \"sq_equal\": %s", n, ITERS,
          mul_eq ? "true" : "false", sq_eq ? "true" : "false");
-  for (int v = 0; v < 11; v++)
-    printf(", \"%s\": {\"ms\": %.3f, \"Gops\": %.2f}", names[v], ms[v], ops / (ms[v] * 1e-3) / 1e9);
+  for (int v = 0; v < 13; v++)
+    printf(", \"%s\": {\"ms\": %.3f, \"Gops\": %.2f}", names[v], ms[v],
+           (v >= 11 ? ops / 2 : ops) / (ms[v] * 1e-3) / 1e9);
   printf("}\n");
   return (mul_eq && sq_eq) ? 0 : 1;
 }
