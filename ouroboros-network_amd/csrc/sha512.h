@@ -31,7 +31,32 @@ constexpr uint64_t kSha512K[80] = {
     0x28db77f523047d84ULL, 0x32caab7b40c72493ULL, 0x3c9ebe0a15c9bebcULL, 0x431d67c49c100d4cULL,
     0x4cc5d4becb3e42b6ULL, 0x597f299cfc657e2aULL, 0x5fcb6fab3ad6faecULL, 0x6c44198c4a475817ULL};
 
-OURO_FI uint64_t rotr64(uint64_t x, int n) { return (x >> n) | (x << (64 - n)); }
+// 64-bit rotate / shift by a compile-time amount on 32-bit halves: two
+// v_alignbit_b32 per rotate (the generic form costs three instructions)
+OURO_FI uint64_t rotr64(uint64_t x, int n) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+  uint32_t rl, rh;
+  if (n < 32) {
+    rl = __builtin_amdgcn_alignbit(hi, lo, n);
+    rh = __builtin_amdgcn_alignbit(lo, hi, n);
+  } else {
+    rl = __builtin_amdgcn_alignbit(lo, hi, n - 32);
+    rh = __builtin_amdgcn_alignbit(hi, lo, n - 32);
+  }
+  return ((uint64_t)rh << 32) | rl;
+#else
+  return (x >> n) | (x << (64 - n));
+#endif
+}
+OURO_FI uint64_t shr64(uint64_t x, int n) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+  return ((uint64_t)(hi >> n) << 32) | __builtin_amdgcn_alignbit(hi, lo, n);
+#else
+  return x >> n;
+#endif
+}
 
 OURO_FI void sha512_init(uint64_t H[8]) {
   H[0] = 0x6a09e667f3bcc908ULL; H[1] = 0xbb67ae8584caa73bULL;
@@ -40,25 +65,32 @@ OURO_FI void sha512_init(uint64_t H[8]) {
   H[6] = 0x1f83d9abfb41bd6bULL; H[7] = 0x5be0cd19137e2179ULL;
 }
 
-// 80 rounds as 5 passes of 16 with the schedule kept in a 16-word ring
-OURO_FI void sha512_compress(uint64_t H[8], uint64_t W[16]) {
+OURO_FI void sha512_round(uint64_t& a, uint64_t& b, uint64_t& c, uint64_t& d, uint64_t& e,
+                          uint64_t& f, uint64_t& g, uint64_t& h, uint64_t k, uint64_t w) {
+  const uint64_t S1 = rotr64(e, 14) ^ rotr64(e, 18) ^ rotr64(e, 41);
+  const uint64_t ch = (e & f) ^ (~e & g);
+  const uint64_t T1 = h + S1 + ch + k + w;
+  const uint64_t S0 = rotr64(a, 28) ^ rotr64(a, 34) ^ rotr64(a, 39);
+  const uint64_t mj = (a & b) ^ (a & c) ^ (b & c);
+  h = g; g = f; f = e; e = d + T1; d = c; c = b; b = a; a = T1 + S0 + mj;
+}
+
+// 80 rounds: 16 on the block's words, then 4 passes of 16 that extend the
+// schedule in a 16-word ring (no per-round branch; out of line so the
+// several hash call sites share one copy of the round code)
+OURO_NI void sha512_compress(uint64_t H[8], uint64_t W[16]) {
   uint64_t a = H[0], b = H[1], c = H[2], d = H[3], e = H[4], f = H[5], g = H[6], h = H[7];
+#pragma unroll
+  for (int i = 0; i < 16; i++) sha512_round(a, b, c, d, e, f, g, h, kSha512K[i], W[i]);
 #pragma unroll 1
-  for (int r0 = 0; r0 < 80; r0 += 16) {
+  for (int r0 = 16; r0 < 80; r0 += 16) {
 #pragma unroll
     for (int i = 0; i < 16; i++) {
-      if (r0 > 0) {
-        const uint64_t w15 = W[(i + 1) & 15], w2 = W[(i + 14) & 15];
-        const uint64_t s0 = rotr64(w15, 1) ^ rotr64(w15, 8) ^ (w15 >> 7);
-        const uint64_t s1 = rotr64(w2, 19) ^ rotr64(w2, 61) ^ (w2 >> 6);
-        W[i] += s0 + W[(i + 9) & 15] + s1;
-      }
-      const uint64_t S1 = rotr64(e, 14) ^ rotr64(e, 18) ^ rotr64(e, 41);
-      const uint64_t ch = (e & f) ^ (~e & g);
-      const uint64_t T1 = h + S1 + ch + kSha512K[r0 + i] + W[i];
-      const uint64_t S0 = rotr64(a, 28) ^ rotr64(a, 34) ^ rotr64(a, 39);
-      const uint64_t mj = (a & b) ^ (a & c) ^ (b & c);
-      h = g; g = f; f = e; e = d + T1; d = c; c = b; b = a; a = T1 + S0 + mj;
+      const uint64_t w15 = W[(i + 1) & 15], w2 = W[(i + 14) & 15];
+      const uint64_t s0 = rotr64(w15, 1) ^ rotr64(w15, 8) ^ shr64(w15, 7);
+      const uint64_t s1 = rotr64(w2, 19) ^ rotr64(w2, 61) ^ shr64(w2, 6);
+      W[i] += s0 + W[(i + 9) & 15] + s1;
+      sha512_round(a, b, c, d, e, f, g, h, kSha512K[r0 + i], W[i]);
     }
   }
   H[0] += a; H[1] += b; H[2] += c; H[3] += d; H[4] += e; H[5] += f; H[6] += g; H[7] += h;
