@@ -165,6 +165,25 @@ int ouro_tpraos_plan_run(ouro_tpraos_plan *plan, const ouro_tpraos_batch *b, uin
                          uint8_t *beta_eta, uint8_t *beta_leader);
 void ouro_tpraos_plan_destroy(ouro_tpraos_plan *plan);
 
+/* ---------------------------------------------- leader threshold ----- */
+/* ledger-specs checkLeaderValue (shelley-spec-ledger BlockChain.hs), called by
+ * meetsLeaderThreshold, ouroboros-consensus-shelley/src/Ouroboros/Consensus/
+ * Shelley/Protocol.hs:473-491: is the leader VRF output beta (64 B) below
+ * 1 - (1 - f)^sigma, decided with shelley-spec-non-integral's taylorExpCmp in
+ * 34-digit fixed point.  sigma = sigma_num[i] / sigma_den[i] (the pool's
+ * relative stake, 0 <= sigma <= 1); f is given as its ActiveSlotCoeff fields:
+ * unActiveSlotLog (a signed 128-bit integer, act_log_hi:act_log_lo; the
+ * reference precomputes it from f) and whether f is exactly 1.
+ * verdict[i] = OURO_LEADER_YES / OURO_LEADER_NO, or OURO_LEADER_BADARG when
+ * sigma or unActiveSlotLog is outside the supported domain
+ * (-8 * 10^34 <= unActiveSlotLog <= 0, i.e. f <= 1 - e^-8). */
+#define OURO_LEADER_NO 0u
+#define OURO_LEADER_YES 1u
+#define OURO_LEADER_BADARG 0xffu
+int ouro_leader_check_batch(size_t n, const uint8_t *beta, const uint64_t *sigma_num,
+                            const uint64_t *sigma_den, int64_t act_log_hi,
+                            uint64_t act_log_lo, int f_is_one, uint8_t *verdict);
+
 /* ----------------------------------- batch, device-resident buffers ----- */
 /* Same kernels on caller-owned device memory, enqueued on `stream` (a
  * hipStream_t; NULL = HIP's default stream) and NOT synchronised: the caller
@@ -192,6 +211,10 @@ int ouro_sum6kes_verify_batch_device(void *stream, size_t n, const uint8_t *vk,
 int ouro_tpraos_verify_batch_device(void *stream, const ouro_tpraos_batch *b,
                                     uint8_t *verdict, uint8_t *beta_eta,
                                     uint8_t *beta_leader);
+int ouro_leader_check_batch_device(void *stream, size_t n, const uint8_t *beta,
+                                   const uint64_t *sigma_num, const uint64_t *sigma_den,
+                                   int64_t act_log_hi, uint64_t act_log_lo, int f_is_one,
+                                   uint8_t *verdict);
 
 #ifdef __cplusplus
 }

@@ -26,6 +26,10 @@ HDR_VRF_ETA_OK = 0x04
 HDR_VRF_LEADER_OK = 0x08
 HDR_ALL_OK = 0x0F
 
+LEADER_NO = 0
+LEADER_YES = 1
+LEADER_BADARG = 0xFF
+
 
 class NativeUnavailable(RuntimeError):
     """The gfx950 library is not built or cannot be loaded."""
@@ -85,6 +89,9 @@ SIGNATURES = {
     "ouro_tpraos_plan_create": (_P, [_SZ, _SZ]),
     "ouro_tpraos_plan_run": (_I, [_P, ctypes.POINTER(TPraosBatch), _P, _P, _P]),
     "ouro_tpraos_plan_destroy": (None, [_P]),
+    "ouro_leader_check_batch": (_I, [_SZ, _P, _P, _P, ctypes.c_int64, ctypes.c_uint64, _I, _P]),
+    "ouro_leader_check_batch_device": (_I, [_P, _SZ, _P, _P, _P, ctypes.c_int64, ctypes.c_uint64,
+                                            _I, _P]),
 }
 
 _lib = None

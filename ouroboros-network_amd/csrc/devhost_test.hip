@@ -9,6 +9,7 @@
 #include <cstring>
 #include <vector>
 
+#include "leader.h"
 #include "tpraos.h"
 
 using namespace ouro;
@@ -157,6 +158,11 @@ void dh_elligator2_ref(uint8_t* out, const uint8_t* r32) {
   uint32_t enc[8];
   ge_encode_with_inv(enc, H.X, H.Y, fe_invert(H.Z));
   memcpy(out, enc, 32);
+}
+// leader.h: 1 leader, 0 not, -1 outside the supported domain
+int dh_leader_check(const uint8_t* beta64, uint64_t num, uint64_t den, uint64_t act_log_lo,
+                    int64_t act_log_hi) {
+  return leader_check_lane(beta64, num, den, act_log_lo, act_log_hi);
 }
 // lattice.h: (|c0|, c1, sign of c0) for h (32 bytes, < 2^253); returns the bit size
 int dh_half_scalars(const uint8_t* h32, uint8_t* c0, uint8_t* c1, int* c0_neg) {

@@ -14,6 +14,7 @@
 #include <vector>
 
 #include "../../include/ouro_verify.h"
+#include "leader.h"
 #include "tpraos.h"
 
 using namespace ouro;
@@ -171,6 +172,23 @@ __global__ void __launch_bounds__(kBlock, OURO_WAVES) k_tpraos_finish(ouro_tprao
     hdr_finish_item(b, i, res_buf + i * kResWords, lane, verdict, beta_eta, beta_leader);
 }
 
+// leader threshold (leader.h), one item per lane; verdict 1 / 0 / 0xff
+__global__ void __launch_bounds__(kBlock) k_leader_check(size_t n, const uint8_t* __restrict__ beta,
+                                                         const uint64_t* __restrict__ num,
+                                                         const uint64_t* __restrict__ den,
+                                                         uint64_t act_log_lo, int64_t act_log_hi,
+                                                         uint32_t f_is_one,
+                                                         uint8_t* __restrict__ verdict) {
+  const size_t tid = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const size_t nth = (size_t)gridDim.x * blockDim.x;
+  for (size_t i = tid; i < n; i += nth) {
+    const int32_t r = f_is_one ? kLeaderYes
+                               : leader_check_lane(beta + 64 * i, num[i], den[i], act_log_lo,
+                                                   act_log_hi);
+    verdict[i] = r < 0 ? (uint8_t)0xff : (uint8_t)r;
+  }
+}
+
 // proof_to_hash only (no verification): beta = H(0x04 || 0x03 || [8]Gamma)
 __global__ void __launch_bounds__(kBlock, OURO_WAVES) k_vrf03_proof_to_hash(size_t n,
                                                                 const uint8_t* __restrict__ proof,
@@ -235,7 +253,7 @@ std::mutex g_dev_mu;
 std::map<int, DeviceState> g_dev;
 
 enum KernelId { kEd = 0, kVrf = 1, kKes = 2, kHdr = 3, kP2H = 4, kCores = 5, kFinish = 6,
-                kNumKernels = 7 };
+                kLeader = 7, kNumKernels = 8 };
 
 const void* kernel_ptr(int id) {
   switch (id) {
@@ -245,6 +263,7 @@ const void* kernel_ptr(int id) {
     case kHdr: return reinterpret_cast<const void*>(&k_tpraos_verify);
     case kCores: return reinterpret_cast<const void*>(&k_tpraos_cores);
     case kFinish: return reinterpret_cast<const void*>(&k_tpraos_finish);
+    case kLeader: return reinterpret_cast<const void*>(&k_leader_check);
     default: return reinterpret_cast<const void*>(&k_vrf03_proof_to_hash);
   }
 }
@@ -398,6 +417,19 @@ int launch_hdr(hipStream_t st, const ouro_tpraos_batch& b, uint8_t* verdict, uin
   if ((rc = plan(ds, kHdr, b.n, st, &grid, &scr, kHdrLaneWords))) return rc;
   hipLaunchKernelGGL(k_tpraos_verify, dim3(grid), dim3(kBlock), 0, st, b, verdict, be, bl, scr,
                      ds->btab);
+  return launch_check();
+}
+
+int launch_leader(hipStream_t st, size_t n, const uint8_t* beta, const uint64_t* num,
+                  const uint64_t* den, int64_t lhi, uint64_t llo, int f_is_one,
+                  uint8_t* verdict) {
+  DeviceState* ds;
+  int rc = device_state(&ds);
+  if (rc) return rc;
+  int grid;
+  if ((rc = plan(ds, kLeader, n, st, &grid, nullptr))) return rc;
+  hipLaunchKernelGGL(k_leader_check, dim3(grid), dim3(kBlock), 0, st, n, beta, num, den, llo, lhi,
+                     f_is_one ? 1u : 0u, verdict);
   return launch_check();
 }
 
@@ -632,6 +664,29 @@ int ouro_tpraos_verify_batch(const ouro_tpraos_batch* b, uint8_t* verdict, uint8
   return OURO_OK;
 }
 
+int ouro_leader_check_batch(size_t n, const uint8_t* beta, const uint64_t* sigma_num,
+                            const uint64_t* sigma_den, int64_t act_log_hi, uint64_t act_log_lo,
+                            int f_is_one, uint8_t* verdict) {
+  if (n == 0) return OURO_OK;
+  if (!beta || !sigma_num || !sigma_den || !verdict) return fail(OURO_EINVAL, "null argument");
+  hipStream_t st;
+  int rc = thread_stream(&st);
+  if (rc) return rc;
+  Stager sg{st};
+  auto dbeta = sg.up(beta, 64 * n);
+  auto dnum = sg.up(sigma_num, n);
+  auto dden = sg.up(sigma_den, n);
+  auto dver = sg.out<uint8_t>(n);
+  if (sg.rc) return sg.rc;
+  if ((rc = launch_leader(st, n, dbeta, dnum, dden, act_log_hi, act_log_lo, f_is_one, dver)))
+    return rc;
+  std::vector<uint8_t> tv(n);
+  if ((rc = download(st, tv.data(), dver, n))) return rc;
+  if ((rc = finish(st))) return rc;
+  memcpy(verdict, tv.data(), n);
+  return OURO_OK;
+}
+
 // ---- single item: a batch of one (ABI-identical to the symbols replaced) ----
 int ouro_ed25519_verify(const unsigned char* sig, const unsigned char* m, unsigned long long mlen,
                         const unsigned char* pk) {
@@ -753,6 +808,16 @@ int ouro_tpraos_verify_batch_device(void* stream, const ouro_tpraos_batch* b, ui
   if (!beta_eta || !beta_leader) return fail(OURO_EINVAL, "device API needs both beta buffers");
   hipStream_t st = static_cast<hipStream_t>(stream);  // NULL = HIP's default stream
   return launch_hdr(st, *b, verdict, beta_eta, beta_leader);
+}
+
+int ouro_leader_check_batch_device(void* stream, size_t n, const uint8_t* beta,
+                                   const uint64_t* sigma_num, const uint64_t* sigma_den,
+                                   int64_t act_log_hi, uint64_t act_log_lo, int f_is_one,
+                                   uint8_t* verdict) {
+  if (n == 0) return OURO_OK;
+  hipStream_t st = static_cast<hipStream_t>(stream);  // NULL = HIP's default stream
+  return launch_leader(st, n, beta, sigma_num, sigma_den, act_log_hi, act_log_lo, f_is_one,
+                       verdict);
 }
 
 // ---- latency mode (ChainSync windows) ----
