@@ -208,7 +208,37 @@ def component_rates(hdr, n: int, reps: int = 3):
                                                  t["kes_sig"].data_ptr(), ver.data_ptr())
         _native.check(rc, "kes device batch")
 
+    # checkLeaderValue on the batch's leader outputs:
+    # synthetic relative stakes ~ 1/1024 per pool, f = 1/20 given as its
+    # unActiveSlotLog = floor(10^34 ln(0.95)) (a constant input, as the
+    # reference's ActiveSlotCoeff stores it)
+    sig_num = (torch.arange(n, dtype=torch.int64, device=dev) % 997 + 1)
+    sig_den = torch.full((n,), 1024 * 1000, dtype=torch.int64, device=dev)
+    act_log = -512932943875505334261961442500000
+    a_lo, a_hi = act_log & ((1 << 64) - 1), act_log >> 64
+    lead = torch.zeros(n, dtype=torch.uint8, device=dev)
+
+    def leader():
+        rc = v.ouro_leader_check_batch_device(S(st.cuda_stream), n, hdr.beta_leader.data_ptr(),
+                                               sig_num.data_ptr(), sig_den.data_ptr(),
+                                               ctypes.c_int64(a_hi), ctypes.c_uint64(a_lo), 0,
+                                               lead.data_ptr())
+        _native.check(rc, "leader device batch")
+
     out = {}
+    leader()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(st)
+    for _ in range(reps):
+        leader()
+    e1.record(st)
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    out["leader"] = {"value": round(n / (ms * 1e-3), 1), "unit": "checks/s", "n": n,
+                     "ms_per_launch": round(ms, 3),
+                     "leaders": int((lead == 1).sum().item()),
+                     "badarg": int((lead == 0xFF).sum().item())}
     for name, fn, macs in (("vrf", vrf, 468_800), ("kes", kes, 190_912)):
         fn()
         torch.cuda.synchronize()
@@ -448,7 +478,7 @@ def main():
             try:
                 comp = component_rates(hdr, n)
                 for k, val in comp.items():
-                    if peak:
+                    if peak and "achieved_tmacs" in val:
                         val["roofline_frac"] = round(val["achieved_tmacs"] / peak, 4)
                     out[k] = val
             except Exception as e:  # noqa: BLE001
