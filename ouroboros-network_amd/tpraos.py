@@ -87,6 +87,12 @@ class HeaderBatch:
         kw = {f.name: getattr(self, f.name)[lo:hi] for f in fields(self) if f.name != "body"}
         return HeaderBatch(body=self.body, **kw)
 
+    def rows(self, idx) -> "HeaderBatch":
+        """The given rows (any order), sharing the body buffer."""
+        idx = np.asarray(idx, dtype=np.int64)
+        kw = {f.name: getattr(self, f.name)[idx] for f in fields(self) if f.name != "body"}
+        return HeaderBatch(body=self.body, **kw)
+
     def c_struct(self) -> _native.TPraosBatch:
         s = _native.TPraosBatch()
         s.n = len(self)

@@ -1,0 +1,81 @@
+"""GPU parity at BASELINE.json's full size (configs[3]: 1,048,576 headers on one
+GPU) through size-independent properties, plus a bit-exact oracle sample.
+
+1/8 of the device-synthesised headers get one byte incremented
+(applyCorruption-style, ouroboros-consensus-test/src/Test/Util/Corruption.hs)
+in exactly one of the four signed objects, so each header's verdict is known
+without the oracle: the corrupted check's bit is cleared and only that one.
+The VRF outputs of the header kernel equal those of the standalone VRF kernel
+(and are zero where the proof fails).  A random sample of 2,048 headers is
+compared with the CPU oracle bit for bit (verdicts and both 64-byte outputs).
+"""
+import os
+import sys
+
+import numpy as np
+import pytest
+
+import oracle_ffi as O
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_full_size_batch_with_corruptions():
+    import ctypes
+
+    import torch
+
+    sys.path.insert(0, ROOT)
+    import bench
+    from ouroboros_network_amd import _native
+
+    dev = torch.device("cuda:0")
+    n = 1 << 20
+    t, _ = bench.synth_headers(n, 1024, dev)
+    g = torch.Generator().manual_seed(20261016)
+    pick = torch.randint(0, 8, (n,), generator=g) == 0
+    which = torch.randint(0, 4, (n,), generator=g)
+    # (field, row width, verdict bit the corruption must clear)
+    fields = [("ocert_sigma", 64, 0x01), ("kes_sig", 448, 0x02), ("eta_proof", 80, 0x04),
+              ("leader_proof", 80, 0x08)]
+    expect = torch.full((n,), 15, dtype=torch.uint8)
+    for k, (name, w, bit) in enumerate(fields):
+        rows = torch.nonzero(pick & (which == k)).squeeze(1)
+        cols = torch.randint(0, w, (rows.numel(),), generator=g)
+        view = t[name].view(n, w)
+        view[rows.to(dev), cols.to(dev)] += 1
+        expect[rows] = 15 ^ bit
+    hdr = bench.DeviceHeaders(t, n, dev)
+    st = torch.cuda.current_stream()
+    hdr.launch(st)
+    torch.cuda.synchronize()
+    verdict = hdr.verdict.cpu()
+    assert torch.equal(verdict, expect), int((verdict != expect).sum())
+
+    # header-kernel eta outputs == standalone VRF kernel outputs (0 where invalid)
+    v = _native.load()
+    off = torch.arange(n, dtype=torch.int64, device=dev) * 32
+    ln = torch.full((n,), 32, dtype=torch.int32, device=dev)
+    beta = torch.zeros(n * 64, dtype=torch.uint8, device=dev)
+    ok = torch.zeros(n, dtype=torch.uint8, device=dev)
+    rc = v.ouro_vrf03_verify_batch_device(ctypes.c_void_p(st.cuda_stream), n,
+                                           t["vrf_vk"].data_ptr(), t["eta_proof"].data_ptr(),
+                                           t["eta_alpha"].data_ptr(), off.data_ptr(),
+                                           ln.data_ptr(), beta.data_ptr(), ok.data_ptr())
+    _native.check(rc, "vrf batch")
+    torch.cuda.synchronize()
+    assert torch.equal(ok.cpu(), ((expect & 0x04) != 0).to(torch.uint8))
+    assert torch.equal(beta, hdr.beta_eta)
+
+    # bit-exact oracle comparison on a random sample
+    rng = np.random.default_rng(5)
+    sample = np.sort(rng.choice(n, 2048, replace=False))
+    hb = hdr.host_sample(n).rows(sample)
+    wv, wbe, wbl = O.tpraos_verify_batch(hb, threads=min(16, os.cpu_count() or 1))
+    np.testing.assert_array_equal(verdict.numpy()[sample], wv)
+    be = hdr.beta_eta.cpu().numpy().reshape(n, 64)[sample]
+    bl = hdr.beta_leader.cpu().numpy().reshape(n, 64)[sample]
+    np.testing.assert_array_equal(be, wbe)
+    np.testing.assert_array_equal(bl, wbl)
