@@ -154,26 +154,6 @@ OURO_FI fe fe_select(const fe& a, const fe& b, bool c) {
   return h;
 }
 
-// acc += a * b (u32 x u32 -> u64).  OURO_MUL_VARIANT (experiments): 0 plain C,
-// 1 plain C with a scheduling barrier after each row of ten products, 2 every
-// product an ordered v_mad_u64_u32, so the ten columns of a row interleave.
-#ifndef OURO_MUL_VARIANT
-#define OURO_MUL_VARIANT 0
-#endif
-OURO_FI void ouro_mad(uint64_t& acc, uint32_t a, uint32_t b) {
-#if defined(__HIP_DEVICE_COMPILE__) && OURO_MUL_VARIANT == 2
-  uint64_t cc;
-  asm volatile("v_mad_u64_u32 %0, %1, %2, %3, %0" : "+v"(acc), "=s"(cc) : "v"(a), "v"(b));
-#else
-  acc += (uint64_t)a * b;
-#endif
-}
-#if defined(__HIP_DEVICE_COMPILE__) && OURO_MUL_VARIANT == 1
-#define OURO_ROW_BARRIER() __builtin_amdgcn_sched_barrier(0)
-#else
-#define OURO_ROW_BARRIER() ((void)0)
-#endif
-
 // Floor carry of a 10-column accumulator into a reduced element.  Two
 // interleaved chains (0..4 and 4..9) for ILP, then the 2^255 = 19 wrap.
 OURO_FI fe fe_carry64(uint64_t t[10]) {
@@ -257,9 +237,8 @@ OURO_FI fe fe_mul(const fe& f, const fe& g) {
       const int k = i + j;
       const uint32_t a = ((i & 1) && (j & 1)) ? f2[i] : f.v[i];
       const uint32_t b = (k >= 10) ? g19[j] : g.v[j];
-      ouro_mad(t[k >= 10 ? k - 10 : k], a, b);
+      t[k >= 10 ? k - 10 : k] += (uint64_t)a * b;
     }
-    OURO_ROW_BARRIER();
   }
   fe h = fe_carry64(t);
   OURO_TRK({

@@ -92,7 +92,7 @@ OURO_HD inline bool vrf_u_core(const uint32_t pk[8], const uint32_t pi[20], bool
   uint64_t* carr = reinterpret_cast<uint64_t*>(lane + kSlotCarry);
   carr[0] = sc_recode_carries<4, 33>(c);
   carr[2] = sc_recode_carries<kBW, 2 * kBDigitsHalf>(s);
-  dsm(lane, btab, dsm_cfg(33, 0, true, true, yslot, 1));
+  dsm(lane, btab, dsm_cfg(33, 0, true, yslot, 1));
   return ok;
 }
 
@@ -132,7 +132,7 @@ OURO_HD inline int32_t vrf_v_core(const uint32_t pk[8], const uint32_t pi[20], c
   uint64_t* carr = reinterpret_cast<uint64_t*>(lane + kSlotCarry);
   carr[0] = sc_recode_carries<4, 64>(s);
   carr[1] = sc_recode_carries<4, 33>(c);
-  dsm(lane, btab, dsm_cfg(64, 33, false, false, 0, 1));
+  dsm(lane, btab, dsm_cfg(64, 33, false, 0, 1));
   st_point_from_dsm(res, ptV, lane);
   ge_p3 G8 = ge_mul8(Gamma);
   st_point(res, ptG8, G8.X, G8.Y, G8.Z);

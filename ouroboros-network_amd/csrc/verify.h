@@ -152,16 +152,14 @@ OURO_HD inline void build_table(int32_t* tab, const ge_p3& P) {
 // cfg: bits 0..6 = number of active width-4 windows of scalar a1 (table 1),
 //      bits 8..14 = same for a2 (table 2, 0 = unused), bit 16 = add [b]B with
 //      b split at bit 128: its kBW-bit digits 0..7 go with B and 8..15 with
-//      B' = 2^128 B, so the doubling chain only spans 128 bits (bit 17, the
-//      split flag of earlier layouts, is implied and ignored),
+//      B' = 2^128 B, so the doubling chain only spans 128 bits,
 //      bits 20..21 / 22..23 = table slots (0..2) read for a1 / a2.
 // Reads a1/a2/b and their recoding carries from the lane slot, writes the
 // resulting p2 point to lane[kSlotOut..].  Out of line: the header kernel calls
 // it six times per item, and the loop body is the I-cache-critical code.
-constexpr uint32_t dsm_cfg(int nw1, int nw2, bool useB, bool splitB = false, int tab1 = 0,
-                           int tab2 = 1) {
+constexpr uint32_t dsm_cfg(int nw1, int nw2, bool useB, int tab1 = 0, int tab2 = 1) {
   return (uint32_t)nw1 | ((uint32_t)nw2 << 8) | (useB ? (1u << 16) : 0u) |
-         (splitB ? (1u << 17) : 0u) | ((uint32_t)tab1 << 20) | ((uint32_t)tab2 << 22);
+         ((uint32_t)tab1 << 20) | ((uint32_t)tab2 << 22);
 }
 
 OURO_NI void dsm(int32_t* lane, const int32_t* btab, uint32_t cfg) {
@@ -349,7 +347,7 @@ OURO_HD inline bool ed25519_verify_lane(const uint32_t sig[16], const uint32_t p
   // windows so that every scalar is < 2^(4 nw - 1) (top carry zero), <= 64
   int nw = wave_max_small((hs.bits + 4) >> 2);
   nw = nw < 1 ? 1 : (nw > 64 ? 64 : nw);
-  dsm(lane, btab, dsm_cfg(nw, nw, true, true, 0, 1));
+  dsm(lane, btab, dsm_cfg(nw, nw, true, 0, 1));
   const ge_p2 Q = dsm_result(lane);
   const bool ident = fe_iszero(Q.X) && fe_iszero(fe_sub(Q.Y, Q.Z));
   return ok && ident;
@@ -483,7 +481,7 @@ OURO_HD inline bool vrf03_verify_lane(uint32_t beta[16], const uint32_t pk[8],
   uint64_t* carr = reinterpret_cast<uint64_t*>(lane + kSlotCarry);
   carr[0] = sc_recode_carries<4, 33>(c);
   carr[2] = sc_recode_carries<kBW, 2 * kBDigitsHalf>(s);
-  dsm(lane, btab, dsm_cfg(33, 0, true, true));
+  dsm(lane, btab, dsm_cfg(33, 0, true));
   ge_p2 U = dsm_result(lane);
   // V = [s]H - [c]Gamma
   build_table(lane + kSlotTab1, Hp);

@@ -115,9 +115,9 @@ __global__ void __launch_bounds__(kBlock, COMP_WAVES) kcomp(int32_t* scratch, co
       carr[0] = sc_recode_carries<4, 64>(a1);
       carr[1] = sc_recode_carries<4, 64>(a2);
       carr[2] = sc_recode_carries<kBW, 2 * kBDigitsHalf>(w);
-      const uint32_t cfg = C == kDsmEd ? dsm_cfg(34, 34, true, true, 0, 1)
-                         : C == kDsmU  ? dsm_cfg(33, 0, true, true, 0, 1)
-                                       : dsm_cfg(64, 33, false, false, 0, 1);
+      const uint32_t cfg = C == kDsmEd ? dsm_cfg(34, 34, true, 0, 1)
+                         : C == kDsmU  ? dsm_cfg(33, 0, true, 0, 1)
+                                       : dsm_cfg(64, 33, false, 0, 1);
       dsm(lane, btab, cfg);
       acc += (uint32_t)lane[kSlotOut + (acc & 7)];
     } else if constexpr (C == kElligator) {
