@@ -96,9 +96,15 @@ class DeviceHeaders:
         self.s.n = n
         for k, v in t.items():
             setattr(self.s, k, v.data_ptr())
-        self.verdict = torch.zeros(n, dtype=torch.uint8, device=device)
-        self.beta_eta = torch.zeros(n * 64, dtype=torch.uint8, device=device)
-        self.beta_leader = torch.zeros(n * 64, dtype=torch.uint8, device=device)
+        # two output sets: the all-gather of step k reads one while step k+1
+        # writes the other (bench.py overlaps the collective with compute)
+        self.sets = [(torch.zeros(n, dtype=torch.uint8, device=device),
+                      torch.zeros(n * 64, dtype=torch.uint8, device=device),
+                      torch.zeros(n * 64, dtype=torch.uint8, device=device)) for _ in range(2)]
+        self.use(0)
+
+    def use(self, k: int) -> None:
+        self.verdict, self.beta_eta, self.beta_leader = self.sets[k]
 
     def launch(self, stream) -> None:
         from ouroboros_network_amd import _native
@@ -387,13 +393,33 @@ def main():
             local = local.cpu()
         return all_gather_results(local, n * world, world)
 
-    def step():
+    # the collective of step k runs on its own stream, overlapped with the
+    # kernel of step k+1 (double-buffered outputs); a set is rewritten only
+    # after the gather that read it has finished
+    comm = torch.cuda.Stream(device) if world > 1 else None
+    gdone = [None, None]
+
+    def step(k: int) -> None:
+        s = k % 2
+        if gdone[s] is not None:
+            stream.wait_event(gdone[s])
+        hdr.use(s)
         hdr.launch(stream)
         if world > 1:
-            gather()
+            if comm is None:
+                gather()
+                return
+            kev = torch.cuda.Event()
+            kev.record(stream)
+            with torch.cuda.stream(comm):
+                comm.wait_event(kev)
+                gather()
+                done = torch.cuda.Event()
+                done.record(comm)
+                gdone[s] = done
 
-    for _ in range(args.warmup):
-        step()
+    for w in range(args.warmup):
+        step(w)
     torch.cuda.synchronize()
     # correctness gate: every synthetic header must verify
     all_ok = bool((hdr.verdict == 15).all().item())
@@ -405,11 +431,23 @@ def main():
           for _ in range(args.steps)]
     t0 = time.perf_counter()
     for k in range(args.steps):
+        s = (args.warmup + k) % 2
+        if gdone[s] is not None:
+            stream.wait_event(gdone[s])
+        hdr.use(s)
         ev[k][0].record(stream)
         hdr.launch(stream)
         ev[k][1].record(stream)
         if world > 1:
-            gather()
+            if comm is None:
+                gather()
+            else:
+                with torch.cuda.stream(comm):
+                    comm.wait_event(ev[k][1])
+                    gather()
+                    done = torch.cuda.Event()
+                    done.record(comm)
+                    gdone[s] = done
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
