@@ -38,7 +38,7 @@ OURO_FI void sc_muladd(uint32_t out[8], const uint32_t a[8], const uint32_t b[8]
 // [k]B for k < L, through the shared multiplication routine (B table only)
 OURO_FI ge_p2 base_mul(const uint32_t k[8], int32_t* lane, const int32_t* btab) {
   st_words8(lane + kSlotB, k);
-  reinterpret_cast<uint64_t*>(lane + kSlotCarry)[2] = sc_recode_carries<kBW, 2 * kBDigitsHalf>(k);
+  reinterpret_cast<uint64_t*>(lane + kSlotCarry)[2] = sc_recode_b(k);
   dsm(lane, btab, dsm_cfg(0, 0, true));
   return dsm_result(lane);
 }

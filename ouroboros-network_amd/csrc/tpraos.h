@@ -91,7 +91,7 @@ OURO_HD inline bool vrf_u_core(const uint32_t pk[8], const uint32_t pi[20], bool
   st_words8(lane + kSlotB, s);
   uint64_t* carr = reinterpret_cast<uint64_t*>(lane + kSlotCarry);
   carr[0] = sc_recode_carries<4, 33>(c);
-  carr[2] = sc_recode_carries<kBW, 2 * kBDigitsHalf>(s);
+  carr[2] = sc_recode_b(s);
   dsm(lane, btab, dsm_cfg(33, 0, true, yslot, 1));
   return ok;
 }

@@ -45,10 +45,16 @@ constexpr int kLaneWords = kSlotOut + 36;         // 1028 words = 4112 B (16-B m
 // the doubling chain spans 128 bits) and each half is cut into signed digits
 // of kBW bits, one every kBW / 4 windows of the chain.  kBW = 16: 8 additions
 // per half from tables of 2^15 affine points (2 x 4 MiB, MALL/L2-resident).
-constexpr int kBW = 16;
+#ifndef OURO_BW
+#define OURO_BW 16
+#endif
+constexpr int kBW = OURO_BW;                       // 8, 12 or 16
 constexpr int kBStride = kBW / 4;                 // chain windows per B digit
-constexpr int kBDigitsHalf = 128 / kBW;           // digits per 128-bit half
-constexpr int kBTabEntries = 1 << (kBW - 1);      // [1..2^15]B, then [1..2^15](2^128 B)
+// widths dividing 128 recode b as one number (a carry out of the low half
+// continues in the high half); others recode each half alone, with headroom
+constexpr bool kBSplitRecode = (128 % kBW) != 0;
+constexpr int kBDigitsHalf = kBSplitRecode ? (128 + kBW) / kBW : 128 / kBW;
+constexpr int kBTabEntries = 1 << (kBW - 1);      // [1..2^(W-1)]B, then the same of 2^128 B
 constexpr int kNielsWords = 32;                   // 30 used, padded to 128 B
 constexpr size_t kBTabWords = 2 * (size_t)kBTabEntries * kNielsWords;
 
@@ -148,6 +154,39 @@ OURO_HD inline void build_table(int32_t* tab, const ge_p3& P) {
   }
 }
 
+// recoding carries of the B scalar (b < 2^253) for the split multiplication:
+// digits 0..D-1 of its low half at mask bits 0..D-1, of its high half at
+// D..2D-1 (one number when kBW divides 128, two otherwise)
+OURO_FI uint64_t sc_recode_b(const uint32_t s[8]) {
+  if constexpr (!kBSplitRecode) {
+    return sc_recode_carries<kBW, 2 * kBDigitsHalf>(s);
+  } else {
+  uint64_t mask = 0;
+#pragma unroll
+  for (int h = 0; h < 2; h++) {
+    uint32_t c = 0;
+#pragma unroll
+    for (int k = 0; k < kBDigitsHalf; k++) {
+      const int rel = kBW * k, bit = 128 * h + rel;
+      const int w = bit >> 5, sh = bit & 31;
+      const uint64_t two = (uint64_t)s[w] | ((w + 1 < 8 ? (uint64_t)s[w + 1] : 0ull) << 32);
+      uint32_t v = (uint32_t)(two >> sh) & ((1u << kBW) - 1);
+      if (128 - rel < kBW) v &= (1u << (128 - rel)) - 1;  // this half's bits only
+      mask |= (uint64_t)c << (kBDigitsHalf * h + k);
+      c = (v + c) > (1u << (kBW - 1)) ? 1u : 0u;
+    }
+  }
+  return mask;
+  }
+}
+
+// 160-bit stream shifted right by 0 < bits < 32
+OURO_FI void ss_shr5(uint32_t w[5], int bits) {
+#pragma unroll
+  for (int i = 0; i < 4; i++) w[i] = (w[i] >> bits) | (w[i + 1] << (32 - bits));
+  w[4] >>= bits;
+}
+
 // ---- the double-scalar multiplication ---------------------------------------
 // cfg: bits 0..6 = number of active width-4 windows of scalar a1 (table 1),
 //      bits 8..14 = same for a2 (table 2, 0 = unused), bit 16 = add [b]B with
@@ -174,16 +213,22 @@ OURO_NI void dsm(int32_t* lane, const int32_t* btab, uint32_t cfg) {
   const uint64_t* carr = reinterpret_cast<const uint64_t*>(lane + kSlotCarry);
   const uint64_t c1 = carr[0], c2 = carr[1], cb = carr[2];
   int top = nw1 > nw2 ? nw1 : nw2;
-  if (useB && top < 32) top = 32;
+  if (useB && top < kBStride * kBDigitsHalf) top = kBStride * kBDigitsHalf;
   // digit streams: window top-1 of a1/a2 at the top of the array
 #pragma unroll 1
   for (int s = top; s < 64; s++) {
     ss_shl<8>(a1, 4);
     ss_shl<8>(a2, 4);
   }
-  // b: two 128-bit streams (its low and high halves), kBW bits per B window
-  uint32_t blo[4] = {b[0], b[1], b[2], b[3]};
-  uint32_t bhi[4] = {b[4], b[5], b[6], b[7]};
+  // b: two streams (its low and high 128-bit halves, the top digit's bits on
+  // top of 160), kBW bits per B window
+  constexpr int kBPre = 160 - kBW * kBDigitsHalf;
+  uint32_t blo[5] = {0, b[0], b[1], b[2], b[3]};
+  uint32_t bhi[5] = {0, b[4], b[5], b[6], b[7]};
+  if (kBPre < 32) {
+    ss_shr5(blo, 32 - kBPre);
+    ss_shr5(bhi, 32 - kBPre);
+  }
   uint32_t prefetch = 0;
   // t starts as the identity in p1p1 form (X/Z = 0, Y/T = 1)
   ge_p1p1 t{fe_zero(), fe_one(), fe_one(), fe_one()};
@@ -191,7 +236,7 @@ OURO_NI void dsm(int32_t* lane, const int32_t* btab, uint32_t cfg) {
   for (int j = top - 1; j >= 0; j--) {
     // this window's digits (wave-uniform activity, per-lane values)
     const bool act1 = j < nw1, act2 = j < nw2;
-    const bool actB = useB && (j % kBStride) == 0 && j < 32;
+    const bool actB = useB && (j % kBStride) == 0 && j < kBStride * kBDigitsHalf;
     const bool actB2 = actB;
     int32_t d1 = 0, d2 = 0, d3 = 0, d4 = 0;
     if (act1) d1 = sc_digit_from<4>(a1[7] >> 28, c1, j, 64);
@@ -200,10 +245,11 @@ OURO_NI void dsm(int32_t* lane, const int32_t* btab, uint32_t cfg) {
     ss_shl<8>(a2, 4);
     if (actB) {
       const int k = j / kBStride;
-      d3 = sc_digit_from<kBW>(blo[3] >> (32 - kBW), cb, k, 2 * kBDigitsHalf);
-      d4 = sc_digit_from<kBW>(bhi[3] >> (32 - kBW), cb, k + kBDigitsHalf, 2 * kBDigitsHalf);
-      ss_shl<4>(blo, kBW);
-      ss_shl<4>(bhi, kBW);
+      d3 = sc_digit_from<kBW>(blo[4] >> (32 - kBW), cb, k,
+                              kBSplitRecode ? kBDigitsHalf : 2 * kBDigitsHalf);
+      d4 = sc_digit_from<kBW>(bhi[4] >> (32 - kBW), cb, k + kBDigitsHalf, 2 * kBDigitsHalf);
+      ss_shl<5>(blo, kBW);
+      ss_shl<5>(bhi, kBW);
     }
     // touch this window's per-lane table entries now, so that the loads
     // after the four doublings hit L2 instead of waiting on HBM
@@ -343,7 +389,7 @@ OURO_HD inline bool ed25519_verify_lane(const uint32_t sig[16], const uint32_t p
   uint64_t* carr = reinterpret_cast<uint64_t*>(lane + kSlotCarry);
   carr[0] = sc_recode_carries<4, 64>(hs.c0);
   carr[1] = sc_recode_carries<4, 64>(hs.c1);
-  carr[2] = sc_recode_carries<kBW, 2 * kBDigitsHalf>(b);
+  carr[2] = sc_recode_b(b);
   // windows so that every scalar is < 2^(4 nw - 1) (top carry zero), <= 64
   int nw = wave_max_small((hs.bits + 4) >> 2);
   nw = nw < 1 ? 1 : (nw > 64 ? 64 : nw);
@@ -480,7 +526,7 @@ OURO_HD inline bool vrf03_verify_lane(uint32_t beta[16], const uint32_t pk[8],
   st_words8(lane + kSlotB, s);
   uint64_t* carr = reinterpret_cast<uint64_t*>(lane + kSlotCarry);
   carr[0] = sc_recode_carries<4, 33>(c);
-  carr[2] = sc_recode_carries<kBW, 2 * kBDigitsHalf>(s);
+  carr[2] = sc_recode_b(s);
   dsm(lane, btab, dsm_cfg(33, 0, true));
   ge_p2 U = dsm_result(lane);
   // V = [s]H - [c]Gamma

@@ -114,7 +114,7 @@ __global__ void __launch_bounds__(kBlock, COMP_WAVES) kcomp(int32_t* scratch, co
       uint64_t* carr = reinterpret_cast<uint64_t*>(lane + kSlotCarry);
       carr[0] = sc_recode_carries<4, 64>(a1);
       carr[1] = sc_recode_carries<4, 64>(a2);
-      carr[2] = sc_recode_carries<kBW, 2 * kBDigitsHalf>(w);
+      carr[2] = sc_recode_b(w);
       const uint32_t cfg = C == kDsmEd ? dsm_cfg(34, 34, true, 0, 1)
                          : C == kDsmU  ? dsm_cfg(33, 0, true, 0, 1)
                                        : dsm_cfg(64, 33, false, 0, 1);
