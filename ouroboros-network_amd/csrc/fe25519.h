@@ -113,6 +113,17 @@ OURO_FI fe fe_sqrtm1() {
 }
 // Montgomery A = 486662 (curve25519), used by Elligator2
 OURO_FI fe fe_mont_a() { return fe_make(486662, 0, 0, 0, 0, 0, 0, 0, 0, 0); }
+// A^2 and (A + 2) A (Elligator2's sqrt-ratio numerator), 1 + sqrt(-1), 1 - sqrt(-1)
+OURO_FI fe fe_mont_a2() { return fe_make(12721188, 3529, 0, 0, 0, 0, 0, 0, 0, 0); }
+OURO_FI fe fe_mont_a2a() { return fe_make(13694512, 3529, 0, 0, 0, 0, 0, 0, 0, 0); }
+OURO_FI fe fe_one_plus_i() {
+  return fe_make(34513073, 25610706, 9377949, 3500415, 12389472, 33281959, 41962654, 31548777,
+                 326685, 11406482);
+}
+OURO_FI fe fe_one_minus_i() {
+  return fe_make(32595774, 7943725, 57730914, 30054016, 54719391, 272472, 25146209, 2005654,
+                 66782178, 22147949);
+}
 OURO_FI fe fe_zero() { return fe_make(0, 0, 0, 0, 0, 0, 0, 0, 0, 0); }
 OURO_FI fe fe_one() { return fe_make(1, 0, 0, 0, 0, 0, 0, 0, 0, 0); }
 OURO_FI fe fe_two() { return fe_make(2, 0, 0, 0, 0, 0, 0, 0, 0, 0); }

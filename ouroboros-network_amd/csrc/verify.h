@@ -403,46 +403,52 @@ OURO_HD inline bool ed25519_verify_lane(const uint32_t sig[16], const uint32_t p
 // libsodium 1.0.18 ge25519_from_uniform with x_sign = 0 (the VRF clears bit 255
 // of r before calling it): returns [8] of the Elligator2 image.
 //
-// Same point as the reference, two exponentiations instead of four.  With
-// D = 1 + 2r^2 the Montgomery x = -A/D is kept as a fraction:
-//   e = x^3 + A x^2 + x has chi(e) = chi(-A W D), W = D^2 - 2 A^2 r^2
-//   (e and -A W D differ by the square D^4);  -x - A = -2 A r^2 / D, so
-//   x_final = Xn / D with Xn = -A (chi = 1 or 0) or -2 A r^2 (chi = -1);
-//   y_ed = (x_final - 1)/(x_final + 1) = (Xn - D)/(Xn + D) = n/m
-// and the Edwards x comes straight from the ratio
-//   x^2 = (y^2 - 1)/(d y^2 + 1) = (n^2 - m^2)/(d n^2 + m^2)
-// with one square-root-of-ratio exponentiation, sign chosen even as
-// ge25519_frombytes does for the (canonical, sign 0) encoding of y_ed.
-// D != 0 (-2 is a non-square mod p) and m != 0 (neither (A-1)/2 nor
-// 1/(2(A-1)) is a square; tools/check_elligator_exceptions.py), so no inverse
-// of zero can occur where libsodium would have computed one.
+// Same point as the reference, one exponentiation instead of four.  With
+// D = 1 + 2r^2 the candidate Montgomery x's are x1 = -A/D and x2 = -x1 - A =
+// 2 r^2 x1, and x1^2 + A x1 + 1 = x2^2 + A x2 + 1 = 1 - x1 x2 = W / D^2 with
+// W = D^2 - 2 A^2 r^2.  The Edwards x of the Montgomery point (u, v) is
+// sqrt(-(A+2)) u / v, whose square is
+//   rho(u) = -(A+2) u^2 / g(u) = -(A+2) u / (u^2 + A u + 1),
+// so rho1 = rho(x1) = (A+2) A D / W, rho2 = rho(x2) = 2 r^2 rho1, and
+// chi(rho1) = chi(g(x1)) (-(A+2) is a square): libsodium's chi test is the
+// squareness of rho1.  One sqrt-ratio exponentiation of num/den = rho1 gives
+// beta with beta^2 den = lambda num, lambda a 4th root of unity:
+//   lambda =  1: x = beta            lambda =  i: x = r beta (1 - i)
+//   lambda = -1: x = beta i          lambda = -i: x = r beta (1 + i)
+// (2/i = (1 - i)^2, 2/(-i) = (1 + i)^2, so (r beta (1 -+ i))^2 = rho2).  The
+// root's sign is then made even, as ge25519_frombytes does for the
+// (canonical, sign 0) encoding of y_ed = (x_final - 1)/(x_final + 1) =
+// (Xn - D)/(Xn + D) = n/m with Xn = -A (square) or -2 A r^2 (non-square).
+// D != 0 (-2 is a non-square mod p), W != 0 (u^2 + A u + 1 has no root:
+// A^2 - 4 is a non-square) and m != 0 (neither (A-1)/2 nor 1/(2(A-1)) is a
+// square; tools/check_elligator_exceptions.py), so no inverse of zero can
+// occur where libsodium would have computed one.
 OURO_HD inline ge_p3 elligator2_h(const uint32_t r[8]) {
-  const fe one = fe_one();
   const fe A = fe_mont_a();
   fe rr = fe_from_words(r);
   fe r2 = fe_sq(rr);
-  fe D = fe_carry(fe_add(fe_add(r2, r2), one));         // 1 + 2 r^2 (re-balanced:
+  fe D = fe_carry(fe_add(fe_add(r2, r2), fe_one()));    // 1 + 2 r^2 (re-balanced:
                                                         // n = Xn - D below sums 4 terms)
-  fe A2r2 = fe_mul(fe_mul(A, A), r2);                   // A^2 r^2
-  fe W = fe_sub4(fe_sq(D), fe_add(A2r2, A2r2));         // D^2 - 2 A^2 r^2
-  fe e = fe_neg(fe_mul(fe_mul(W, A), D));               // -A W D
-  fe chi = fe_mul(fe_sq(fe_sq(fe_pow22523(e))), fe_sq(e));  // e^((p-1)/2)
-  uint32_t cw[8];
-  fe_to_words(cw, chi);
-  const bool e_is_minus_1 = (cw[0] >> 8) & 1;  // libsodium's byte-1 test
-  fe Ar2 = fe_mul(A, r2);
-  fe Xn = fe_carry(fe_select(fe_neg4(fe_add(Ar2, Ar2)), fe_neg(A), e_is_minus_1));
-  fe n = fe_sub(Xn, D), m = fe_add(Xn, D);
-  // x = sqrt(u / v), u = n^2 - m^2, v = d n^2 + m^2
-  fe n2 = fe_sq(n), m2 = fe_sq(m);
-  fe u = fe_sub(n2, m2);
-  fe v = fe_add(fe_mul(n2, fe_d()), m2);
-  fe v3 = fe_mul(fe_sq(v), v);
-  fe x = fe_mul(fe_mul(u, v3), fe_pow22523(fe_mul(fe_mul(fe_sq(v3), v), u)));
-  fe vxx = fe_mul(fe_sq(x), v);
-  const bool m_root = fe_iszero(fe_sub4(vxx, u));
-  x = fe_select(x, fe_mul(x, fe_sqrtm1()), m_root);
+  fe A2r2 = fe_mul(fe_mont_a2(), r2);                   // A^2 r^2
+  fe W = fe_carry(fe_sub4(fe_sq(D), fe_add(A2r2, A2r2)));  // D^2 - 2 A^2 r^2
+  fe num = fe_mul(fe_mont_a2a(), D);                    // (A + 2) A D
+  // beta = num W^3 (num W^7)^((p-5)/8)
+  fe W3 = fe_mul(fe_sq(W), W);
+  fe W7 = fe_mul(fe_sq(W3), W);
+  fe beta = fe_mul(fe_mul(num, W3), fe_pow22523(fe_mul(num, W7)));
+  fe vxx = fe_mul(fe_sq(beta), W);
+  const bool lam_p1 = fe_iszero(fe_sub4(vxx, num));
+  const bool lam_m1 = fe_iszero(fe_add(vxx, num));
+  const bool lam_pi = fe_iszero(fe_sub4(vxx, fe_mul(num, fe_sqrtm1())));
+  const bool nonsq = !(lam_p1 || lam_m1);
+  const fe F = fe_select(fe_select(fe_one_minus_i(), fe_one_plus_i(), lam_pi),
+                         fe_select(fe_one(), fe_sqrtm1(), lam_p1), nonsq);
+  fe x = fe_mul(beta, F);
+  x = fe_select(fe_mul(x, rr), x, nonsq);
   x = fe_select(fe_neg(x), x, fe_isnegative(x));  // sign bit 0: even x
+  fe Ar2 = fe_mul(A, r2);
+  fe Xn = fe_carry(fe_select(fe_neg4(fe_add(Ar2, Ar2)), fe_neg(A), nonsq));
+  fe n = fe_sub(Xn, D), m = fe_add(Xn, D);
   const fe nc = fe_carry(n);
   ge_p3 P{fe_mul(x, m), nc, m, fe_mul(x, nc)};
   return ge_mul8(P);
