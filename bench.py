@@ -322,6 +322,48 @@ def latency_leg(hdr, batch: int, iters: int, cpu_threads: int, cpu_iters: int):
                            "iters": cpu_iters}}
 
 
+def e2e_leg(hdr, n: int, reps: int = 3):
+    """Host buffers in, host buffers out (SURVEY.md §8(d) "end-to-end"): the
+    whole n-header batch from pageable host memory through the C ABI's
+    ouro_tpraos_verify_batch -- PCIe H2D, the header kernel, D2H of verdicts
+    and both VRF outputs -- wall clock per call.  The default path pipelines
+    chunks over two streams; OURO_HOST_CHUNK=0 (one-piece staging) is timed
+    beside it.  Never `value` (inputs are not HBM-resident here)."""
+    from ouroboros_network_amd.tpraos import verify_headers
+
+    hb = hdr.host_sample(n)
+    in_bytes = sum(getattr(hb, k).nbytes for k in hb.__dataclass_fields__)
+    dv = hdr.verdict.cpu().numpy()
+    dbe = hdr.beta_eta.cpu().numpy().reshape(n, 64)
+    dbl = hdr.beta_leader.cpu().numpy().reshape(n, 64)
+    res = {"workload": f"configs[3] batch of {n} headers in pageable host memory, "
+                       "ouro_tpraos_verify_batch (H2D + kernel + D2H)",
+           "h2d_bytes": int(in_bytes), "d2h_bytes": int(129 * n)}
+    saved = os.environ.get("OURO_HOST_CHUNK")
+    try:
+        for name, chunk in (("pipelined", saved), ("one_piece", "0")):
+            if chunk is None:
+                os.environ.pop("OURO_HOST_CHUNK", None)
+            else:
+                os.environ["OURO_HOST_CHUNK"] = chunk
+            v, be, bl = verify_headers(hb)  # warm: device/pinned buffers grown
+            t = []
+            for _ in range(reps):
+                t0 = time.perf_counter()
+                v, be, bl = verify_headers(hb)
+                t.append(time.perf_counter() - t0)
+            best = min(t)
+            res[name] = {"headers_per_s": round(n / best, 1), "ms": round(best * 1e3, 2),
+                         "equals_device_path": bool((v == dv).all() and (be == dbe).all()
+                                                    and (bl == dbl).all())}
+    finally:
+        if saved is None:
+            os.environ.pop("OURO_HOST_CHUNK", None)
+        else:
+            os.environ["OURO_HOST_CHUNK"] = saved
+    return res
+
+
 def load_pmc_traffic():
     """HBM bytes per launch of the header kernel from the committed PMC run."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
@@ -344,6 +386,8 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-extras", action="store_true")
     ap.add_argument("--no-latency", action="store_true")
+    ap.add_argument("--no-e2e", action="store_true",
+                    help="skip the host-buffer (PCIe-inclusive) end-to-end leg")
     ap.add_argument("--lat-iters", type=int, default=2000,
                     help="configs[4] 64-header plan launches timed for p50/p99")
     ap.add_argument("--lat-cpu-iters", type=int, default=50)
@@ -521,6 +565,11 @@ def main():
                     out[k] = val
             except Exception as e:  # noqa: BLE001
                 out["components_error"] = str(e)
+        if not args.no_e2e and world == 1:
+            try:
+                out["e2e"] = e2e_leg(hdr, n)
+            except Exception as e:  # noqa: BLE001
+                out["e2e"] = {"error": str(e)}
         if not args.no_latency and world == 1:
             try:
                 out["latency"] = latency_leg(hdr, 64, args.lat_iters, min(16, os.cpu_count() or 1),

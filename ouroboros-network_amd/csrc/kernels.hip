@@ -463,11 +463,12 @@ struct Stager {
   hipStream_t st;
   int slot = 0;
   int rc = OURO_OK;
+  Buf* bufs = t_ctx.in;  // device buffers, one per up()/out() call
   template <class T>
   T* up(const T* host, size_t count) {
     if (rc) return nullptr;
     const size_t bytes = std::max<size_t>(count * sizeof(T), 16);
-    Buf& b = t_ctx.in[slot++];
+    Buf& b = bufs[slot++];
     if ((rc = ensure(b, bytes))) return nullptr;
     if (count) {
       hipError_t e = hipMemcpyAsync(b.p, host, count * sizeof(T), hipMemcpyHostToDevice, st);
@@ -478,7 +479,7 @@ struct Stager {
   template <class T>
   T* out(size_t count) {
     if (rc) return nullptr;
-    Buf& b = t_ctx.in[slot++];
+    Buf& b = bufs[slot++];
     if ((rc = ensure(b, std::max<size_t>(count * sizeof(T), 16)))) return nullptr;
     return static_cast<T*>(b.p);
   }
@@ -616,6 +617,141 @@ int ouro_sum6kes_verify_batch(size_t n, const uint8_t* vk, const uint32_t* t, co
   return OURO_OK;
 }
 
+}  // extern "C"
+
+namespace {
+// ---- pipelined host-buffer header batches ----
+// A large batch from pageable host memory is cut into chunks of one full grid
+// of lanes.  Two slots (stream, device buffers, pinned result staging) take
+// turns: while chunk c's kernel runs on one stream, the host uploads chunk
+// c + 1 on the other and copies chunk c - 1's results out, so PCIe and the
+// host copies hide behind the kernel instead of adding to it.
+struct PipeSlot {
+  hipStream_t st = nullptr;
+  hipEvent_t done = nullptr;
+  Buf in[18];
+  uint8_t* h_out = nullptr;  // pinned: verdict (m) | beta_eta (64 m) | beta_leader (64 m)
+  size_t h_cap = 0;
+  std::vector<uint64_t> off;  // body offsets rebased to the chunk's body span
+  size_t lo = 0, m = 0;
+  bool busy = false;
+};
+struct Pipe {
+  int dev = -1;
+  PipeSlot s[2];
+};
+thread_local Pipe t_pipe;
+
+int pipe_slots(int dev) {
+  if (t_pipe.dev == dev) return OURO_OK;
+  for (PipeSlot& p : t_pipe.s) {
+    OURO_HIP(hipStreamCreateWithFlags(&p.st, hipStreamNonBlocking));
+    OURO_HIP(hipEventCreateWithFlags(&p.done, hipEventDisableTiming));
+  }
+  t_pipe.dev = dev;
+  return OURO_OK;
+}
+
+int pipe_drain(PipeSlot& p, uint8_t* verdict, uint8_t* beta_eta, uint8_t* beta_leader) {
+  if (!p.busy) return OURO_OK;
+  p.busy = false;
+  OURO_HIP(hipEventSynchronize(p.done));
+  memcpy(verdict + p.lo, p.h_out, p.m);
+  if (beta_eta) memcpy(beta_eta + 64 * p.lo, p.h_out + p.m, 64 * p.m);
+  if (beta_leader) memcpy(beta_leader + 64 * p.lo, p.h_out + 65 * p.m, 64 * p.m);
+  return OURO_OK;
+}
+
+int pipe_chunk(PipeSlot& p, const ouro_tpraos_batch* b, size_t lo, size_t m, bool be, bool bl) {
+  uint64_t blo = ~0ull, bhi = 0;
+  for (size_t i = lo; i < lo + m; i++) {
+    if (b->body_len[i] == 0) continue;
+    blo = std::min<uint64_t>(blo, b->body_off[i]);
+    bhi = std::max<uint64_t>(bhi, b->body_off[i] + b->body_len[i]);
+  }
+  if (bhi == 0) blo = 0;
+  if (bhi > blo && !b->body) return fail(OURO_EINVAL, "null body buffer");
+  p.off.resize(m);
+  for (size_t i = 0; i < m; i++)
+    p.off[i] = b->body_len[lo + i] ? b->body_off[lo + i] - blo : 0;
+  Stager sg{p.st};
+  sg.bufs = p.in;
+  ouro_tpraos_batch d;
+  d.n = m;
+  d.issuer_vk = sg.up(b->issuer_vk + 32 * lo, 32 * m);
+  d.vrf_vk = sg.up(b->vrf_vk + 32 * lo, 32 * m);
+  d.eta_proof = sg.up(b->eta_proof + 80 * lo, 80 * m);
+  d.leader_proof = sg.up(b->leader_proof + 80 * lo, 80 * m);
+  d.eta_alpha = sg.up(b->eta_alpha + 32 * lo, 32 * m);
+  d.leader_alpha = sg.up(b->leader_alpha + 32 * lo, 32 * m);
+  d.hot_vk = sg.up(b->hot_vk + 32 * lo, 32 * m);
+  d.ocert_counter = sg.up(b->ocert_counter + lo, m);
+  d.ocert_kes_period = sg.up(b->ocert_kes_period + lo, m);
+  d.ocert_sigma = sg.up(b->ocert_sigma + 64 * lo, 64 * m);
+  d.kes_t = sg.up(b->kes_t + lo, m);
+  d.kes_sig = sg.up(b->kes_sig + 448 * lo, 448 * m);
+  d.body = sg.up(bhi > blo ? b->body + blo : b->body, (size_t)(bhi - blo));
+  d.body_off = sg.up(p.off.data(), m);
+  d.body_len = sg.up(b->body_len + lo, m);
+  uint8_t* dver = sg.out<uint8_t>(m);
+  uint8_t* dbe = sg.out<uint8_t>(64 * m);
+  uint8_t* dbl = sg.out<uint8_t>(64 * m);
+  if (sg.rc) return sg.rc;
+  int rc = launch_hdr(p.st, d, dver, dbe, dbl);
+  if (rc) return rc;
+  if (p.h_cap < 129 * m) {
+    if (p.h_out) OURO_HIP(hipHostFree(p.h_out));
+    p.h_out = nullptr;
+    p.h_cap = 0;
+    OURO_HIP(hipHostMalloc(reinterpret_cast<void**>(&p.h_out), 129 * m, hipHostMallocDefault));
+    p.h_cap = 129 * m;
+  }
+  OURO_HIP(hipMemcpyAsync(p.h_out, dver, m, hipMemcpyDeviceToHost, p.st));
+  if (be) OURO_HIP(hipMemcpyAsync(p.h_out + m, dbe, 64 * m, hipMemcpyDeviceToHost, p.st));
+  if (bl) OURO_HIP(hipMemcpyAsync(p.h_out + 65 * m, dbl, 64 * m, hipMemcpyDeviceToHost, p.st));
+  OURO_HIP(hipEventRecord(p.done, p.st));
+  p.lo = lo;
+  p.m = m;
+  p.busy = true;
+  return OURO_OK;
+}
+
+// headers per chunk: one full grid of the header kernel (OURO_HOST_CHUNK
+// overrides; 0 = the whole batch in one piece)
+size_t host_chunk(DeviceState* ds) {
+  if (const char* e = getenv("OURO_HOST_CHUNK")) return (size_t)strtoull(e, nullptr, 10);
+  return (size_t)ds->max_blocks[kHdr] * kBlock;
+}
+
+int hdr_batch_pipelined(const ouro_tpraos_batch* b, size_t chunk, uint8_t* verdict,
+                        uint8_t* beta_eta, uint8_t* beta_leader) {
+  int dev, rc = current_device(&dev);
+  if (rc) return rc;
+  if ((rc = pipe_slots(dev))) return rc;
+  size_t c = 0;
+  for (size_t lo = 0; lo < b->n && !rc; lo += chunk, c++) {
+    PipeSlot& p = t_pipe.s[c & 1];
+    rc = pipe_drain(p, verdict, beta_eta, beta_leader);
+    if (!rc)
+      rc = pipe_chunk(p, b, lo, std::min(chunk, b->n - lo), beta_eta != nullptr,
+                      beta_leader != nullptr);
+  }
+  // older chunk first; on an error, still wait for everything in flight
+  for (int k = 0; k < 2; k++) {
+    PipeSlot& p = t_pipe.s[(c + k) & 1];
+    if (rc) {
+      (void)hipStreamSynchronize(p.st);
+      p.busy = false;
+    } else {
+      rc = pipe_drain(p, verdict, beta_eta, beta_leader);
+    }
+  }
+  return rc;
+}
+}  // namespace
+
+extern "C" {
+
 int ouro_tpraos_verify_batch(const ouro_tpraos_batch* b, uint8_t* verdict, uint8_t* beta_eta,
                              uint8_t* beta_leader) {
   if (!b) return fail(OURO_EINVAL, "null batch");
@@ -625,9 +761,13 @@ int ouro_tpraos_verify_batch(const ouro_tpraos_batch* b, uint8_t* verdict, uint8
       !b->leader_alpha || !b->hot_vk || !b->ocert_counter || !b->ocert_kes_period ||
       !b->ocert_sigma || !b->kes_t || !b->kes_sig || !b->body_off || !b->body_len || !verdict)
     return fail(OURO_EINVAL, "null argument");
-  hipStream_t st;
-  int rc = thread_stream(&st);
+  DeviceState* ds;
+  int rc = device_state(&ds);
   if (rc) return rc;
+  const size_t chunk = host_chunk(ds);
+  if (chunk && n > chunk) return hdr_batch_pipelined(b, chunk, verdict, beta_eta, beta_leader);
+  hipStream_t st;
+  if ((rc = thread_stream(&st))) return rc;
   const size_t span = span_of(n, b->body_off, b->body_len);
   if (span && !b->body) return fail(OURO_EINVAL, "null body buffer");
   Stager sg{st};

@@ -253,6 +253,42 @@ def test_lowlat_equals_throughput_and_oracle(gpu_lib, kats):
         np.testing.assert_array_equal(bl, wbl[lo:hi])
 
 
+def test_pipelined_host_batches(gpu_lib, kats, monkeypatch):
+    """Host-buffer header batches larger than one chunk go through the
+    two-stream pipeline (kernels.hip hdr_batch_pipelined): same verdicts and
+    outputs as one-piece staging and the oracle, for ragged chunk sizes, rows
+    in shuffled order (bodies not monotonic in the buffer, with gaps) and an
+    empty body in the middle of a chunk."""
+    from ouroboros_network_amd.tpraos import HeaderBatch, verify_headers
+
+    base = _golden_variants(kats)
+    n = len(base)
+    rng = np.random.default_rng(11)
+    order = rng.permutation(n)
+    # re-lay the bodies: reversed row order, 3-byte gaps between them
+    blens = base.body_len.astype(np.int64)
+    new_off = np.zeros(n, dtype=np.uint64)
+    chunks, pos = [], 0
+    for i in reversed(range(n)):
+        o = int(base.body_off[i])
+        chunks.append(bytes(3) + base.body[o:o + int(blens[i])].tobytes())
+        new_off[i] = pos + 3
+        pos += 3 + int(blens[i])
+    body = np.frombuffer(b"".join(chunks), dtype=np.uint8)
+    kw = {k: getattr(base, k) for k in HeaderBatch.__dataclass_fields__ if k != "body"}
+    kw["body_off"] = new_off
+    batch = HeaderBatch(body=body, **kw).rows(order)
+    batch.body_len[5] = 0  # an empty body: its KES leaf check fails, nothing else
+    wv, wbe, wbl = O.tpraos_verify_batch(batch)
+    assert wv[5] & 0x02 == 0
+    for chunk in ("0", "1", "7", "64", str(n - 1)):
+        monkeypatch.setenv("OURO_HOST_CHUNK", chunk)
+        v, be, bl = verify_headers(batch)
+        np.testing.assert_array_equal(v, wv)
+        np.testing.assert_array_equal(be, wbe)
+        np.testing.assert_array_equal(bl, wbl)
+
+
 def test_header_plan_replays(gpu_lib, kats):
     """The captured-graph plan over 64-header windows (BASELINE configs[4]):
     every window and a ragged tail match the oracle; replays are independent

@@ -79,3 +79,12 @@ def test_full_size_batch_with_corruptions():
     bl = hdr.beta_leader.cpu().numpy().reshape(n, 64)[sample]
     np.testing.assert_array_equal(be, wbe)
     np.testing.assert_array_equal(bl, wbl)
+
+    # the same 1M headers from pageable host memory through the host-buffer
+    # ABI (two-stream chunked pipeline) give the device path's results
+    from ouroboros_network_amd.tpraos import verify_headers
+
+    hv, hbe, hbl = verify_headers(hdr.host_sample(n))
+    np.testing.assert_array_equal(hv, verdict.numpy())
+    np.testing.assert_array_equal(hbe.reshape(-1), hdr.beta_eta.cpu().numpy())
+    np.testing.assert_array_equal(hbl.reshape(-1), hdr.beta_leader.cpu().numpy())

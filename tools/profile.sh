@@ -10,7 +10,7 @@ set -euo pipefail
 TAG=${1:-r01}
 HEADERS=${HEADERS:-262144}
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-B="python3 bench.py --no-cpu --no-extras --no-latency"
+B="python3 bench.py --no-cpu --no-extras --no-latency --no-e2e"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$TAG -o run \
   -- $B --steps 3 > gpurun_out/prof_$TAG.bench.json
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch_$TAG -o run \
