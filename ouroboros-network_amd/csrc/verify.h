@@ -201,6 +201,9 @@ constexpr uint32_t dsm_cfg(int nw1, int nw2, bool useB, int tab1 = 0, int tab2 =
          ((uint32_t)tab1 << 20) | ((uint32_t)tab2 << 22);
 }
 
+#ifndef OURO_DSM_SKIP_ID
+#define OURO_DSM_SKIP_ID 1  // A/B switch: 0 = doublings/addition from the identity kept
+#endif
 OURO_NI void dsm(int32_t* lane, const int32_t* btab, uint32_t cfg) {
   const int nw1 = (int)(cfg & 0x7f), nw2 = (int)((cfg >> 8) & 0x7f);
   const bool useB = (cfg >> 16) & 1;
@@ -232,6 +235,7 @@ OURO_NI void dsm(int32_t* lane, const int32_t* btab, uint32_t cfg) {
   uint32_t prefetch = 0;
   // t starts as the identity in p1p1 form (X/Z = 0, Y/T = 1)
   ge_p1p1 t{fe_zero(), fe_one(), fe_one(), fe_one()};
+  bool fresh = true;  // t is the identity (wave-uniform)
 #pragma unroll 1
   for (int j = top - 1; j >= 0; j--) {
     // this window's digits (wave-uniform activity, per-lane values)
@@ -265,8 +269,11 @@ OURO_NI void dsm(int32_t* lane, const int32_t* btab, uint32_t cfg) {
       pf5 = (uint32_t)btab[(size_t)(i3 > 0 ? i3 : 0) * kNielsWords];
       pf6 = (uint32_t)btab[((size_t)kBTabEntries + (i4 > 0 ? i4 : 0)) * kNielsWords];
     }
+    // (the top window starts from the identity: its doublings are skipped)
+    if (!OURO_DSM_SKIP_ID || j != top - 1) {
 #pragma unroll 1
-    for (int k = 0; k < 4; k++) t = ge_p2_dbl(ge_p1p1_to_p2(t));
+      for (int k = 0; k < 4; k++) t = ge_p2_dbl(ge_p1p1_to_p2(t));
+    }
     prefetch ^= pf1 ^ pf2 ^ pf3 ^ pf4 ^ pf5 ^ pf6;
     // up to four additions, each from a wave-uniform source
 #pragma unroll 1
@@ -286,6 +293,14 @@ OURO_NI void dsm(int32_t* lane, const int32_t* btab, uint32_t cfg) {
         q = ge_cached{nq.yplusx, nq.yminusx, fe_two(), nq.xy2d};
       }
       if (mag == 0) q = ge_cached_identity();
+      if (OURO_DSM_SKIP_ID && fresh) {
+        // t is still the identity: O +- q = (2x, 2y, 2z, 2z) with no multiply
+        const fe qa = fe_select(q.YminusX, q.YplusX, neg);
+        const fe qb = fe_select(q.YplusX, q.YminusX, neg);
+        t = ge_p1p1{fe_carry(fe_sub4(qa, qb)), fe_carry(fe_add(qa, qb)), q.Z2, q.Z2};
+        fresh = false;
+        continue;
+      }
       t = ge_add_cached(ge_p1p1_to_p3(t), q, neg, src >= 2);
     }
   }
