@@ -45,12 +45,19 @@ def all_gather_results(local, n_total: int, world: int, group=None):
     import torch.distributed as dist
 
     per = -(-n_total // world) if n_total else 0
-    pad = torch.zeros((per, RESULT_BYTES), dtype=torch.uint8, device=local.device)
-    pad[: local.shape[0]] = local
+    if local.shape[0] == per:
+        pad = local.contiguous()
+    else:
+        pad = torch.zeros((per, RESULT_BYTES), dtype=torch.uint8, device=local.device)
+        pad[: local.shape[0]] = local
+    if local.device.type == "cuda":
+        # one flat RCCL all-gather straight into the result (no list, no cat)
+        full = torch.empty((world * per, RESULT_BYTES), dtype=torch.uint8, device=local.device)
+        dist.all_gather_into_tensor(full, pad, group=group)
+        return full[:n_total]
     bufs = [torch.empty_like(pad) for _ in range(world)]
     dist.all_gather(bufs, pad, group=group)
-    full = torch.cat(bufs, dim=0)[:n_total]
-    return full
+    return torch.cat(bufs, dim=0)[:n_total]
 
 
 def unpack_results(full) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:

@@ -79,3 +79,36 @@ def test_verify_sharded_gloo(tmp_path, world, kats):
         np.testing.assert_array_equal(np.load(tmp_path / f"be{r}.npy"), want[1])
         np.testing.assert_array_equal(np.load(tmp_path / f"bl{r}.npy"), want[2])
     assert want[0][3] == 0x07 and (np.delete(want[0], 3) == 0x0F).all()
+
+
+def _nccl_worker(rank, world, port, out_dir):
+    import torch
+    import torch.distributed as dist
+
+    from ouroboros_network_amd.shard import all_gather_results, pack_results
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                      HSA_ENABLE_IPC_MODE_LEGACY="0")
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+    n = 1000
+    g = torch.Generator().manual_seed(3)
+    v = torch.randint(0, 16, (n,), generator=g, dtype=torch.uint8).to(dev)
+    be = torch.randint(0, 256, (n * 64,), generator=g, dtype=torch.uint8).to(dev)
+    bl = torch.randint(0, 256, (n * 64,), generator=g, dtype=torch.uint8).to(dev)
+    full = all_gather_results(pack_results(v, be, bl), n, world)
+    torch.cuda.synchronize()
+    ok = bool(torch.equal(full.cpu(), pack_results(v, be, bl).cpu()))
+    dist.destroy_process_group()
+    with open(os.path.join(out_dir, "ok"), "w") as f:
+        f.write("1" if ok else "0")
+
+
+@pytest.mark.gpu
+def test_result_gather_over_rccl(tmp_path):
+    """The device branch of all_gather_results (one flat RCCL all-gather into
+    the result tensor) on a one-rank nccl group: the only multi-rank
+    collective bench.py uses at N > 1, exercised on the one-GPU box."""
+    mp.spawn(_nccl_worker, args=(1, _free_port(), str(tmp_path)), nprocs=1, join=True)
+    assert (tmp_path / "ok").read_text() == "1"
