@@ -165,6 +165,21 @@ int ouro_tpraos_plan_run(ouro_tpraos_plan *plan, const ouro_tpraos_batch *b, uin
                          uint8_t *beta_eta, uint8_t *beta_leader);
 void ouro_tpraos_plan_destroy(ouro_tpraos_plan *plan);
 
+/* Asynchronous form of ouro_tpraos_plan_run for pipelined ChainSync windows
+ * (SURVEY.md §8(b) "Async": a client keeps up to 300 headers in flight,
+ * ouroboros-network/src/Ouroboros/Network/NodeToNode.hs:197-200, and
+ * validates each window as its headers arrive,
+ * ouroboros-consensus/src/Ouroboros/Consensus/MiniProtocol/ChainSync/Client.hs:792).
+ * submit copies the batch into the plan's pinned staging and launches its
+ * graph, returning at once (the caller's input buffers are free again on
+ * return); wait blocks until that batch's results are in the caller's buffers.
+ * One batch in flight per plan: a second submit before wait, or a wait with
+ * nothing submitted, returns OURO_EINVAL.  Several plans = several windows in
+ * flight, each on its own stream. */
+int ouro_tpraos_plan_submit(ouro_tpraos_plan *plan, const ouro_tpraos_batch *b);
+int ouro_tpraos_plan_wait(ouro_tpraos_plan *plan, uint8_t *verdict, uint8_t *beta_eta,
+                          uint8_t *beta_leader);
+
 /* ---------------------------------------------- leader threshold ----- */
 /* ledger-specs checkLeaderValue (shelley-spec-ledger BlockChain.hs), called by
  * meetsLeaderThreshold, ouroboros-consensus-shelley/src/Ouroboros/Consensus/

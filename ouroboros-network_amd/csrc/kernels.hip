@@ -1030,6 +1030,8 @@ struct ouro_tpraos_plan {
   int32_t *res = nullptr, *scratch = nullptr;
   size_t off[16] = {0};  // byte offsets of the 15 fields + n in the packed input block
   ouro_tpraos_batch dev_batch{};
+  size_t pending = 0;     // headers of the batch in flight (submit .. wait)
+  bool inflight = false;
 };
 
 namespace {
@@ -1040,6 +1042,7 @@ constexpr size_t kFieldBytes[15] = {32, 32, 80, 80, 32, 32, 32, 8, 8, 64, 4, 448
 
 void plan_free(ouro_tpraos_plan* p) {
   if (!p) return;
+  if (p->inflight && p->st) (void)hipStreamSynchronize(p->st);  // no DMA into freed staging
   if (p->exec) (void)hipGraphExecDestroy(p->exec);
   if (p->graph) (void)hipGraphDestroy(p->graph);
   if (p->h_in) (void)hipHostFree(p->h_in);
@@ -1126,12 +1129,16 @@ ouro_tpraos_plan* ouro_tpraos_plan_create(size_t max_headers, size_t max_body_by
   return p;
 }
 
-int ouro_tpraos_plan_run(ouro_tpraos_plan* p, const ouro_tpraos_batch* b, uint8_t* verdict,
-                         uint8_t* beta_eta, uint8_t* beta_leader) {
-  if (!p || !b || !verdict) return fail(OURO_EINVAL, "null argument");
+int ouro_tpraos_plan_submit(ouro_tpraos_plan* p, const ouro_tpraos_batch* b) {
+  if (!p || !b) return fail(OURO_EINVAL, "null argument");
+  if (p->inflight) return fail(OURO_EINVAL, "the plan already has a batch in flight");
   const size_t n = b->n;
-  if (n == 0) return OURO_OK;
   if (n > p->cap) return fail(OURO_EINVAL, "batch larger than the plan");
+  if (n == 0) {
+    p->pending = 0;
+    p->inflight = true;
+    return OURO_OK;
+  }
   const size_t span = span_of(n, b->body_off, b->body_len);
   if (span > p->body_cap) return fail(OURO_EINVAL, "body bytes exceed the plan");
   const void* src[15] = {b->issuer_vk, b->vrf_vk, b->eta_proof, b->leader_proof, b->eta_alpha,
@@ -1140,17 +1147,43 @@ int ouro_tpraos_plan_run(ouro_tpraos_plan* p, const ouro_tpraos_batch* b, uint8_
   for (int f = 0; f < 15; f++) {
     const size_t bytes = kFieldBytes[f] ? kFieldBytes[f] * n : span;
     if (bytes && !src[f]) return fail(OURO_EINVAL, "null field");
+  }
+  for (int f = 0; f < 15; f++) {
+    const size_t bytes = kFieldBytes[f] ? kFieldBytes[f] * n : span;
     if (bytes) memcpy(p->h_in + p->off[f], src[f], bytes);
   }
   const uint32_t n32 = (uint32_t)n;
   memcpy(p->h_in, &n32, sizeof n32);
   OURO_HIP(hipSetDevice(p->dev));
   OURO_HIP(hipGraphLaunch(p->exec, p->st));
+  p->pending = n;
+  p->inflight = true;
+  return OURO_OK;
+}
+
+int ouro_tpraos_plan_wait(ouro_tpraos_plan* p, uint8_t* verdict, uint8_t* beta_eta,
+                          uint8_t* beta_leader) {
+  if (!p) return fail(OURO_EINVAL, "null plan");
+  if (!p->inflight) return fail(OURO_EINVAL, "no batch in flight on this plan");
+  const size_t n = p->pending;
+  if (n && !verdict) return fail(OURO_EINVAL, "null verdict");
+  p->inflight = false;
+  if (n == 0) return OURO_OK;
+  OURO_HIP(hipSetDevice(p->dev));
   OURO_HIP(hipStreamSynchronize(p->st));
   memcpy(verdict, p->h_out, n);
   if (beta_eta) memcpy(beta_eta, p->h_out + align16(p->cap), 64 * n);
   if (beta_leader) memcpy(beta_leader, p->h_out + align16(p->cap) + 64 * p->cap, 64 * n);
   return OURO_OK;
+}
+
+int ouro_tpraos_plan_run(ouro_tpraos_plan* p, const ouro_tpraos_batch* b, uint8_t* verdict,
+                         uint8_t* beta_eta, uint8_t* beta_leader) {
+  if (!p || !b || !verdict) return fail(OURO_EINVAL, "null argument");
+  if (b->n == 0) return OURO_OK;
+  int rc = ouro_tpraos_plan_submit(p, b);
+  if (rc) return rc;
+  return ouro_tpraos_plan_wait(p, verdict, beta_eta, beta_leader);
 }
 
 void ouro_tpraos_plan_destroy(ouro_tpraos_plan* p) { plan_free(p); }

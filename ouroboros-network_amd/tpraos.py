@@ -150,6 +150,24 @@ class HeaderPlan:
         _native.check(rc, "ouro_tpraos_plan_run")
         return out
 
+    def submit(self, batch: HeaderBatch) -> None:
+        """Start a batch and return at once (ouro_tpraos_plan_submit); the
+        batch's arrays may be reused immediately."""
+        s = batch.c_struct()
+        _native.check(self._lib.ouro_tpraos_plan_submit(self._p, ctypes.byref(s)),
+                      "ouro_tpraos_plan_submit")
+        self._pending = len(batch)
+
+    def wait(self, out=None):
+        """Results of the submitted batch (ouro_tpraos_plan_wait)."""
+        n = getattr(self, "_pending", 0)
+        if out is None:
+            out = (np.zeros(n, np.uint8), np.zeros((n, 64), np.uint8), np.zeros((n, 64), np.uint8))
+        rc = self._lib.ouro_tpraos_plan_wait(self._p, ptr(out[0]), ptr(out[1]), ptr(out[2]))
+        _native.check(rc, "ouro_tpraos_plan_wait")
+        self._pending = 0
+        return out
+
     def close(self):
         if self._p:
             self._lib.ouro_tpraos_plan_destroy(self._p)

@@ -317,6 +317,44 @@ def test_header_plan_replays(gpu_lib, kats):
         plan.close()
 
 
+def test_plan_submit_wait_windows_in_flight(gpu_lib, kats):
+    """Asynchronous plans (ouro_tpraos_plan_submit / _wait): four 64-header
+    windows in flight on four plans at once, inputs overwritten right after
+    submit, results collected in reverse order -- each equals the oracle.
+    Misuse (second submit before wait, wait with nothing in flight) is an
+    error, never a stale or silent result."""
+    from ouroboros_network_amd.tpraos import HeaderPlan
+
+    batch = _golden_variants(kats)
+    n = len(batch)
+    wv, wbe, wbl = O.tpraos_verify_batch(batch)
+    plans = [HeaderPlan(max_headers=64, max_body_bytes=int(batch.body.size)) for _ in range(4)]
+    try:
+        for rnd in range(2):
+            lows = [(rnd * 256 + 64 * k) % (n - 64) for k in range(4)]
+            for plan, lo in zip(plans, lows):
+                w = batch.slice(lo, lo + 64)
+                w = type(w)(**{k: getattr(w, k).copy() for k in w.__dataclass_fields__})
+                plan.submit(w)
+                w.ocert_sigma[:] = 0  # the plan staged its own copy
+                w.body[:] = 0
+            for plan, lo in reversed(list(zip(plans, lows))):
+                v, be, bl = plan.wait()
+                np.testing.assert_array_equal(v, wv[lo:lo + 64])
+                np.testing.assert_array_equal(be, wbe[lo:lo + 64])
+                np.testing.assert_array_equal(bl, wbl[lo:lo + 64])
+        plans[0].submit(batch.slice(0, 3))
+        with pytest.raises(ValueError):
+            plans[0].submit(batch.slice(3, 6))
+        v, _, _ = plans[0].wait()
+        np.testing.assert_array_equal(v, wv[0:3])
+        with pytest.raises(ValueError):
+            plans[0].wait()
+    finally:
+        for plan in plans:
+            plan.close()
+
+
 # ---- ByronDSIGN (SURVEY.md §8(a) a11, App. B.5) ------------------------------
 
 def test_byron_golden_header(gpu_lib, kats):
