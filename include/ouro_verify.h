@@ -151,8 +151,8 @@ int ouro_tpraos_verify_batch(const ouro_tpraos_batch *b, uint8_t *verdict,
 
 /* Latency-oriented variant for small batches (ChainSync windows of up to 300
  * pipelined headers, ouroboros-network/src/Ouroboros/Network/NodeToNode.hs:197-200):
- * the six checks of a header run on six lanes concurrently, then one finish
- * pass.  Same verdicts and outputs as ouro_tpraos_verify_batch. */
+ * the checks of a header run on eight lanes concurrently (each VRF's
+ * V = [s]H - [c]Gamma split over two), then one finish pass.  Same verdicts and outputs as ouro_tpraos_verify_batch. */
 int ouro_tpraos_verify_batch_lowlat(const ouro_tpraos_batch *b, uint8_t *verdict,
                                     uint8_t *beta_eta, uint8_t *beta_leader);
 

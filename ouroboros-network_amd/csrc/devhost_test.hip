@@ -206,13 +206,15 @@ int dh_sum6kes_verify(const uint8_t* vk, uint32_t t, const uint8_t* m, uint32_t 
 // per core, no sharing).  Pointers must be 16-B aligned like device buffers.
 int dh_tpraos_verify(const ouro_tpraos_batch* b, int mode, uint8_t* verdict, uint8_t* beta_eta,
                      uint8_t* beta_leader) {
-  std::vector<Lane> lanes(kHdrCores);
-  std::vector<int32_t> res(kResWords + 4);
+  std::vector<Lane> lanes(kLatCores);
+  std::vector<int32_t> res(kLatResWords + 4);
   int32_t* r = reinterpret_cast<int32_t*>((reinterpret_cast<uintptr_t>(res.data()) + 15) & ~uintptr_t(15));
   for (size_t i = 0; i < b->n; i++) {
-    memset(r, 0, kResWords * sizeof(int32_t));
-    for (int core = 0; core < kHdrCores; core++)
-      hdr_core(*b, i, core, lanes[mode ? core : 0].w, r, host_btab(), mode == 0);
+    memset(r, 0, kLatResWords * sizeof(int32_t));
+    const int cores = mode ? kLatCores : kHdrCores;
+    for (int core = 0; core < cores; core++)
+      hdr_core(*b, i, core, lanes[mode ? core : 0].w, r, host_btab(), mode == 0, mode != 0);
+    if (mode) hdr_combine_split(r);
     hdr_finish_item(*b, i, r, lanes[0].w, verdict, beta_eta, beta_leader);
   }
   return 0;

@@ -87,6 +87,25 @@ OURO_FI ge_p3 ge_p3_add(const ge_p3& p, const ge_p3& q) {
   return ge_p1p1_to_p3(ge_add_cached(p, ge_p3_to_cached(q), false));
 }
 
+// P + Q in projective (X:Y:Z) coordinates, complete for a = -1 and non-square
+// d (Bernstein-Birkner-Joye-Lange-Peters 2008, "add-2008-bbjlp"):
+//   A = Z1 Z2, B = A^2, C = X1 X2, D = Y1 Y2, E = d C D, F = B - E, G = B + E,
+//   X3 = A F ((X1 + Y1)(X2 + Y2) - C - D), Y3 = A G (D + C), Z3 = F G.
+OURO_FI ge_p2 ge_p2_add(const ge_p2& p, const ge_p2& q) {
+  fe A = fe_mul(p.Z, q.Z);
+  fe B = fe_sq(A);
+  fe C = fe_mul(p.X, q.X);
+  fe D = fe_mul(p.Y, q.Y);
+  fe E = fe_mul(fe_mul(C, D), fe_d());
+  fe F = fe_carry(fe_sub(B, E));
+  fe G = fe_carry(fe_add(B, E));
+  fe S = fe_mul(fe_carry(fe_add(p.X, p.Y)), fe_carry(fe_add(q.X, q.Y)));
+  fe CD = fe_carry(fe_add(C, D));
+  fe X3 = fe_mul(fe_mul(A, F), fe_carry(fe_sub(S, CD)));
+  fe Y3 = fe_mul(fe_mul(A, G), CD);
+  return ge_p2{X3, Y3, fe_mul(F, G)};
+}
+
 OURO_FI ge_p3 ge_p3_neg(const ge_p3& p) { return ge_p3{fe_neg(p.X), p.Y, p.Z, fe_neg(p.T)}; }
 
 // [8]P

@@ -149,17 +149,18 @@ __global__ void __launch_bounds__(kBlock, OURO_WAVES) k_tpraos_cores(ouro_tpraos
   const size_t tid = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   const size_t nth = (size_t)gridDim.x * blockDim.x;
   int32_t* lane = scratch + tid * kLaneWords;
-  for (size_t w = tid; w < (size_t)kHdrCores * n; w += nth) {
+  for (size_t w = tid; w < (size_t)kLatCores * n; w += nth) {
     const int core = (int)(w / n);
     const size_t i = w - (size_t)core * n;
-    hdr_core(b, i, core, lane, res_buf + i * kResWords, btab, /*share_key=*/false);
+    hdr_core(b, i, core, lane, res_buf + i * kLatResWords, btab, /*share_key=*/false,
+             /*split=*/true);
   }
 }
 
 // Latency mode, launch 2: the shared-inversion finish, one lane per header.
 __global__ void __launch_bounds__(kBlock, OURO_WAVES) k_tpraos_finish(ouro_tpraos_batch b,
                                                              const uint32_t* __restrict__ d_n,
-                                                             const int32_t* res_buf,
+                                                             int32_t* res_buf,
                                                              uint8_t* __restrict__ verdict,
                                                              uint8_t* __restrict__ beta_eta,
                                                              uint8_t* __restrict__ beta_leader,
@@ -168,8 +169,11 @@ __global__ void __launch_bounds__(kBlock, OURO_WAVES) k_tpraos_finish(ouro_tprao
   const size_t tid = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   const size_t nth = (size_t)gridDim.x * blockDim.x;
   int32_t* lane = scratch + tid * kLaneWords;
-  for (size_t i = tid; i < n; i += nth)
-    hdr_finish_item(b, i, res_buf + i * kResWords, lane, verdict, beta_eta, beta_leader);
+  for (size_t i = tid; i < n; i += nth) {
+    int32_t* res = res_buf + i * kLatResWords;
+    hdr_combine_split(res);
+    hdr_finish_item(b, i, res, lane, verdict, beta_eta, beta_leader);
+  }
 }
 
 // leader threshold (leader.h), one item per lane; verdict 1 / 0 / 0xff
@@ -441,7 +445,7 @@ int launch_lowlat(hipStream_t st, const ouro_tpraos_batch& b, const uint32_t* d_
   int rc = device_state(&ds);
   if (rc) return rc;
   int g1, g2;
-  if ((rc = plan(ds, kCores, (size_t)kHdrCores * n_cap, st, &g1, nullptr))) return rc;
+  if ((rc = plan(ds, kCores, (size_t)kLatCores * n_cap, st, &g1, nullptr))) return rc;
   if ((rc = plan(ds, kFinish, n_cap, st, &g2, nullptr))) return rc;
   hipLaunchKernelGGL(k_tpraos_cores, dim3(g1), dim3(kBlock), 0, st, b, d_n, res_buf, scratch,
                      ds->btab);
@@ -452,7 +456,7 @@ int launch_lowlat(hipStream_t st, const ouro_tpraos_batch& b, const uint32_t* d_
 }
 
 size_t lowlat_scratch_words(DeviceState* ds, size_t n_cap) {
-  size_t b1 = std::min<size_t>(((size_t)kHdrCores * n_cap + kBlock - 1) / kBlock,
+  size_t b1 = std::min<size_t>(((size_t)kLatCores * n_cap + kBlock - 1) / kBlock,
                                (size_t)ds->max_blocks[kCores]);
   size_t b2 = std::min<size_t>((n_cap + kBlock - 1) / kBlock, (size_t)ds->max_blocks[kFinish]);
   return std::max<size_t>(1, std::max(b1, b2)) * kBlock * kLaneWords;
@@ -998,7 +1002,7 @@ int ouro_tpraos_verify_batch_lowlat(const ouro_tpraos_batch* b, uint8_t* verdict
   d.body_len = sg.up(b->body_len, n);
   const uint32_t n32 = (uint32_t)n;
   const uint32_t* d_n = sg.up(&n32, 1);
-  int32_t* res = sg.out<int32_t>(n * kResWords);
+  int32_t* res = sg.out<int32_t>(n * kLatResWords);
   int32_t* scr = sg.out<int32_t>(lowlat_scratch_words(ds, n));
   uint8_t* dver = sg.out<uint8_t>(n);
   uint8_t* dbe = sg.out<uint8_t>(64 * n);
@@ -1072,7 +1076,7 @@ int plan_build(ouro_tpraos_plan* p) {
   OURO_HIP(hipHostMalloc(&p->h_out, p->out_bytes, hipHostMallocDefault));
   OURO_HIP(hipMalloc(&p->d_in, p->in_bytes));
   OURO_HIP(hipMalloc(&p->d_out, p->out_bytes));
-  OURO_HIP(hipMalloc(&p->res, sizeof(int32_t) * kResWords * p->cap));
+  OURO_HIP(hipMalloc(&p->res, sizeof(int32_t) * kLatResWords * p->cap));
   OURO_HIP(hipMalloc(&p->scratch, sizeof(int32_t) * lowlat_scratch_words(ds, p->cap)));
   memset(p->h_in, 0, p->in_bytes);
   uint8_t* d = p->d_in;

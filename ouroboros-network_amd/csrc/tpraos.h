@@ -12,8 +12,10 @@
 // then does every encoding, comparison and hash.  The cores are independent, so the same code runs
 //   * throughput mode: one lane runs all six cores of a header, the VRF key is
 //     decoded once and its [1..8](-Y) table serves both U computations;
-//   * latency mode (64-header ChainSync windows): six lanes per header run the
-//     cores concurrently, a second launch finishes.
+//   * latency mode (64-header ChainSync windows): eight lanes per header run
+//     the cores concurrently -- each V split into [s]H and -[c]Gamma halves so
+//     the longest lane is one 252-bit chain -- and a second launch adds the
+//     halves (hdr_combine_split) and finishes.
 // Verdicts and outputs are identical in both modes (tests pin both against
 // the oracle).
 #pragma once
@@ -27,16 +29,27 @@ enum HdrPoint { kPtHe = 0, kPtUe, kPtVe, kPtG8e, kPtHl, kPtUl, kPtVl, kPtG8l, kH
 constexpr int kPtWords = 36;                          // X, Y, Z at a 12-word stride
 constexpr int kResFlags = kHdrPoints * kPtWords;      // 6 flag words, one per core
 constexpr int kResWords = kResFlags + 8;              // 296 words (16-B multiple)
-enum HdrCore { kCoreOcert = 0, kCoreKes, kCoreUe, kCoreUl, kCoreVe, kCoreVl, kHdrCores };
+// latency mode: the record plus the two -[c]Gamma partial points
+constexpr int kLatPart = kResWords;
+constexpr int kLatResWords = kResWords + 2 * kPtWords;  // 368 words (16-B multiple)
+enum HdrCore { kCoreOcert = 0, kCoreKes, kCoreUe, kCoreUl, kCoreVe, kCoreVl, kHdrCores,
+               // latency mode splits each V = [s]H - [c]Gamma over two lanes: the V
+               // cores do [s]H (252-bit chain), these do -[c]Gamma (128-bit chain)
+               kCoreGe = kHdrCores, kCoreGl, kLatCores };
 // flag bits
 constexpr int32_t kFlagOk = 1;        // the core's acceptance checks passed
 constexpr int32_t kFlagGammaX0 = 2;   // Gamma decoded with x = 0 (re-encodes with sign 0)
 
-OURO_FI void st_point(int32_t* res, int which, const fe& X, const fe& Y, const fe& Z) {
-  int32_t* p = res + which * kPtWords;
+OURO_FI void st_point_at(int32_t* p, const fe& X, const fe& Y, const fe& Z) {
   st_fe(p, X);
   st_fe(p + 12, Y);
   st_fe(p + 24, Z);
+}
+OURO_FI void st_point(int32_t* res, int which, const fe& X, const fe& Y, const fe& Z) {
+  st_point_at(res + which * kPtWords, X, Y, Z);
+}
+OURO_FI ge_p2 ld_point_at(const int32_t* p) {
+  return ge_p2{ld_fe(p), ld_fe(p + 12), ld_fe(p + 24)};
 }
 OURO_FI void st_point_from_dsm(int32_t* res, int which, const int32_t* lane) {
   const ge_p2 r = dsm_result(lane);
@@ -97,11 +110,15 @@ OURO_HD inline bool vrf_u_core(const uint32_t pk[8], const uint32_t pi[20], bool
 }
 
 // Gamma checks, H = hash_to_curve(Y, alpha), V = [s]H - [c]Gamma, [8]Gamma.
-// Writes H, V, [8]Gamma into res; returns the flag word.
+// Writes H, V, [8]Gamma into res; returns the flag word.  part = 0: all of it
+// (throughput mode); part = 1: H and [s]H only, written as V; part = 2: the
+// Gamma checks, [8]Gamma and -[c]Gamma, written to `partial` (latency mode:
+// the two halves run on two lanes and hdr_combine_split adds them).
 template <class Tail>
 OURO_HD inline int32_t vrf_v_core(const uint32_t pk[8], const uint32_t pi[20], const Tail& alpha,
                                   uint32_t alen, int32_t* lane, const int32_t* btab,
-                                  int32_t* res, int ptH, int ptV, int ptG8) {
+                                  int32_t* res, int ptH, int ptV, int ptG8, int part = 0,
+                                  int32_t* partial = nullptr) {
   uint32_t G[8], c[8], s_raw[8], s[8];
 #pragma unroll
   for (int i = 0; i < 8; i++) {
@@ -109,31 +126,48 @@ OURO_HD inline int32_t vrf_v_core(const uint32_t pk[8], const uint32_t pi[20], c
     s_raw[i] = pi[12 + i];
     c[i] = i < 4 ? pi[8 + i] : 0u;
   }
-  ge_p3 Gamma;
-  bool ok = ge_is_canonical(G);
-  ok = ge_decode(&Gamma, G, false) && ok;
-  sc_reduce256(s, s_raw);
-  uint32_t pre[9];
-  pre[0] = 0x04u | (0x01u << 8) | (pk[0] << 16);
-#pragma unroll
-  for (int i = 1; i < 8; i++) pre[i] = (pk[i - 1] >> 16) | (pk[i] << 16);
-  pre[8] = pk[7] >> 16;
-  uint64_t Hs[8];
-  sha512_prefixed<34>(Hs, pre, alpha, alen);
-  uint32_t rw[16];
-  sha512_digest_words(rw, Hs);
-  rw[7] &= 0x7fffffffu;
-  ge_p3 Hp = elligator2_h(rw);
-  st_point(res, ptH, Hp.X, Hp.Y, Hp.Z);
-  build_table(lane + kSlotTab1, Hp);
-  build_table(lane + kSlotTab2, ge_p3_neg(Gamma));
-  st_words8(lane + kSlotA1, s);
-  st_words8(lane + kSlotA2, c);
   uint64_t* carr = reinterpret_cast<uint64_t*>(lane + kSlotCarry);
-  carr[0] = sc_recode_carries<4, 64>(s);
-  carr[1] = sc_recode_carries<4, 33>(c);
-  dsm(lane, btab, dsm_cfg(64, 33, false, 0, 1));
-  st_point_from_dsm(res, ptV, lane);
+  ge_p3 Gamma;
+  bool ok = true;
+  if (part != 1) {
+    ok = ge_is_canonical(G);
+    ok = ge_decode(&Gamma, G, false) && ok;
+  }
+  if (part == 2) {
+    build_table(lane + kSlotTab1, ge_p3_neg(Gamma));
+    st_words8(lane + kSlotA1, c);
+    carr[0] = sc_recode_carries<4, 33>(c);
+    dsm(lane, btab, dsm_cfg(33, 0, false, 0, 1));
+    const ge_p2 r = dsm_result(lane);
+    st_point_at(partial, r.X, r.Y, r.Z);
+  } else {
+    sc_reduce256(s, s_raw);
+    uint32_t pre[9];
+    pre[0] = 0x04u | (0x01u << 8) | (pk[0] << 16);
+#pragma unroll
+    for (int i = 1; i < 8; i++) pre[i] = (pk[i - 1] >> 16) | (pk[i] << 16);
+    pre[8] = pk[7] >> 16;
+    uint64_t Hs[8];
+    sha512_prefixed<34>(Hs, pre, alpha, alen);
+    uint32_t rw[16];
+    sha512_digest_words(rw, Hs);
+    rw[7] &= 0x7fffffffu;
+    ge_p3 Hp = elligator2_h(rw);
+    st_point(res, ptH, Hp.X, Hp.Y, Hp.Z);
+    build_table(lane + kSlotTab1, Hp);
+    st_words8(lane + kSlotA1, s);
+    carr[0] = sc_recode_carries<4, 64>(s);
+    if (part == 0) {
+      build_table(lane + kSlotTab2, ge_p3_neg(Gamma));
+      st_words8(lane + kSlotA2, c);
+      carr[1] = sc_recode_carries<4, 33>(c);
+      dsm(lane, btab, dsm_cfg(64, 33, false, 0, 1));
+    } else {
+      dsm(lane, btab, dsm_cfg(64, 0, false, 0, 1));
+    }
+    st_point_from_dsm(res, ptV, lane);
+    if (part == 1) return kFlagOk;
+  }
   ge_p3 G8 = ge_mul8(Gamma);
   st_point(res, ptG8, G8.X, G8.Y, G8.Z);
   return (ok ? kFlagOk : 0) | (fe_iszero(Gamma.X) ? kFlagGammaX0 : 0);
@@ -173,6 +207,22 @@ OURO_HD inline bool vrf_finish(uint32_t beta[16], const uint32_t Henc[8], const 
   sha512_prefixed<34>(Hb, bp, ShaNoTail{}, 0);
   sha512_digest_words(beta, Hb);
   return ceq;
+}
+
+// Latency mode: V = [s]H + (-[c]Gamma) from the two half cores, and the V
+// flag word from both (acceptance of both halves; Gamma's x = 0 bit from the
+// Gamma half).  Complete projective addition, so no case is special.
+OURO_HD inline void hdr_combine_split(int32_t* res) {
+#pragma unroll 1
+  for (int which = 0; which < 2; which++) {
+    const int ptV = which ? kPtVl : kPtVe;
+    const ge_p2 V = ge_p2_add(ld_point_at(res + ptV * kPtWords),
+                              ld_point_at(res + kLatPart + which * kPtWords));
+    st_point(res, ptV, V.X, V.Y, V.Z);
+    int32_t* fv = res + kResFlags + (which ? kCoreVl : kCoreVe);
+    const int32_t fg = res[kResFlags + (which ? kCoreGl : kCoreGe)];
+    *fv = (*fv & fg & kFlagOk) | (fg & kFlagGammaX0);
+  }
 }
 
 // One inversion for all eight Z; tmp = 8 x 12 scratch words.  Then every
@@ -246,7 +296,7 @@ OURO_FI void st_words(uint8_t* p, const uint32_t* w, int n16) {
 // built by the eta U core (table slot 2) for the leader U core.
 OURO_HD inline void hdr_core(const ouro_tpraos_batch& b, size_t i, int core,
                                          int32_t* lane, int32_t* res, const int32_t* btab,
-                                         bool share_key = true) {
+                                         bool share_key = true, bool split = false) {
   int32_t flag = 0;
   switch (core) {
     case kCoreOcert: {
@@ -279,15 +329,17 @@ OURO_HD inline void hdr_core(const ouro_tpraos_batch& b, size_t i, int core,
       st_point_from_dsm(res, leader ? kPtUl : kPtUe, lane);
       break;
     }
-    default: {  // kCoreVe / kCoreVl
-      const bool leader = core == kCoreVl;
+    default: {  // kCoreVe / kCoreVl, and in latency mode kCoreGe / kCoreGl
+      const bool gamma = core == kCoreGe || core == kCoreGl;
+      const bool leader = core == kCoreVl || core == kCoreGl;
       uint32_t p[8], pi[20];
       ld_words(p, b.vrf_vk + 32 * i, 2);
       ld_words(pi, (leader ? b.leader_proof : b.eta_proof) + 80 * i, 5);
       const uint8_t* a = (leader ? b.leader_alpha : b.eta_alpha) + 32 * i;
       flag = vrf_v_core(p, pi, ShaGlobalTail{a}, 32, lane, btab, res,
                         leader ? kPtHl : kPtHe, leader ? kPtVl : kPtVe,
-                        leader ? kPtG8l : kPtG8e);
+                        leader ? kPtG8l : kPtG8e, gamma ? 2 : (split ? 1 : 0),
+                        res + kLatPart + (leader ? kPtWords : 0));
       break;
     }
   }

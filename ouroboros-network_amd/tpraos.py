@@ -115,7 +115,7 @@ def verify_headers(batch: HeaderBatch) -> Tuple[np.ndarray, np.ndarray, np.ndarr
 
 
 def verify_headers_lowlat(batch: HeaderBatch) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
-    """Same results as verify_headers; six lanes per header (small batches)."""
+    """Same results as verify_headers; eight lanes per header (small batches)."""
     n = len(batch)
     verdict = np.zeros(n, dtype=np.uint8)
     be = np.zeros((n, 64), dtype=np.uint8)
