@@ -28,6 +28,7 @@ constexpr int kBlock = 256;
 #endif
 // throughput header kernel: scratch slot + the per-header result record
 constexpr int kHdrLaneWords = kLaneWords + kResWords;
+constexpr int kLatBlock = 64;  // default latency-mode workgroup (lat_block(); A/B: tools/ab_latency.py)
 
 // message bytes held in registers (the 48-byte OCertSignable); a select chain
 // keeps a dynamic byte index out of scratch
@@ -437,20 +438,37 @@ int launch_leader(hipStream_t st, size_t n, const uint8_t* beta, const uint64_t*
   return launch_check();
 }
 
-// latency mode: six lanes per header, then the finish; n read from d_n
+// Workgroup size of the latency-mode launches (OURO_LAT_BLOCK = 64/128/256).
+// A small window fills only a few waves; one-wave workgroups spread them over
+// as many CUs (own L1, TA and instruction fetch per wave) instead of packing
+// four onto each CU.
+int lat_block() {
+  if (const char* e = getenv("OURO_LAT_BLOCK")) {
+    const int v = atoi(e);
+    if (v == 64 || v == 128 || v == 256) return v;
+  }
+  return kLatBlock;
+}
+
+// latency mode: eight lanes per header, then the finish; n read from d_n.
+// Lanes used <= the kBlock-rounded count lowlat_scratch_words provides for.
 int launch_lowlat(hipStream_t st, const ouro_tpraos_batch& b, const uint32_t* d_n, size_t n_cap,
                   int32_t* res_buf, int32_t* scratch, uint8_t* verdict, uint8_t* be,
                   uint8_t* bl) {
   DeviceState* ds;
   int rc = device_state(&ds);
   if (rc) return rc;
-  int g1, g2;
-  if ((rc = plan(ds, kCores, (size_t)kLatCores * n_cap, st, &g1, nullptr))) return rc;
-  if ((rc = plan(ds, kFinish, n_cap, st, &g2, nullptr))) return rc;
-  hipLaunchKernelGGL(k_tpraos_cores, dim3(g1), dim3(kBlock), 0, st, b, d_n, res_buf, scratch,
+  const int blk = lat_block();
+  const size_t per = kBlock / blk;
+  auto grid = [&](size_t items, int id) {
+    size_t g = (items + blk - 1) / blk;
+    return (int)std::max<size_t>(1, std::min<size_t>(g, (size_t)ds->max_blocks[id] * per));
+  };
+  const int g1 = grid((size_t)kLatCores * n_cap, kCores), g2 = grid(n_cap, kFinish);
+  hipLaunchKernelGGL(k_tpraos_cores, dim3(g1), dim3(blk), 0, st, b, d_n, res_buf, scratch,
                      ds->btab);
   if ((rc = launch_check())) return rc;
-  hipLaunchKernelGGL(k_tpraos_finish, dim3(g2), dim3(kBlock), 0, st, b, d_n, res_buf, verdict, be,
+  hipLaunchKernelGGL(k_tpraos_finish, dim3(g2), dim3(blk), 0, st, b, d_n, res_buf, verdict, be,
                      bl, scratch);
   return launch_check();
 }
