@@ -156,6 +156,19 @@ int ouro_tpraos_verify_batch(const ouro_tpraos_batch *b, uint8_t *verdict,
 int ouro_tpraos_verify_batch_lowlat(const ouro_tpraos_batch *b, uint8_t *verdict,
                                     uint8_t *beta_eta, uint8_t *beta_leader);
 
+/* One process, several GPUs: the batch is cut into
+ * contiguous shards, shard k verified on devices[k] (devices = NULL: every
+ * visible device) by a persistent per-shard worker thread with its own
+ * streams and pinned staging -- the pipelined path of ouro_tpraos_verify_batch
+ * -- writing straight into the caller's buffers (no collective is needed
+ * inside one process).  A device may be listed more than once (two pipelines
+ * on one GPU).  Calls are serialised process-wide; the first shard error is
+ * returned after every shard has finished.  Same results as
+ * ouro_tpraos_verify_batch. */
+int ouro_device_count(void);
+int ouro_tpraos_verify_batch_multi(const ouro_tpraos_batch *b, const int *devices, int ndev,
+                                   uint8_t *verdict, uint8_t *beta_eta, uint8_t *beta_leader);
+
 /* A captured plan for repeated fixed-capacity batches: pinned staging and one
  * hipGraph (H2D, the two latency-mode kernels, D2H) replayed per call.  A plan
  * is used by one thread at a time; any n <= max_headers per run. */

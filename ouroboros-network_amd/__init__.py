@@ -11,7 +11,7 @@ from ._native import DeviceError, NativeUnavailable
 from .byron import ByronDSIGN, parse_byron_header, verify_byron_headers
 from .dsign import Ed25519DSIGN
 from .kes import Sum6KES, kes_period
-from .tpraos import HeaderBatch, first_invalid, verify_headers
+from .tpraos import HeaderBatch, first_invalid, verify_headers, verify_headers_multi
 from .vrf import PraosVRF
 
 __all__ = [
@@ -27,6 +27,7 @@ __all__ = [
     "parse_byron_header",
     "verify_byron_headers",
     "verify_headers",
+    "verify_headers_multi",
 ]
 
 

@@ -89,6 +89,8 @@ SIGNATURES = {
     "ouro_tpraos_plan_create": (_P, [_SZ, _SZ]),
     "ouro_tpraos_plan_run": (_I, [_P, ctypes.POINTER(TPraosBatch), _P, _P, _P]),
     "ouro_tpraos_plan_destroy": (None, [_P]),
+    "ouro_device_count": (_I, []),
+    "ouro_tpraos_verify_batch_multi": (_I, [ctypes.POINTER(TPraosBatch), _P, _I, _P, _P, _P]),
     "ouro_tpraos_plan_submit": (_I, [_P, ctypes.POINTER(TPraosBatch)]),
     "ouro_tpraos_plan_wait": (_I, [_P, _P, _P, _P]),
     "ouro_leader_check_batch": (_I, [_SZ, _P, _P, _P, ctypes.c_int64, ctypes.c_uint64, _I, _P]),

@@ -6,11 +6,13 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <condition_variable>
 #include <cstdio>
 #include <cstring>
 #include <map>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/ouro_verify.h"
@@ -1209,5 +1211,129 @@ int ouro_tpraos_plan_run(ouro_tpraos_plan* p, const ouro_tpraos_batch* b, uint8_
 }
 
 void ouro_tpraos_plan_destroy(ouro_tpraos_plan* p) { plan_free(p); }
+
+}  // extern "C"
+
+// ---- one process, several GPUs ----------------------------
+// A persistent worker thread per shard slot: its thread-local streams, device
+// buffers and pinned staging (the pipelined host path) live as long as the
+// process, so repeated calls allocate nothing.  Each worker verifies one
+// contiguous shard straight into the caller's buffers; in one process no
+// collective is needed.
+namespace {
+struct Worker {
+  std::mutex mu;
+  std::condition_variable cv;
+  bool has_job = false, done = false;
+  int dev = 0, rc = OURO_OK;
+  std::string err;
+  ouro_tpraos_batch shard{};
+  uint8_t *verdict = nullptr, *be = nullptr, *bl = nullptr;
+
+  void loop() {
+    for (;;) {
+      std::unique_lock<std::mutex> lk(mu);
+      cv.wait(lk, [&] { return has_job; });
+      has_job = false;
+      lk.unlock();
+      int r = ouro_set_device(dev);
+      if (r == OURO_OK) r = ouro_tpraos_verify_batch(&shard, verdict, be, bl);
+      lk.lock();
+      rc = r;
+      err = r ? t_last_error : std::string();
+      done = true;
+      cv.notify_all();
+    }
+  }
+};
+
+std::mutex g_multi_mu;                 // one multi-device call at a time
+std::vector<Worker*> g_workers;        // never freed: threads outlive every call
+
+Worker* worker(size_t k) {
+  while (g_workers.size() <= k) {
+    Worker* w = new Worker;
+    std::thread([w] { w->loop(); }).detach();
+    g_workers.push_back(w);
+  }
+  return g_workers[k];
+}
+
+ouro_tpraos_batch shard_of(const ouro_tpraos_batch& b, size_t lo, size_t m) {
+  ouro_tpraos_batch s = b;  // body + absolute offsets shared
+  s.n = m;
+  s.issuer_vk = b.issuer_vk + 32 * lo;
+  s.vrf_vk = b.vrf_vk + 32 * lo;
+  s.eta_proof = b.eta_proof + 80 * lo;
+  s.leader_proof = b.leader_proof + 80 * lo;
+  s.eta_alpha = b.eta_alpha + 32 * lo;
+  s.leader_alpha = b.leader_alpha + 32 * lo;
+  s.hot_vk = b.hot_vk + 32 * lo;
+  s.ocert_counter = b.ocert_counter + lo;
+  s.ocert_kes_period = b.ocert_kes_period + lo;
+  s.ocert_sigma = b.ocert_sigma + 64 * lo;
+  s.kes_t = b.kes_t + lo;
+  s.kes_sig = b.kes_sig + 448 * lo;
+  s.body_off = b.body_off + lo;
+  s.body_len = b.body_len + lo;
+  return s;
+}
+}  // namespace
+
+extern "C" {
+
+int ouro_device_count(void) {
+  int count = 0;
+  if (hipGetDeviceCount(&count) != hipSuccess) return 0;
+  return count;
+}
+
+int ouro_tpraos_verify_batch_multi(const ouro_tpraos_batch* b, const int* devices, int ndev,
+                                   uint8_t* verdict, uint8_t* beta_eta, uint8_t* beta_leader) {
+  if (!b) return fail(OURO_EINVAL, "null batch");
+  if (b->n == 0) return OURO_OK;
+  if (!verdict) return fail(OURO_EINVAL, "null verdict");
+  std::vector<int> devs;
+  if (devices) {
+    if (ndev <= 0 || ndev > 64) return fail(OURO_EINVAL, "bad device count");
+    devs.assign(devices, devices + ndev);
+  } else {
+    const int count = ouro_device_count();
+    for (int d = 0; d < count; d++) devs.push_back(d);
+    if (devs.empty()) return fail(OURO_ENODEV, "no device");
+  }
+  const size_t g = std::min<size_t>(devs.size(), b->n);
+  const size_t per = (b->n + g - 1) / g;
+  std::lock_guard<std::mutex> guard(g_multi_mu);
+  std::vector<Worker*> used;
+  for (size_t k = 0; k < g; k++) {
+    const size_t lo = k * per;
+    if (lo >= b->n) break;
+    const size_t m = std::min(per, b->n - lo);
+    Worker* w = worker(k);
+    {
+      std::lock_guard<std::mutex> lk(w->mu);
+      w->dev = devs[k];
+      w->shard = shard_of(*b, lo, m);
+      w->verdict = verdict + lo;
+      w->be = beta_eta ? beta_eta + 64 * lo : nullptr;
+      w->bl = beta_leader ? beta_leader + 64 * lo : nullptr;
+      w->done = false;
+      w->has_job = true;
+    }
+    w->cv.notify_all();
+    used.push_back(w);
+  }
+  int rc = OURO_OK;
+  for (Worker* w : used) {  // wait for every shard, errors included
+    std::unique_lock<std::mutex> lk(w->mu);
+    w->cv.wait(lk, [&] { return w->done; });
+    if (w->rc && rc == OURO_OK) {
+      rc = w->rc;
+      t_last_error = "device " + std::to_string(w->dev) + ": " + w->err;
+    }
+  }
+  return rc;
+}
 
 }  // extern "C"

@@ -114,6 +114,27 @@ def verify_headers(batch: HeaderBatch) -> Tuple[np.ndarray, np.ndarray, np.ndarr
     return verdict, be, bl
 
 
+def verify_headers_multi(batch: HeaderBatch, devices=None) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
+    """verify_headers over several GPUs of this process (contiguous shards,
+    one worker thread per shard; devices=None: every visible device)."""
+    n = len(batch)
+    verdict = np.zeros(n, dtype=np.uint8)
+    be = np.zeros((n, 64), dtype=np.uint8)
+    bl = np.zeros((n, 64), dtype=np.uint8)
+    if n:
+        s = batch.c_struct()
+        if devices is None:
+            dv, nd = None, 0
+        else:
+            dv = np.ascontiguousarray(devices, dtype=np.int32)
+            nd = int(dv.size)
+        rc = _native.load().ouro_tpraos_verify_batch_multi(
+            ctypes.byref(s), ptr(dv) if dv is not None else None, nd, ptr(verdict), ptr(be),
+            ptr(bl))
+        _native.check(rc, "ouro_tpraos_verify_batch_multi")
+    return verdict, be, bl
+
+
 def verify_headers_lowlat(batch: HeaderBatch) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
     """Same results as verify_headers; eight lanes per header (small batches)."""
     n = len(batch)

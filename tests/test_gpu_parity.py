@@ -289,6 +289,33 @@ def test_pipelined_host_batches(gpu_lib, kats, monkeypatch):
         np.testing.assert_array_equal(bl, wbl)
 
 
+def test_multi_device_shards(gpu_lib, kats, monkeypatch):
+    """ouro_tpraos_verify_batch_multi: contiguous shards on persistent worker
+    threads (here several pipelines sharing the one GPU of the box, and every
+    visible device) give the single-call results and the oracle's, for
+    shard counts that do not divide the batch and with small pipeline chunks."""
+    from ouroboros_network_amd import _native
+    from ouroboros_network_amd.tpraos import verify_headers, verify_headers_multi
+
+    batch = _golden_variants(kats)
+    wv, wbe, wbl = O.tpraos_verify_batch(batch)
+    assert _native.load().ouro_device_count() >= 1
+    monkeypatch.setenv("OURO_HOST_CHUNK", "50")
+    for devices in ([0], [0, 0], [0, 0, 0], None, [0] * 7):
+        for _ in range(2):  # the workers persist between calls
+            v, be, bl = verify_headers_multi(batch, devices)
+            np.testing.assert_array_equal(v, wv)
+            np.testing.assert_array_equal(be, wbe)
+            np.testing.assert_array_equal(bl, wbl)
+    v, _, _ = verify_headers_multi(batch.slice(0, 2), [0, 0, 0])  # fewer headers than shards
+    np.testing.assert_array_equal(v, wv[:2])
+    with pytest.raises(ValueError):
+        verify_headers_multi(batch, [])
+    with pytest.raises(Exception):
+        verify_headers_multi(batch, [0, 99])  # no such device: an error, never a verdict
+    np.testing.assert_array_equal(verify_headers(batch)[0], wv)
+
+
 def test_header_plan_replays(gpu_lib, kats):
     """The captured-graph plan over 64-header windows (BASELINE configs[4]):
     every window and a ragged tail match the oracle; replays are independent
