@@ -203,7 +203,8 @@ int dh_sum6kes_verify(const uint8_t* vk, uint32_t t, const uint8_t* m, uint32_t 
 }
 // The header drivers of tpraos.h for every header of a host SoA batch.
 // mode 0 = throughput (one lane, key table shared), 1 = latency (a fresh lane
-// per core, no sharing).  Pointers must be 16-B aligned like device buffers.
+// per core, no sharing), 2 = latency on lane quads (the four products of each
+// group operation emulated in sequence, with the merged operand bounds).  Pointers must be 16-B aligned like device buffers.
 int dh_tpraos_verify(const ouro_tpraos_batch* b, int mode, uint8_t* verdict, uint8_t* beta_eta,
                      uint8_t* beta_leader) {
   std::vector<Lane> lanes(kLatCores);
@@ -213,7 +214,8 @@ int dh_tpraos_verify(const ouro_tpraos_batch* b, int mode, uint8_t* verdict, uin
     memset(r, 0, kLatResWords * sizeof(int32_t));
     const int cores = mode ? kLatCores : kHdrCores;
     for (int core = 0; core < cores; core++)
-      hdr_core(*b, i, core, lanes[mode ? core : 0].w, r, host_btab(), mode == 0, mode != 0);
+      hdr_core(*b, i, core, lanes[mode ? core : 0].w, r, host_btab(), mode == 0, mode != 0,
+               mode == 2);
     if (mode) hdr_combine_split(r);
     hdr_finish_item(*b, i, r, lanes[0].w, verdict, beta_eta, beta_leader);
   }

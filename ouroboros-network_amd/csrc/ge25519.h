@@ -83,6 +83,131 @@ OURO_FI ge_p1p1 ge_add_cached(const ge_p3& p, const ge_cached& q, bool neg,
   return r;
 }
 
+// ---- lane-quad group operations (latency mode) --------------------------------
+// Four consecutive lanes (one DPP quad) hold the same point and split the
+// independent field products of one group operation: lane q = threadIdx.x & 3
+// computes product q, then every lane reads all four through quad_perm
+// broadcasts.  A doubling or an addition then costs one product's time
+// instead of three or four on the critical lane of a small window.
+// Bounds: a lane's operand is one of four candidates, so the worst case of
+// each operand is the largest of its candidates' -- the host build (which
+// runs the four products in sequence) gives every emulated product exactly
+// those merged bounds, so test_zero_bound_violations covers these formulas.
+struct fe4 { fe v[4]; };
+
+#if defined(__HIP_DEVICE_COMPILE__)
+// per-limb v_cndmask with a constant lane mask (lanes in `mask` take b).  In
+// asm so LLVM cannot turn a select of four elements into a scratch array
+// indexed by the lane.
+constexpr uint64_t kQuadOdd = 0xaaaaaaaaaaaaaaaaull;   // quad position 1, 3
+constexpr uint64_t kQuadHigh = 0xccccccccccccccccull;  // quad position 2, 3
+OURO_FI fe fe_sel_lanes(const fe& a, const fe& b, uint64_t mask) {
+  fe h;
+#pragma unroll
+  for (int i = 0; i < 10; i++)
+    asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(h.v[i]) : "v"(a.v[i]), "v"(b.v[i]), "s"(mask));
+  return h;
+}
+OURO_FI fe fe_quad_pick(const fe& a0, const fe& a1, const fe& a2, const fe& a3) {
+  return fe_sel_lanes(fe_sel_lanes(a0, a1, kQuadOdd), fe_sel_lanes(a2, a3, kQuadOdd), kQuadHigh);
+}
+template <int J>
+OURO_FI fe fe_quad_bcast(const fe& f) {
+  fe h;
+#pragma unroll
+  for (int i = 0; i < 10; i++)
+    h.v[i] = (uint32_t)__builtin_amdgcn_mov_dpp((int)f.v[i], J * 0x55, 0xf, 0xf, true);
+  return h;
+}
+OURO_FI fe4 fe_quad_gather(const fe& m) {
+  return fe4{{fe_quad_bcast<0>(m), fe_quad_bcast<1>(m), fe_quad_bcast<2>(m), fe_quad_bcast<3>(m)}};
+}
+#else
+// candidate j with the bounds of the largest candidate (see above)
+OURO_FI fe fe_quad_merged(const fe4& a, int j) {
+  fe r = a.v[j];
+  OURO_TRK(for (int i = 0; i < 10; i++) for (int k = 0; k < 4; k++) if (a.v[k].b[i] > r.b[i])
+               r.b[i] = a.v[k].b[i];)
+  return r;
+}
+#endif
+
+// out.v[j] = a.v[j] * b.v[j]
+OURO_FI fe4 fe_mul_quad(const fe4& a, const fe4& b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return fe_quad_gather(fe_mul(fe_quad_pick(a.v[0], a.v[1], a.v[2], a.v[3]),
+                               fe_quad_pick(b.v[0], b.v[1], b.v[2], b.v[3])));
+#else
+  fe4 r;
+  for (int j = 0; j < 4; j++) r.v[j] = fe_mul(fe_quad_merged(a, j), fe_quad_merged(b, j));
+  return r;
+#endif
+}
+// out.v[j] = a.v[j]^2, except out.v[2] = 2 a.v[2]^2
+OURO_FI fe4 fe_sq_quad_dbl2(const fe4& a) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  uint64_t t[10];
+  fe_sq_cols(t, fe_quad_pick(a.v[0], a.v[1], a.v[2], a.v[3]));
+  const uint32_t sh = (threadIdx.x & 3u) == 2u ? 1u : 0u;
+#pragma unroll
+  for (int k = 0; k < 10; k++) t[k] <<= sh;
+  return fe_quad_gather(fe_carry64(t));
+#else
+  fe4 r;
+  for (int j = 0; j < 4; j++) {
+    const fe x = fe_quad_merged(a, j);
+    r.v[j] = j == 2 ? fe_sq2(x) : fe_sq(x);
+  }
+  return r;
+#endif
+}
+// the products of the p1p1 conversions: (T X, Z Y, T Z, X Y)
+OURO_FI fe4 ge_p1p1_products_quad(const ge_p1p1& p) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const fe a = fe_sel_lanes(p.T, fe_sel_lanes(p.Z, p.X, kQuadHigh), kQuadOdd);
+  const fe b = fe_sel_lanes(fe_sel_lanes(p.X, p.Z, kQuadHigh), p.Y, kQuadOdd);
+  return fe_quad_gather(fe_mul(a, b));
+#else
+  return fe_mul_quad(fe4{{p.T, p.Z, p.T, p.X}}, fe4{{p.X, p.Y, p.Z, p.Y}});
+#endif
+}
+
+OURO_FI ge_p2 ge_p1p1_to_p2_quad(const ge_p1p1& p) {
+  const fe4 m = ge_p1p1_products_quad(p);
+  return ge_p2{m.v[0], m.v[1], m.v[2]};
+}
+OURO_FI ge_p3 ge_p1p1_to_p3_quad(const ge_p1p1& p) {
+  const fe4 m = ge_p1p1_products_quad(p);
+  return ge_p3{m.v[0], m.v[1], m.v[2], m.v[3]};
+}
+// ge_p2_dbl with its four squarings on the four lanes
+OURO_FI ge_p1p1 ge_p2_dbl_quad(const ge_p2& p) {
+  const fe4 s = fe_sq_quad_dbl2(fe4{{p.X, p.Y, p.Z, fe_add(p.X, p.Y)}});
+  const fe &A = s.v[0], &B = s.v[1], &C = s.v[2], &S = s.v[3];
+  ge_p1p1 r;
+  r.Y = fe_carry(fe_add(B, A));
+  r.Z = fe_sub(B, A);
+  r.X = fe_sub(S, r.Y);
+  r.T = fe_sub(fe_add(C, A), B);
+  return r;
+}
+// ge_add_cached with its four products on the four lanes; an affine Q carries
+// Z2 = 2, so D = 2 Z_P either way
+OURO_FI ge_p1p1 ge_add_cached_quad(const ge_p3& p, const ge_cached& q, bool neg) {
+  const fe qa = fe_select(q.YminusX, q.YplusX, neg);
+  const fe qb = fe_select(q.YplusX, q.YminusX, neg);
+  const fe4 m = fe_mul_quad(fe4{{fe_add(p.Y, p.X), fe_sub(p.Y, p.X), p.T, p.Z}},
+                            fe4{{qa, qb, q.T2d, q.Z2}});
+  const fe &A = m.v[0], &B = m.v[1], &C = m.v[2], &D = m.v[3];
+  const fe Dp = fe_add(D, C), Dm = fe_sub(D, C);
+  ge_p1p1 r;
+  r.X = fe_sub(A, B);
+  r.Y = fe_add(A, B);
+  r.Z = fe_select(Dm, Dp, neg);
+  r.T = fe_select(Dp, Dm, neg);
+  return r;
+}
+
 OURO_FI ge_p3 ge_p3_add(const ge_p3& p, const ge_p3& q) {
   return ge_p1p1_to_p3(ge_add_cached(p, ge_p3_to_cached(q), false));
 }

@@ -141,22 +141,27 @@ __global__ void __launch_bounds__(kBlock, OURO_WAVES) k_tpraos_verify(ouro_tprao
   }
 }
 
-// Latency mode, launch 1: six lanes per header (work item w = core * n + i,
+// Latency mode, launch 1: eight cores per header (work item w = core * n + i,
 // so each wave runs one core type), results to a per-header record.
-// n is read from device memory so a captured graph serves any n <= capacity.
+// quad = 1: each work item runs on the four lanes of a DPP quad, which share
+// its scratch slot and split every group operation's products (ge25519.h);
+// quad = 0: one lane per item.  n is read from device memory so a captured
+// graph serves any n <= capacity.
 __global__ void __launch_bounds__(kBlock, OURO_WAVES) k_tpraos_cores(ouro_tpraos_batch b,
                                                             const uint32_t* __restrict__ d_n,
                                                             int32_t* res_buf, int32_t* scratch,
-                                                            const int32_t* __restrict__ btab) {
+                                                            const int32_t* __restrict__ btab,
+                                                            int quad) {
   const size_t n = *d_n;
-  const size_t tid = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const size_t nth = (size_t)gridDim.x * blockDim.x;
+  const int sh = quad ? 2 : 0;
+  const size_t tid = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) >> sh;
+  const size_t nth = ((size_t)gridDim.x * blockDim.x) >> sh;
   int32_t* lane = scratch + tid * kLaneWords;
   for (size_t w = tid; w < (size_t)kLatCores * n; w += nth) {
     const int core = (int)(w / n);
     const size_t i = w - (size_t)core * n;
     hdr_core(b, i, core, lane, res_buf + i * kLatResWords, btab, /*share_key=*/false,
-             /*split=*/true);
+             /*split=*/true, quad != 0);
   }
 }
 
@@ -452,7 +457,15 @@ int lat_block() {
   return kLatBlock;
 }
 
-// latency mode: eight lanes per header, then the finish; n read from d_n.
+// Latency-mode cores on lane quads (1, default) or one lane per core
+// (OURO_LAT_QUAD=0, for A/B).
+int lat_quad() {
+  if (const char* e = getenv("OURO_LAT_QUAD")) return atoi(e) != 0;
+  return 1;
+}
+
+// latency mode: eight cores per header (x4 lanes in quad mode), then the
+// finish; n read from d_n.
 // Lanes used <= the kBlock-rounded count lowlat_scratch_words provides for.
 int launch_lowlat(hipStream_t st, const ouro_tpraos_batch& b, const uint32_t* d_n, size_t n_cap,
                   int32_t* res_buf, int32_t* scratch, uint8_t* verdict, uint8_t* be,
@@ -466,9 +479,10 @@ int launch_lowlat(hipStream_t st, const ouro_tpraos_batch& b, const uint32_t* d_
     size_t g = (items + blk - 1) / blk;
     return (int)std::max<size_t>(1, std::min<size_t>(g, (size_t)ds->max_blocks[id] * per));
   };
-  const int g1 = grid((size_t)kLatCores * n_cap, kCores), g2 = grid(n_cap, kFinish);
+  const int quad = lat_quad();
+  const int g1 = grid((size_t)kLatCores * n_cap << (quad ? 2 : 0), kCores), g2 = grid(n_cap, kFinish);
   hipLaunchKernelGGL(k_tpraos_cores, dim3(g1), dim3(blk), 0, st, b, d_n, res_buf, scratch,
-                     ds->btab);
+                     ds->btab, quad);
   if ((rc = launch_check())) return rc;
   hipLaunchKernelGGL(k_tpraos_finish, dim3(g2), dim3(blk), 0, st, b, d_n, res_buf, verdict, be,
                      bl, scratch);

@@ -85,13 +85,14 @@ OURO_HD inline void ocert_msg(OcertMsg& m, const uint32_t hot_vk[8], uint64_t ct
 // table written to table slot `yslot`; otherwise a previous call's table is
 // reused (throughput mode: both VRFs of a header share the key).
 OURO_HD inline bool vrf_u_core(const uint32_t pk[8], const uint32_t pi[20], bool build_y,
-                               int yslot, int32_t* lane, const int32_t* btab) {
+                               int yslot, int32_t* lane, const int32_t* btab,
+                               bool quad = false) {
   bool ok = true;
   if (build_y) {
     ge_p3 Y;
     ok = !ge_has_small_order(pk) && ge_is_canonical(pk);
     ok = ge_decode(&Y, pk, false) && ok;
-    build_table(lane + yslot * kTabWords, ge_p3_neg(Y));
+    build_table(lane + yslot * kTabWords, ge_p3_neg(Y), quad);
   }
   uint32_t c[8], s_raw[8], s[8];
 #pragma unroll
@@ -105,7 +106,7 @@ OURO_HD inline bool vrf_u_core(const uint32_t pk[8], const uint32_t pi[20], bool
   uint64_t* carr = reinterpret_cast<uint64_t*>(lane + kSlotCarry);
   carr[0] = sc_recode_carries<4, 33>(c);
   carr[2] = sc_recode_b(s);
-  dsm(lane, btab, dsm_cfg(33, 0, true, yslot, 1));
+  dsm(lane, btab, dsm_cfg(33, 0, true, yslot, 1), quad);
   return ok;
 }
 
@@ -118,7 +119,7 @@ template <class Tail>
 OURO_HD inline int32_t vrf_v_core(const uint32_t pk[8], const uint32_t pi[20], const Tail& alpha,
                                   uint32_t alen, int32_t* lane, const int32_t* btab,
                                   int32_t* res, int ptH, int ptV, int ptG8, int part = 0,
-                                  int32_t* partial = nullptr) {
+                                  int32_t* partial = nullptr, bool quad = false) {
   uint32_t G[8], c[8], s_raw[8], s[8];
 #pragma unroll
   for (int i = 0; i < 8; i++) {
@@ -134,10 +135,10 @@ OURO_HD inline int32_t vrf_v_core(const uint32_t pk[8], const uint32_t pi[20], c
     ok = ge_decode(&Gamma, G, false) && ok;
   }
   if (part == 2) {
-    build_table(lane + kSlotTab1, ge_p3_neg(Gamma));
+    build_table(lane + kSlotTab1, ge_p3_neg(Gamma), quad);
     st_words8(lane + kSlotA1, c);
     carr[0] = sc_recode_carries<4, 33>(c);
-    dsm(lane, btab, dsm_cfg(33, 0, false, 0, 1));
+    dsm(lane, btab, dsm_cfg(33, 0, false, 0, 1), quad);
     const ge_p2 r = dsm_result(lane);
     st_point_at(partial, r.X, r.Y, r.Z);
   } else {
@@ -154,16 +155,16 @@ OURO_HD inline int32_t vrf_v_core(const uint32_t pk[8], const uint32_t pi[20], c
     rw[7] &= 0x7fffffffu;
     ge_p3 Hp = elligator2_h(rw);
     st_point(res, ptH, Hp.X, Hp.Y, Hp.Z);
-    build_table(lane + kSlotTab1, Hp);
+    build_table(lane + kSlotTab1, Hp, quad);
     st_words8(lane + kSlotA1, s);
     carr[0] = sc_recode_carries<4, 64>(s);
     if (part == 0) {
-      build_table(lane + kSlotTab2, ge_p3_neg(Gamma));
+      build_table(lane + kSlotTab2, ge_p3_neg(Gamma), quad);
       st_words8(lane + kSlotA2, c);
       carr[1] = sc_recode_carries<4, 33>(c);
-      dsm(lane, btab, dsm_cfg(64, 33, false, 0, 1));
+      dsm(lane, btab, dsm_cfg(64, 33, false, 0, 1), quad);
     } else {
-      dsm(lane, btab, dsm_cfg(64, 0, false, 0, 1));
+      dsm(lane, btab, dsm_cfg(64, 0, false, 0, 1), quad);
     }
     st_point_from_dsm(res, ptV, lane);
     if (part == 1) return kFlagOk;
@@ -296,7 +297,8 @@ OURO_FI void st_words(uint8_t* p, const uint32_t* w, int n16) {
 // built by the eta U core (table slot 2) for the leader U core.
 OURO_HD inline void hdr_core(const ouro_tpraos_batch& b, size_t i, int core,
                                          int32_t* lane, int32_t* res, const int32_t* btab,
-                                         bool share_key = true, bool split = false) {
+                                         bool share_key = true, bool split = false,
+                                         bool quad = false) {
   int32_t flag = 0;
   switch (core) {
     case kCoreOcert: {
@@ -306,7 +308,7 @@ OURO_HD inline void hdr_core(const ouro_tpraos_batch& b, size_t i, int core,
       ld_words(hv, b.hot_vk + 32 * i, 2);
       OcertMsg m;
       ocert_msg(m, hv, b.ocert_counter[i], b.ocert_kes_period[i]);
-      flag = ed25519_verify_lane(s, p, m, 48, lane, btab) ? kFlagOk : 0;
+      flag = ed25519_verify_lane(s, p, m, 48, lane, btab, false, quad) ? kFlagOk : 0;
       break;
     }
     case kCoreKes: {
@@ -314,7 +316,7 @@ OURO_HD inline void hdr_core(const ouro_tpraos_batch& b, size_t i, int core,
       ld_words(hv, b.hot_vk + 32 * i, 2);
       const uint32_t* sw = reinterpret_cast<const uint32_t*>(b.kes_sig + 448 * i);
       flag = sum6kes_verify_lane(hv, b.kes_t[i], sw, ShaGlobalTail{b.body + b.body_off[i]},
-                                 b.body_len[i], lane, btab) ? kFlagOk : 0;
+                                 b.body_len[i], lane, btab, quad) ? kFlagOk : 0;
       break;
     }
     case kCoreUe:
@@ -324,7 +326,7 @@ OURO_HD inline void hdr_core(const ouro_tpraos_batch& b, size_t i, int core,
       ld_words(p, b.vrf_vk + 32 * i, 2);
       ld_words(pi, (leader ? b.leader_proof : b.eta_proof) + 80 * i, 5);
       const bool build = !(share_key && leader);
-      const bool ok = vrf_u_core(p, pi, build, 2, lane, btab);
+      const bool ok = vrf_u_core(p, pi, build, 2, lane, btab, quad);
       flag = build ? (ok ? kFlagOk : 0) : (res[kResFlags + kCoreUe] & kFlagOk);
       st_point_from_dsm(res, leader ? kPtUl : kPtUe, lane);
       break;
@@ -339,7 +341,7 @@ OURO_HD inline void hdr_core(const ouro_tpraos_batch& b, size_t i, int core,
       flag = vrf_v_core(p, pi, ShaGlobalTail{a}, 32, lane, btab, res,
                         leader ? kPtHl : kPtHe, leader ? kPtVl : kPtVe,
                         leader ? kPtG8l : kPtG8e, gamma ? 2 : (split ? 1 : 0),
-                        res + kLatPart + (leader ? kPtWords : 0));
+                        res + kLatPart + (leader ? kPtWords : 0), quad);
       break;
     }
   }

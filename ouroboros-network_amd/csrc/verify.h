@@ -142,14 +142,17 @@ OURO_FI void ld_words8(uint32_t w[8], const int32_t* p) {
 }
 
 // [1..8]P in cached form into a per-lane table
-OURO_HD inline void build_table(int32_t* tab, const ge_p3& P) {
+// (quad: the lane-quad formulas of ge25519.h, latency mode)
+OURO_HD inline void build_table(int32_t* tab, const ge_p3& P, bool quad = false) {
   ge_cached c1 = ge_p3_to_cached(P);
   st_cached(tab, c1);
-  ge_p3 Pk = ge_p1p1_to_p3(ge_p3_dbl(P));
+  ge_p3 Pk = quad ? ge_p1p1_to_p3_quad(ge_p2_dbl_quad(ge_p3_to_p2(P)))
+                  : ge_p1p1_to_p3(ge_p3_dbl(P));
   st_cached(tab + kCachedWords, ge_p3_to_cached(Pk));
 #pragma unroll 1
   for (int k = 2; k < kTabEntries; k++) {
-    Pk = ge_p1p1_to_p3(ge_add_cached(Pk, c1, false));
+    Pk = quad ? ge_p1p1_to_p3_quad(ge_add_cached_quad(Pk, c1, false))
+              : ge_p1p1_to_p3(ge_add_cached(Pk, c1, false));
     st_cached(tab + k * kCachedWords, ge_p3_to_cached(Pk));
   }
 }
@@ -204,7 +207,8 @@ constexpr uint32_t dsm_cfg(int nw1, int nw2, bool useB, int tab1 = 0, int tab2 =
 #ifndef OURO_DSM_SKIP_ID
 #define OURO_DSM_SKIP_ID 1  // A/B switch: 0 = doublings/addition from the identity kept
 #endif
-OURO_NI void dsm(int32_t* lane, const int32_t* btab, uint32_t cfg) {
+template <bool kQuad>
+OURO_FI void dsm_body(int32_t* lane, const int32_t* btab, uint32_t cfg) {
   const int nw1 = (int)(cfg & 0x7f), nw2 = (int)((cfg >> 8) & 0x7f);
   const bool useB = (cfg >> 16) & 1;
   const int32_t* tab1 = lane + (int)((cfg >> 20) & 3) * kTabWords;
@@ -272,7 +276,8 @@ OURO_NI void dsm(int32_t* lane, const int32_t* btab, uint32_t cfg) {
     // (the top window starts from the identity: its doublings are skipped)
     if (!OURO_DSM_SKIP_ID || j != top - 1) {
 #pragma unroll 1
-      for (int k = 0; k < 4; k++) t = ge_p2_dbl(ge_p1p1_to_p2(t));
+      for (int k = 0; k < 4; k++)
+        t = kQuad ? ge_p2_dbl_quad(ge_p1p1_to_p2_quad(t)) : ge_p2_dbl(ge_p1p1_to_p2(t));
     }
     prefetch ^= pf1 ^ pf2 ^ pf3 ^ pf4 ^ pf5 ^ pf6;
     // up to four additions, each from a wave-uniform source
@@ -301,15 +306,30 @@ OURO_NI void dsm(int32_t* lane, const int32_t* btab, uint32_t cfg) {
         fresh = false;
         continue;
       }
-      t = ge_add_cached(ge_p1p1_to_p3(t), q, neg, src >= 2);
+      t = kQuad ? ge_add_cached_quad(ge_p1p1_to_p3_quad(t), q, neg)
+                : ge_add_cached(ge_p1p1_to_p3(t), q, neg, src >= 2);
     }
   }
-  ge_p2 r = ge_p1p1_to_p2(t);
+  ge_p2 r = kQuad ? ge_p1p1_to_p2_quad(t) : ge_p1p1_to_p2(t);
   st_fe(lane + kSlotOut, r.X);
   st_fe(lane + kSlotOut + 12, r.Y);
   st_fe(lane + kSlotOut + 24, r.Z);
   // keeps the prefetch loads alive; limbs are < 2^27, so this never stores
   if (prefetch == 0xffffffffu) lane[kSlotOut + 35] = (int32_t)prefetch;
+}
+OURO_NI void dsm_lane(int32_t* lane, const int32_t* btab, uint32_t cfg) {
+  dsm_body<false>(lane, btab, cfg);
+}
+// latency mode: the four lanes of a quad run one chain (same inputs, same
+// slot), splitting each group operation's products
+OURO_NI void dsm_quad(int32_t* lane, const int32_t* btab, uint32_t cfg) {
+  dsm_body<true>(lane, btab, cfg);
+}
+OURO_FI void dsm(int32_t* lane, const int32_t* btab, uint32_t cfg, bool quad = false) {
+  if (quad)
+    dsm_quad(lane, btab, cfg);
+  else
+    dsm_lane(lane, btab, cfg);
 }
 
 OURO_FI ge_p2 dsm_result(const int32_t* lane) {
@@ -345,7 +365,8 @@ OURO_FI int wave_max_small(int x) {
 template <class Tail>
 OURO_HD inline bool ed25519_verify_lane(const uint32_t sig[16], const uint32_t pk[8],
                                         const Tail& msg, uint32_t mlen, int32_t* lane,
-                                        const int32_t* btab, bool byron = false) {
+                                        const int32_t* btab, bool byron = false,
+                                        bool quad = false) {
   uint32_t R[8], S[8];
 #pragma unroll
   for (int i = 0; i < 8; i++) {
@@ -396,8 +417,8 @@ OURO_HD inline bool ed25519_verify_lane(const uint32_t sig[16], const uint32_t p
   }
   sc_reduce512(b, prod);
   // [|c0|](+-A) + [c1](-R) + [b]B, one ~130-bit doubling chain
-  build_table(lane + kSlotTab1, hs.c0_neg ? ge_p3_neg(negA) : negA);
-  build_table(lane + kSlotTab2, negR);
+  build_table(lane + kSlotTab1, hs.c0_neg ? ge_p3_neg(negA) : negA, quad);
+  build_table(lane + kSlotTab2, negR, quad);
   st_words8(lane + kSlotA1, hs.c0);
   st_words8(lane + kSlotA2, hs.c1);
   st_words8(lane + kSlotB, b);
@@ -408,7 +429,7 @@ OURO_HD inline bool ed25519_verify_lane(const uint32_t sig[16], const uint32_t p
   // windows so that every scalar is < 2^(4 nw - 1) (top carry zero), <= 64
   int nw = wave_max_small((hs.bits + 4) >> 2);
   nw = nw < 1 ? 1 : (nw > 64 ? 64 : nw);
-  dsm(lane, btab, dsm_cfg(nw, nw, true, 0, 1));
+  dsm(lane, btab, dsm_cfg(nw, nw, true, 0, 1), quad);
   const ge_p2 Q = dsm_result(lane);
   const bool ident = fe_iszero(Q.X) && fe_iszero(fe_sub(Q.Y, Q.Z));
   return ok && ident;
@@ -616,7 +637,7 @@ OURO_HD inline bool vrf03_verify_lane(uint32_t beta[16], const uint32_t pk[8],
 template <class Tail>
 OURO_HD inline bool sum6kes_verify_lane(const uint32_t vk[8], uint32_t t, const uint32_t* sigw,
                                         const Tail& msg, uint32_t mlen, int32_t* lane,
-                                        const int32_t* btab) {
+                                        const int32_t* btab, bool quad = false) {
   uint32_t cur[8];
 #pragma unroll
   for (int i = 0; i < 8; i++) cur[i] = vk[i];
@@ -647,7 +668,7 @@ OURO_HD inline bool sum6kes_verify_lane(const uint32_t vk[8], uint32_t t, const 
     uint4 v = s4[i];
     sig[4 * i] = v.x; sig[4 * i + 1] = v.y; sig[4 * i + 2] = v.z; sig[4 * i + 3] = v.w;
   }
-  const bool leaf = ed25519_verify_lane(sig, cur, msg, mlen, lane, btab);
+  const bool leaf = ed25519_verify_lane(sig, cur, msg, mlen, lane, btab, false, quad);
   return ok && leaf;
 }
 

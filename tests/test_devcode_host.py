@@ -195,7 +195,7 @@ def _hdr_variants(kats, stride):
     return H.pack(parsed, ea, la, slots_per_kes_period=100)
 
 
-@pytest.mark.parametrize("mode", [0, 1], ids=["throughput", "latency"])
+@pytest.mark.parametrize("mode", [0, 1, 2], ids=["throughput", "latency", "latency_quad"])
 def test_header_drivers(dh, kats, mode):
     """tpraos.h's cores + single-inversion finish, in the throughput schedule
     (one lane, VRF key table shared) and the latency schedule (a lane per

@@ -235,10 +235,15 @@ def _golden_variants(kats):
     return H.pack(parsed, ea, la, slots_per_kes_period=100)
 
 
-def test_lowlat_equals_throughput_and_oracle(gpu_lib, kats):
-    """Latency mode (six lanes per header + finish launch) gives the same
-    verdict bits and outputs as the throughput kernel and the oracle."""
+@pytest.mark.parametrize("quad", ["1", "0"], ids=["lane_quads", "one_lane"])
+def test_lowlat_equals_throughput_and_oracle(gpu_lib, kats, monkeypatch, quad):
+    """Latency mode (eight cores per header + finish launch; each core on a
+    DPP lane quad that splits every group operation's products, or on one
+    lane) gives the same verdict bits and outputs as the throughput kernel and
+    the oracle."""
     from ouroboros_network_amd.tpraos import verify_headers, verify_headers_lowlat
+
+    monkeypatch.setenv("OURO_LAT_QUAD", quad)
 
     batch = _golden_variants(kats)
     wv, wbe, wbl = O.tpraos_verify_batch(batch)
