@@ -204,7 +204,8 @@ int dh_sum6kes_verify(const uint8_t* vk, uint32_t t, const uint8_t* m, uint32_t 
 // The header drivers of tpraos.h for every header of a host SoA batch.
 // mode 0 = throughput (one lane, key table shared), 1 = latency (a fresh lane
 // per core, no sharing), 2 = latency on lane quads (the four products of each
-// group operation emulated in sequence, with the merged operand bounds).  Pointers must be 16-B aligned like device buffers.
+// group operation emulated in sequence, with the merged operand bounds; the
+// finish VRF by VRF as the lane pairs run it).  Pointers must be 16-B aligned like device buffers.
 int dh_tpraos_verify(const ouro_tpraos_batch* b, int mode, uint8_t* verdict, uint8_t* beta_eta,
                      uint8_t* beta_leader) {
   std::vector<Lane> lanes(kLatCores);
@@ -216,6 +217,10 @@ int dh_tpraos_verify(const ouro_tpraos_batch* b, int mode, uint8_t* verdict, uin
     for (int core = 0; core < cores; core++)
       hdr_core(*b, i, core, lanes[mode ? core : 0].w, r, host_btab(), mode == 0, mode != 0,
                mode == 2);
+    if (mode == 2) {
+      hdr_finish_item_split(*b, i, r, verdict, beta_eta, beta_leader);
+      continue;
+    }
     if (mode) hdr_combine_split(r);
     hdr_finish_item(*b, i, r, lanes[0].w, verdict, beta_eta, beta_leader);
   }

@@ -284,6 +284,30 @@ OURO_FI bool ge_decode(ge_p3* h, const uint32_t s[8], bool negate) {
   return m_root || p_root;
 }
 
+// Two decodes at once on a lane quad (latency mode): quad positions 0/2
+// decode sa, 1/3 decode sb -- one exponentiation's time instead of two --
+// and every lane reads both results.  Same semantics as two ge_decode calls.
+OURO_FI void ge_decode_pair_quad(ge_p3* a, bool* oka, ge_p3* b, bool* okb, const uint32_t sa[8],
+                                 const uint32_t sb[8], bool negate) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  uint32_t w[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++)
+    asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(w[i]) : "v"(sa[i]), "v"(sb[i]), "s"(kQuadOdd));
+  ge_p3 P;
+  const uint32_t ok = ge_decode(&P, w, negate) ? 1u : 0u;
+  *a = ge_p3{fe_quad_bcast<0>(P.X), fe_quad_bcast<0>(P.Y), fe_quad_bcast<0>(P.Z),
+             fe_quad_bcast<0>(P.T)};
+  *b = ge_p3{fe_quad_bcast<1>(P.X), fe_quad_bcast<1>(P.Y), fe_quad_bcast<1>(P.Z),
+             fe_quad_bcast<1>(P.T)};
+  *oka = __builtin_amdgcn_mov_dpp((int)ok, 0x00, 0xf, 0xf, true) != 0;
+  *okb = __builtin_amdgcn_mov_dpp((int)ok, 0x55, 0xf, 0xf, true) != 0;
+#else
+  *oka = ge_decode(a, sa, negate);
+  *okb = ge_decode(b, sb, negate);
+#endif
+}
+
 // ge25519_is_canonical: y (bit 255 masked) < p
 OURO_FI bool ge_is_canonical(const uint32_t s[8]) {
   bool top_all_ones = (s[7] & 0x7fffffffu) == 0x7fffffffu;

@@ -165,22 +165,44 @@ __global__ void __launch_bounds__(kBlock, OURO_WAVES) k_tpraos_cores(ouro_tpraos
   }
 }
 
-// Latency mode, launch 2: the shared-inversion finish, one lane per header.
+// Latency mode, launch 2: the finish.  quad = 1: a lane quad per header, its
+// lane pairs finishing one VRF each (vrf_finish_split: one inversion of four
+// Z per VRF), quad position 0 assembling the verdict; quad = 0: one lane per
+// header with one inversion of all eight Z.
 __global__ void __launch_bounds__(kBlock, OURO_WAVES) k_tpraos_finish(ouro_tpraos_batch b,
                                                              const uint32_t* __restrict__ d_n,
                                                              int32_t* res_buf,
                                                              uint8_t* __restrict__ verdict,
                                                              uint8_t* __restrict__ beta_eta,
                                                              uint8_t* __restrict__ beta_leader,
-                                                             int32_t* scratch) {
+                                                             int32_t* scratch, int quad) {
   const size_t n = *d_n;
-  const size_t tid = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const size_t nth = (size_t)gridDim.x * blockDim.x;
+  const int sh = quad ? 2 : 0;
+  const size_t tid = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) >> sh;
+  const size_t nth = ((size_t)gridDim.x * blockDim.x) >> sh;
   int32_t* lane = scratch + tid * kLaneWords;
+  const uint32_t q = threadIdx.x & 3u;
   for (size_t i = tid; i < n; i += nth) {
     int32_t* res = res_buf + i * kLatResWords;
-    hdr_combine_split(res);
-    hdr_finish_item(b, i, res, lane, verdict, beta_eta, beta_leader);
+    if (!quad) {
+      hdr_combine_split(res);
+      hdr_finish_item(b, i, res, lane, verdict, beta_eta, beta_leader);
+      continue;
+    }
+    const int which = (int)(q >> 1);
+    uint32_t pi[20], beta[16];
+    load_words(pi, (which ? b.leader_proof : b.eta_proof) + 80 * i, 5);
+    const uint32_t bit = vrf_finish_split(res, which, pi, beta);
+    // quad position 0 takes position 2's (the leader VRF's) bit
+    const uint32_t other = (uint32_t)__builtin_amdgcn_mov_dpp((int)bit, 0x0a, 0xf, 0xf, true);
+    uint8_t* dst = which ? beta_leader : beta_eta;
+    if ((q & 1u) == 0 && dst) store_words(dst + 64 * i, beta, 4);
+    if (q == 0) {
+      uint32_t v = bit | other;
+      if (res[kResFlags + kCoreOcert] & kFlagOk) v |= 0x01u;
+      if (res[kResFlags + kCoreKes] & kFlagOk) v |= 0x02u;
+      verdict[i] = (uint8_t)v;
+    }
   }
 }
 
@@ -480,12 +502,13 @@ int launch_lowlat(hipStream_t st, const ouro_tpraos_batch& b, const uint32_t* d_
     return (int)std::max<size_t>(1, std::min<size_t>(g, (size_t)ds->max_blocks[id] * per));
   };
   const int quad = lat_quad();
-  const int g1 = grid((size_t)kLatCores * n_cap << (quad ? 2 : 0), kCores), g2 = grid(n_cap, kFinish);
+  const int g1 = grid((size_t)kLatCores * n_cap << (quad ? 2 : 0), kCores);
+  const int g2 = grid(n_cap << (quad ? 2 : 0), kFinish);
   hipLaunchKernelGGL(k_tpraos_cores, dim3(g1), dim3(blk), 0, st, b, d_n, res_buf, scratch,
                      ds->btab, quad);
   if ((rc = launch_check())) return rc;
   hipLaunchKernelGGL(k_tpraos_finish, dim3(g2), dim3(blk), 0, st, b, d_n, res_buf, verdict, be,
-                     bl, scratch);
+                     bl, scratch, quad);
   return launch_check();
 }
 

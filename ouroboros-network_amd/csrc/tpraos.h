@@ -278,6 +278,51 @@ OURO_HD inline uint32_t hdr_finish(const int32_t* res, int32_t* tmp, const uint3
   return v;
 }
 
+// Latency-mode finish of ONE VRF (which = 0: eta, 1: leader) straight from
+// the split cores' record: V = [s]H + (-[c]Gamma), one inversion for this
+// VRF's four Z (H, U, V, [8]Gamma), the c' check and beta.  Returns the VRF's
+// verdict bit (OURO_HDR 0x04 / 0x08); beta is zeroed unless it is set.  The
+// two VRFs of a header run on two lane pairs of a quad (k_tpraos_finish), so
+// a header's finish takes one VRF's time.  Reads res only.
+OURO_HD inline uint32_t vrf_finish_split(const int32_t* res, int which, const uint32_t pi[20],
+                                         uint32_t beta[16]) {
+  const int base = which ? kPtHl : kPtHe;
+  const ge_p2 V = ge_p2_add(ld_point_at(res + (base + 2) * kPtWords),
+                            ld_point_at(res + kLatPart + which * kPtWords));
+  const int32_t* fl = res + kResFlags;
+  const int32_t fu = fl[which ? kCoreUl : kCoreUe];
+  const int32_t fg = fl[which ? kCoreGl : kCoreGe];
+  const int32_t fv = (fl[which ? kCoreVl : kCoreVe] & fg & kFlagOk) | (fg & kFlagGammaX0);
+  // Z^-1 of H, U, V, [8]Gamma by one inversion (prefix products)
+  const fe z0 = ld_fe(res + base * kPtWords + 24), z1 = ld_fe(res + (base + 1) * kPtWords + 24);
+  const fe z3 = ld_fe(res + (base + 3) * kPtWords + 24);
+  const fe p1 = fe_mul(z0, z1), p2 = fe_mul(p1, V.Z);
+  fe inv = fe_invert(fe_mul(p2, z3));
+  const fe i3 = fe_mul(inv, p2);
+  inv = fe_mul(inv, z3);
+  const fe i2 = fe_mul(inv, p1);
+  inv = fe_mul(inv, V.Z);
+  const fe i1 = fe_mul(inv, z0), i0 = fe_mul(inv, z1);
+  uint32_t Henc[8], Uenc[8], Venc[8], G8enc[8];
+  ge_encode_with_inv(Henc, ld_fe(res + base * kPtWords), ld_fe(res + base * kPtWords + 12), i0);
+  ge_encode_with_inv(Uenc, ld_fe(res + (base + 1) * kPtWords),
+                     ld_fe(res + (base + 1) * kPtWords + 12), i1);
+  ge_encode_with_inv(Venc, V.X, V.Y, i2);
+  ge_encode_with_inv(G8enc, ld_fe(res + (base + 3) * kPtWords),
+                     ld_fe(res + (base + 3) * kPtWords + 12), i3);
+  uint32_t Genc[8], c[4], b[16];
+#pragma unroll
+  for (int i = 0; i < 8; i++) Genc[i] = pi[i];
+  if (fv & kFlagGammaX0) Genc[7] &= 0x7fffffffu;
+#pragma unroll
+  for (int i = 0; i < 4; i++) c[i] = pi[8 + i];
+  const bool ceq = vrf_finish(b, Henc, Genc, Uenc, Venc, G8enc, c);
+  const bool ok = (fu & kFlagOk) && (fv & kFlagOk) && ceq;
+#pragma unroll
+  for (int i = 0; i < 16; i++) beta[i] = ok ? b[i] : 0u;
+  return ok ? (which ? 0x08u : 0x04u) : 0u;
+}
+
 // ---- per-header drivers (the kernels' bodies; host-testable) -------------
 OURO_FI void ld_words(uint32_t* w, const uint8_t* p, int n16) {
   const uint4* q = reinterpret_cast<const uint4*>(p);
@@ -346,6 +391,24 @@ OURO_HD inline void hdr_core(const ouro_tpraos_batch& b, size_t i, int core,
     }
   }
   res[kResFlags + core] = flag;
+}
+
+// latency-mode finish of header i, VRF by VRF (the host form of the lane-pair
+// finish in k_tpraos_finish)
+OURO_HD inline void hdr_finish_item_split(const ouro_tpraos_batch& b, size_t i, const int32_t* res,
+                                          uint8_t* verdict, uint8_t* beta_eta,
+                                          uint8_t* beta_leader) {
+  uint32_t v = 0;
+  if (res[kResFlags + kCoreOcert] & kFlagOk) v |= 0x01u;
+  if (res[kResFlags + kCoreKes] & kFlagOk) v |= 0x02u;
+  for (int which = 0; which < 2; which++) {
+    uint32_t pi[20], beta[16];
+    ld_words(pi, (which ? b.leader_proof : b.eta_proof) + 80 * i, 5);
+    v |= vrf_finish_split(res, which, pi, beta);
+    uint8_t* dst = which ? beta_leader : beta_eta;
+    if (dst) st_words(dst + 64 * i, beta, 4);
+  }
+  verdict[i] = (uint8_t)v;
 }
 
 OURO_HD inline void hdr_finish_item(const ouro_tpraos_batch& b, size_t i,

@@ -381,10 +381,17 @@ OURO_HD inline bool ed25519_verify_lane(const uint32_t sig[16], const uint32_t p
     ok = ok && ge_is_canonical(pk) && !ge_has_small_order(pk);
   }
   ge_p3 negA, negR;
-  ok = ge_decode(&negA, pk, true) && ok;
+  bool okA, okR;
+  if (quad) {
+    ge_decode_pair_quad(&negA, &okA, &negR, &okR, pk, R, true);
+  } else {
+    okA = ge_decode(&negA, pk, true);
+    okR = ge_decode(&negR, R, true);
+  }
+  ok = okA && ok;
   // encode(R') == R_bytes  <=>  R_bytes is the canonical encoding of R' (a point)
   ok = ge_is_canonical(R) && ok;
-  ok = ge_decode(&negR, R, true) && ok;
+  ok = okR && ok;
   ok = ok && !(fe_iszero(negR.X) && (R[7] >> 31) != 0);
   // h = SHA-512(R || A || M) mod L
   uint32_t pre[16];
