@@ -106,6 +106,15 @@ void dh_fe_sub(uint8_t* out, const uint8_t* a, const uint8_t* b) {
 void dh_fe_invert(uint8_t* out, const uint8_t* a) {
   fe_to_bytes(out, fe_invert(fe_from_bytes(a)));
 }
+void dh_fe_invert_vartime(uint8_t* out, const uint8_t* a) {
+  fe_to_bytes(out, fe_invert_vartime(fe_from_bytes(a)));
+}
+// the same from raw limbs (< 2^31 each: unreduced representations)
+void dh_fe_invert_vartime_limbs(uint8_t* out, const uint32_t* limbs) {
+  fe f = fe_make(limbs[0], limbs[1], limbs[2], limbs[3], limbs[4], limbs[5], limbs[6], limbs[7],
+                 limbs[8], limbs[9]);
+  fe_to_bytes(out, fe_invert_vartime(f));
+}
 // raw-limb round trip: limbs given as 10 uint32 (< 2^31), canonical encoding out
 void dh_fe_limbs_tobytes(uint8_t* out, const uint32_t* limbs) {
   fe f = fe_make(limbs[0], limbs[1], limbs[2], limbs[3], limbs[4], limbs[5], limbs[6], limbs[7],

@@ -13,6 +13,7 @@
 // libsodium 1.0.18 exactly.
 #pragma once
 #include "fe25519.h"
+#include "modinv.h"
 
 namespace ouro {
 
@@ -251,7 +252,7 @@ OURO_FI void ge_encode_with_inv(uint32_t out[8], const fe& X, const fe& Y, const
 }
 
 OURO_FI void ge_p2_encode(uint32_t out[8], const ge_p2& p) {
-  ge_encode_with_inv(out, p.X, p.Y, fe_invert(p.Z));
+  ge_encode_with_inv(out, p.X, p.Y, fe_invert_vartime(p.Z));
 }
 
 // ---- decoding & acceptance predicates (libsodium 1.0.18) -------------------

@@ -239,7 +239,7 @@ OURO_HD inline uint32_t hdr_finish(const int32_t* res, int32_t* tmp, const uint3
     acc = fe_mul(acc, ld_fe(res + k * kPtWords + 24));
     st_fe(tmp + 12 * k, acc);
   }
-  fe inv = fe_invert(acc);
+  fe inv = fe_invert_vartime(acc);
   // walk back: Z_k^-1 = inv * P_{k-1}, inv <- inv * Z_k
 #pragma unroll 1
   for (int k = kHdrPoints - 1; k > 0; k--) {
@@ -297,7 +297,7 @@ OURO_HD inline uint32_t vrf_finish_split(const int32_t* res, int which, const ui
   const fe z0 = ld_fe(res + base * kPtWords + 24), z1 = ld_fe(res + (base + 1) * kPtWords + 24);
   const fe z3 = ld_fe(res + (base + 3) * kPtWords + 24);
   const fe p1 = fe_mul(z0, z1), p2 = fe_mul(p1, V.Z);
-  fe inv = fe_invert(fe_mul(p2, z3));
+  fe inv = fe_invert_vartime(fe_mul(p2, z3));
   const fe i3 = fe_mul(inv, p2);
   inv = fe_mul(inv, z3);
   const fe i2 = fe_mul(inv, p1);

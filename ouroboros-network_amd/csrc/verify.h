@@ -22,6 +22,7 @@
 #include "blake2b.h"
 #include "ge25519.h"
 #include "lattice.h"
+#include "modinv.h"
 #include "sc25519.h"
 #include "sha512.h"
 
@@ -527,7 +528,7 @@ OURO_FI void fe_invert4(fe out[4], const fe z[4]) {
   fe a1 = fe_mul(z[0], z[1]);
   fe a2 = fe_mul(a1, z[2]);
   fe a3 = fe_mul(a2, z[3]);
-  fe inv = fe_invert(a3);
+  fe inv = fe_invert_vartime(a3);
   out[3] = fe_mul(inv, a2);
   inv = fe_mul(inv, z[3]);
   out[2] = fe_mul(inv, a1);

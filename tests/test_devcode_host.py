@@ -55,6 +55,29 @@ def test_field_ops(dh):
         assert dec(out.raw) == pow(x, P - 2, P)
 
 
+def test_invert_vartime(dh):
+    """modinv.h's divsteps inversion equals z^(p-2) (0 -> 0) on edge values,
+    random canonical values, values >= p and unreduced limb vectors."""
+    rng = np.random.default_rng(5)
+    out = ctypes.create_string_buffer(32)
+    specials = [0, 1, 2, 3, 19, P - 1, P - 2, (P - 1) // 2, (P + 1) // 2, 2**254, 2**255 - 20,
+                2**128 - 1, 2**30, 2**30 - 1, 2**240 + 1, 5**100 % P]
+    vals = specials + [int.from_bytes(rng.bytes(32), "little") % P for _ in range(3000)]
+    vals += [int.from_bytes(rng.bytes(32), "little") >> int(rng.integers(0, 250))
+             for _ in range(500)]
+    for x in vals:
+        dh.dh_fe_invert_vartime(out, enc(x % P))
+        assert dec(out.raw) == pow(x, P - 2, P), x
+    E = [0, 26, 51, 77, 102, 128, 153, 179, 204, 230]
+    for _ in range(500):
+        top = int(rng.choice([1 << 26, 1 << 28, 1 << 31]))
+        limbs = [int(rng.integers(0, top)) for _ in range(10)]
+        arr = (ctypes.c_uint32 * 10)(*limbs)
+        dh.dh_fe_invert_vartime_limbs(out, arr)
+        x = sum(l << E[i] for i, l in enumerate(limbs)) % P
+        assert dec(out.raw) == pow(x, P - 2, P)
+
+
 def test_tobytes_canonicalises_unreduced_limbs(dh):
     """fe_to_words on unsigned limb vectors at and beyond the 'reduced' bounds
     (anything below 2^31 per limb)."""
