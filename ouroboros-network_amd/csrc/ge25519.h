@@ -144,15 +144,21 @@ OURO_FI fe4 fe_mul_quad(const fe4& a, const fe4& b) {
   return r;
 #endif
 }
-// out.v[j] = a.v[j]^2, except out.v[2] = 2 a.v[2]^2
-OURO_FI fe4 fe_sq_quad_dbl2(const fe4& a) {
 #if defined(__HIP_DEVICE_COMPILE__)
+// this lane's x^2 (2 x^2 on quad position 2), gathered
+OURO_FI fe4 fe_sq_quad_dbl2_own(const fe& x) {
   uint64_t t[10];
-  fe_sq_cols(t, fe_quad_pick(a.v[0], a.v[1], a.v[2], a.v[3]));
+  fe_sq_cols(t, x);
   const uint32_t sh = (threadIdx.x & 3u) == 2u ? 1u : 0u;
 #pragma unroll
   for (int k = 0; k < 10; k++) t[k] <<= sh;
   return fe_quad_gather(fe_carry64(t));
+}
+#endif
+// out.v[j] = a.v[j]^2, except out.v[2] = 2 a.v[2]^2
+OURO_FI fe4 fe_sq_quad_dbl2(const fe4& a) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return fe_sq_quad_dbl2_own(fe_quad_pick(a.v[0], a.v[1], a.v[2], a.v[3]));
 #else
   fe4 r;
   for (int j = 0; j < 4; j++) {
@@ -181,9 +187,9 @@ OURO_FI ge_p3 ge_p1p1_to_p3_quad(const ge_p1p1& p) {
   const fe4 m = ge_p1p1_products_quad(p);
   return ge_p3{m.v[0], m.v[1], m.v[2], m.v[3]};
 }
-// ge_p2_dbl with its four squarings on the four lanes
-OURO_FI ge_p1p1 ge_p2_dbl_quad(const ge_p2& p) {
-  const fe4 s = fe_sq_quad_dbl2(fe4{{p.X, p.Y, p.Z, fe_add(p.X, p.Y)}});
+// the doubling formula from the four squares A = X^2, B = Y^2, C = 2 Z^2,
+// S = (X + Y)^2 (every lane holds all four)
+OURO_FI ge_p1p1 ge_dbl_from_squares(const fe4& s) {
   const fe &A = s.v[0], &B = s.v[1], &C = s.v[2], &S = s.v[3];
   ge_p1p1 r;
   r.Y = fe_carry(fe_add(B, A));
@@ -191,6 +197,32 @@ OURO_FI ge_p1p1 ge_p2_dbl_quad(const ge_p2& p) {
   r.X = fe_sub(S, r.Y);
   r.T = fe_sub(fe_add(C, A), B);
   return r;
+}
+// ge_p2_dbl with its four squarings on the four lanes
+OURO_FI ge_p1p1 ge_p2_dbl_quad(const ge_p2& p) {
+  return ge_dbl_from_squares(fe_sq_quad_dbl2(fe4{{p.X, p.Y, p.Z, fe_add(p.X, p.Y)}}));
+}
+// 2 * (p1p1 point): the p2 conversion's products X, Y, Z stay on quad
+// positions 0, 1, 2, which are exactly the squaring inputs those positions
+// need; position 3 adds X + Y from its neighbours -- no gather, no pick
+OURO_FI ge_p1p1 ge_dbl_from_p1p1_quad(const ge_p1p1& t) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const fe a = fe_sel_lanes(t.T, fe_sel_lanes(t.Z, t.X, kQuadHigh), kQuadOdd);
+  const fe b = fe_sel_lanes(fe_sel_lanes(t.X, t.Z, kQuadHigh), t.Y, kQuadOdd);
+  const fe m = fe_mul(a, b);  // position 0: X, 1: Y, 2: Z, 3: (unused) X Y
+  const uint32_t pos3 = (threadIdx.x & 3u) == 3u ? 0xffffffffu : 0u;
+  fe in;
+#pragma unroll
+  for (int i = 0; i < 10; i++) {
+    // quad_perm [0,1,2,0]: own product, position 3 takes X; [1,1,1,1]: Y
+    const uint32_t own = (uint32_t)__builtin_amdgcn_mov_dpp((int)m.v[i], 0x24, 0xf, 0xf, true);
+    const uint32_t y = (uint32_t)__builtin_amdgcn_mov_dpp((int)m.v[i], 0x55, 0xf, 0xf, true);
+    in.v[i] = own + (y & pos3);
+  }
+  return ge_dbl_from_squares(fe_sq_quad_dbl2_own(in));
+#else
+  return ge_p2_dbl_quad(ge_p1p1_to_p2_quad(t));
+#endif
 }
 // ge_add_cached with its four products on the four lanes; an affine Q carries
 // Z2 = 2, so D = 2 Z_P either way
@@ -208,6 +240,36 @@ OURO_FI ge_p1p1 ge_add_cached_quad(const ge_p3& p, const ge_cached& q, bool neg)
   r.T = fe_select(Dp, Dm, neg);
   return r;
 }
+
+#if defined(__HIP_DEVICE_COMPILE__)
+// P + Q for a p1p1 P, each lane holding only its own operand of Q (quad
+// position 0: Y+X or Y-X of Q as the sign asks, 1: the other, 2: 2dT, 3: 2Z),
+// loaded by that lane alone.  The p3 conversion's products stay on their
+// positions (0: X, 1: Y, 2: Z, 3: T); positions 0/1 form Y +- X from two
+// quad_perm reads, 2/3 read T / Z directly.
+OURO_FI ge_p1p1 ge_add_own_quad(const ge_p1p1& t, const fe& b, bool neg) {
+  const fe pa = fe_sel_lanes(t.T, fe_sel_lanes(t.Z, t.X, kQuadHigh), kQuadOdd);
+  const fe pb = fe_sel_lanes(fe_sel_lanes(t.X, t.Z, kQuadHigh), t.Y, kQuadOdd);
+  const fe m = fe_mul(pa, pb);
+  fe u, v;
+#pragma unroll
+  for (int i = 0; i < 10; i++) {
+    // quad_perm [1,1,3,2]: Y, Y, T, Z; [0,0,0,0]: X
+    u.v[i] = (uint32_t)__builtin_amdgcn_mov_dpp((int)m.v[i], 0xb5, 0xf, 0xf, true);
+    v.v[i] = (uint32_t)__builtin_amdgcn_mov_dpp((int)m.v[i], 0x00, 0xf, 0xf, true);
+  }
+  const fe a = fe_sel_lanes(fe_sel_lanes(fe_add(u, v), fe_sub(u, v), kQuadOdd), u, kQuadHigh);
+  const fe4 g = fe_quad_gather(fe_mul(a, b));
+  const fe &A = g.v[0], &B = g.v[1], &C = g.v[2], &D = g.v[3];
+  const fe Dp = fe_add(D, C), Dm = fe_sub(D, C);
+  ge_p1p1 r;
+  r.X = fe_sub(A, B);
+  r.Y = fe_add(A, B);
+  r.Z = fe_select(Dm, Dp, neg);
+  r.T = fe_select(Dp, Dm, neg);
+  return r;
+}
+#endif
 
 OURO_FI ge_p3 ge_p3_add(const ge_p3& p, const ge_p3& q) {
   return ge_p1p1_to_p3(ge_add_cached(p, ge_p3_to_cached(q), false));

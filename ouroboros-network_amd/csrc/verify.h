@@ -77,6 +77,12 @@ OURO_FI fe ld_fe(const int32_t* p) {
   OURO_TRK(ouro_trk_load(p, f.b));
   return f;
 }
+// one element at an 8-byte-aligned address (fe k of a table entry)
+OURO_FI fe ld_fe_w2(const int32_t* p) {
+  const int2* q = reinterpret_cast<const int2*>(p);
+  const int2 a = q[0], b = q[1], c = q[2], d = q[3], e = q[4];
+  return fe_make(a.x, a.y, b.x, b.y, c.x, c.y, d.x, d.y, e.x, e.y);
+}
 // cached point: 40 words = 10 x int4, fe k at words [10k, 10k+10)
 OURO_FI void st_cached(int32_t* p, const ge_cached& c) {
   int4* q = reinterpret_cast<int4*>(p);
@@ -278,7 +284,7 @@ OURO_FI void dsm_body(int32_t* lane, const int32_t* btab, uint32_t cfg) {
     if (!OURO_DSM_SKIP_ID || j != top - 1) {
 #pragma unroll 1
       for (int k = 0; k < 4; k++)
-        t = kQuad ? ge_p2_dbl_quad(ge_p1p1_to_p2_quad(t)) : ge_p2_dbl(ge_p1p1_to_p2(t));
+        t = kQuad ? ge_dbl_from_p1p1_quad(t) : ge_p2_dbl(ge_p1p1_to_p2(t));
     }
     prefetch ^= pf1 ^ pf2 ^ pf3 ^ pf4 ^ pf5 ^ pf6;
     // up to four additions, each from a wave-uniform source
@@ -290,6 +296,25 @@ OURO_FI void dsm_body(int32_t* lane, const int32_t* btab, uint32_t cfg) {
       const bool neg = d < 0;
       const int32_t mag = neg ? -d : d;
       const int idx = mag > 0 ? mag - 1 : 0;
+#if defined(__HIP_DEVICE_COMPILE__)
+      if (kQuad && !(OURO_DSM_SKIP_ID && fresh)) {
+        // each lane of the quad loads only its own operand of the entry
+        const uint32_t qp = threadIdx.x & 3u;
+        const bool niels = src >= 2;
+        const int k = qp < 2 ? (int)(qp ^ (neg ? 1u : 0u)) : (qp == 2 ? (niels ? 2 : 3) : (niels ? 0 : 2));
+        const int32_t* ent =
+            niels ? btab + ((src == 3 ? (size_t)kBTabEntries : 0) + idx) * kNielsWords
+                  : (src == 0 ? tab1 : tab2) + idx * kCachedWords;
+        fe b = ld_fe_w2(ent + 10 * k);
+        // constants: the identity's operands (1, 1, 0, 2); a niels entry's 2Z = 2
+        if (mag == 0 || (niels && qp == 3)) {
+          b = fe_zero();
+          b.v[0] = qp < 2 ? 1u : (qp == 2 ? 0u : 2u);
+        }
+        t = ge_add_own_quad(t, b, neg);
+        continue;
+      }
+#endif
       ge_cached q;
       if (src < 2) {
         q = ld_cached((src == 0 ? tab1 : tab2) + idx * kCachedWords);
