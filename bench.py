@@ -177,9 +177,62 @@ def ed25519_rate(device, n: int, reps: int):
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / reps
     ok = int(ver.sum().item())
-    return {"value": n / (ms * 1e-3), "unit": "verifies/s", "n": n, "ms_per_launch": ms,
-            "all_valid": ok == n,
-            "roofline_frac": (n * MACS_PER_ED25519 / (ms * 1e-3) / 1e12)}
+    out = {"value": n / (ms * 1e-3), "unit": "verifies/s", "n": n, "ms_per_launch": ms,
+           "all_valid": ok == n,
+           "roofline_frac": (n * MACS_PER_ED25519 / (ms * 1e-3) / 1e12)}
+    m = min(n, 65536)
+    try:
+        out["cpu_libsodium"] = libsodium_ed25519_rate(pk[: m * 32].cpu().numpy(),
+                                                      sig[: m * 64].cpu().numpy(),
+                                                      msg[: m * 32].cpu().numpy(),
+                                                      min(16, os.cpu_count() or 1))
+    except Exception as e:  # noqa: BLE001
+        out["cpu_libsodium"] = {"error": str(e)}
+    return out
+
+
+SODIUM_SO = "/opt/conda/lib/libsodium.so.23"
+
+
+def libsodium_ed25519_rate(pk, sig, msg, threads: int):
+    """the function the reference calls for Ed25519,
+    libsodium 1.0.18's crypto_sign_ed25519_verify_detached (the CI pin), timed
+    on the host cores over the same synthetic signatures the GPU leg verified.
+    ctypes drops the GIL for the call, so one Python thread per core runs the
+    library concurrently.  A CPU baseline only -- never the measured path."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    if not os.path.exists(SODIUM_SO):
+        return {"error": f"{SODIUM_SO} absent on this host"}
+    so = ctypes.CDLL(SODIUM_SO)
+    if so.sodium_init() < 0:
+        return {"error": "sodium_init failed"}
+    fn = so.crypto_sign_ed25519_verify_detached
+    fn.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_ulonglong, ctypes.c_char_p]
+    fn.restype = ctypes.c_int
+    m = len(pk) // 32
+    pkb, sgb, msb = pk.tobytes(), sig.tobytes(), msg.tobytes()
+    items = [(sgb[i * 64:(i + 1) * 64], msb[i * 32:(i + 1) * 32], pkb[i * 32:(i + 1) * 32])
+             for i in range(m)]
+
+    def run(lo, hi):
+        return sum(1 for s, g, p in items[lo:hi] if fn(s, g, 32, p) == 0)
+
+    def timed(k, nthreads):
+        step = (k + nthreads - 1) // nthreads
+        t0 = time.perf_counter()
+        with ThreadPoolExecutor(nthreads) as ex:
+            acc = sum(ex.map(lambda j: run(j * step, min(k, (j + 1) * step)), range(nthreads)))
+        return k / (time.perf_counter() - t0), acc
+
+    rate, acc = timed(m, threads)
+    m1 = min(m, 4096)
+    rate1, acc1 = timed(m1, 1)
+    return {"value": round(rate, 1), "unit": "verifies/s", "cores": threads, "kind": "reference",
+            "sample": f"first {m} of the same synthetic signatures (32-B messages), "
+                      f"libsodium 1.0.18 crypto_sign_ed25519_verify_detached via ctypes",
+            "one_core": round(rate1, 1), "one_core_sample": m1,
+            "accepts_all": acc == m and acc1 == m1}
 
 
 def component_rates(hdr, n: int, reps: int = 3):
