@@ -88,7 +88,9 @@ int ouro_vrf03_proof_to_hash(unsigned char *output, const unsigned char *proof);
 
 /* Replaces SumKES.verifyKES (Sum6KES Ed25519DSIGN Blake2b_256), called via
  * SL.verifySignedKES at ouroboros-consensus-shelley/src/Ouroboros/Consensus/
- * Shelley/Ledger/Integrity.hs:27.  t = KES period relative to the opcert. */
+ * Shelley/Ledger/Integrity.hs:27.  t = KES period relative to the opcert.
+ * The reference's Period is a 64-bit Word; every t >= 63 selects leaf 63, so
+ * callers saturate larger periods at 2^32 - 1 (kes.py periods_u32). */
 int ouro_sum6kes_verify(const unsigned char *vk, unsigned int t, const unsigned char *m,
                         unsigned long long mlen, const unsigned char *sig);
 

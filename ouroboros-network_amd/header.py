@@ -22,6 +22,7 @@ from typing import List, Sequence, Tuple
 
 import numpy as np
 
+from .kes import periods_u32
 from .tpraos import HeaderBatch
 
 
@@ -207,8 +208,8 @@ def pack(headers: Sequence[ShelleyHeader], eta_alpha: Sequence[bytes],
         ocert_counter=np.array([h.ocert_counter for h in headers], np.uint64),
         ocert_kes_period=np.array([h.ocert_kes_period for h in headers], np.uint64),
         ocert_sigma=rows(lambda h: h.ocert_sigma, 64),
-        kes_t=np.array([kes_t(h.slot, slots_per_kes_period, h.ocert_kes_period)
-                        for h in headers], np.uint32),
+        kes_t=periods_u32([kes_t(h.slot, slots_per_kes_period, h.ocert_kes_period)
+                           for h in headers]),
         kes_sig=rows(lambda h: h.kes_sig, 448),
         body=np.frombuffer(b"".join(h.body for h in headers) or b"\0", np.uint8),
         body_off=offs,

@@ -79,3 +79,28 @@ def test_missing_library_fails_loudly(tmp_path):
             _native.load(str(tmp_path / "nope.so"))
         finally:
             _native._lib = _native._lib_saved
+
+
+def test_kes_period_saturation_keeps_word_semantics():
+    """kes.periods_u32: the reference's SumKES path choice (t >= half: go right,
+    t -= half) restated over unbounded ints picks the same leaf for t and for
+    min(t, 2^32 - 1), for every Word-sized t."""
+    import numpy as np
+
+    from ouroboros_network_amd.kes import periods_u32
+
+    def leaf(t):
+        idx = 0
+        for k in range(6, 0, -1):
+            half = 1 << (k - 1)
+            if t >= half:
+                idx, t = idx + half, t - half
+        return idx
+
+    ts = [0, 1, 31, 32, 62, 63, 64, 65, 1000, (1 << 32) - 1, 1 << 32, (1 << 63) + 5, (1 << 64) - 1]
+    sat = periods_u32(ts)
+    assert sat.dtype == np.uint32
+    assert [leaf(t) for t in ts] == [leaf(int(s)) for s in sat]
+    assert list(periods_u32(np.array(ts, np.uint64))) == list(sat)
+    with pytest.raises(ValueError):
+        periods_u32([3, -1])

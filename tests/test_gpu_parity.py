@@ -425,3 +425,27 @@ def test_byron_batch_matches_oracle(gpu_lib):
     want = np.array([O.ed25519_verify_byron(c[1], c[2], c[0]) for c in cases])
     np.testing.assert_array_equal(got, want)
     assert want.sum() > 700
+
+
+def test_kes_periods_beyond_the_tree(gpu_lib):
+    """Periods >= 64 (the reference's Period is a 64-bit Word): every t >= 63
+    walks right at all six levels to leaf 63 (SumKES.verifyKES; SingleKES's
+    assert is compiled out), so a leaf-63 signature verifies and others do
+    not.  The host layer saturates Word periods at 2^32 - 1 for the ABI."""
+    from ouroboros_network_amd import Sum6KES
+
+    rng = np.random.default_rng(11)
+    seed = rng.bytes(32)
+    vk = O.kes_keygen(seed)
+    m = rng.bytes(544)
+    sig63, sig62 = O.kes_sign(seed, 63, m), O.kes_sign(seed, 62, m)
+    periods = [62, 63, 64, 65, 100, 127, 128, 1 << 20, (1 << 32) - 1, 1 << 32, (1 << 64) - 1]
+    rows = [(t, s) for t in periods for s in (sig63, sig62)]
+    got = Sum6KES.verify_batch([vk] * len(rows), [t for t, _ in rows], [m] * len(rows),
+                               np.frombuffer(b"".join(s for _, s in rows), np.uint8).reshape(-1, 448))
+    want = [O.kes_verify(vk, min(t, (1 << 32) - 1), m, s) for t, s in rows]
+    np.testing.assert_array_equal(got, want)
+    # leaf 63 for every t >= 63, leaf 62 only at t = 62
+    assert list(got) == [t == 62 if s is sig62 else t >= 63 for t, s in rows]
+    for t, s in rows:
+        assert (Sum6KES.verify_kes((), vk, t, m, s) is None) == (t == 62 if s is sig62 else t >= 63)
