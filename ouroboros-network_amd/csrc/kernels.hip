@@ -118,6 +118,21 @@ __global__ void __launch_bounds__(kBlock, OURO_WAVES) k_sum6kes_verify(
   }
 }
 
+#ifndef OURO_HDR_LOOP
+#define OURO_HDR_LOOP 0
+#endif
+#ifndef OURO_HDR_FINISH_NI
+#define OURO_HDR_FINISH_NI 0
+#endif
+#if OURO_HDR_FINISH_NI
+// A/B: the finish (inversion, encodings, hashes) with its own register allocation
+__device__ __noinline__ void hdr_finish_item_ni(const ouro_tpraos_batch& b, size_t i,
+                                                const int32_t* res, int32_t* tmp, uint8_t* verdict,
+                                                uint8_t* beta_eta, uint8_t* beta_leader) {
+  hdr_finish_item(b, i, res, tmp, verdict, beta_eta, beta_leader);
+}
+#endif
+
 // Throughput mode: one lane per header runs every core of tpraos.h, sharing
 // the VRF key decode and its table, then the single-inversion finish.
 __global__ void __launch_bounds__(kBlock, OURO_WAVES) k_tpraos_verify(ouro_tpraos_batch b,
@@ -131,13 +146,23 @@ __global__ void __launch_bounds__(kBlock, OURO_WAVES) k_tpraos_verify(ouro_tprao
   int32_t* lane = scratch + tid * kHdrLaneWords;
   int32_t* res = lane + kLaneWords;
   for (size_t i = tid; i < b.n; i += nth) {
+#if OURO_HDR_LOOP
+    // A/B: one copy of the core dispatch, the core chosen at run time
+#pragma unroll 1
+    for (int c = kCoreOcert; c <= kCoreVl; c++) hdr_core(b, i, c, lane, res, btab);
+#else
     hdr_core(b, i, kCoreOcert, lane, res, btab);
     hdr_core(b, i, kCoreKes, lane, res, btab);
     hdr_core(b, i, kCoreUe, lane, res, btab);
     hdr_core(b, i, kCoreUl, lane, res, btab);
     hdr_core(b, i, kCoreVe, lane, res, btab);
     hdr_core(b, i, kCoreVl, lane, res, btab);
+#endif
+#if OURO_HDR_FINISH_NI
+    hdr_finish_item_ni(b, i, res, lane, verdict, beta_eta, beta_leader);
+#else
     hdr_finish_item(b, i, res, lane, verdict, beta_eta, beta_leader);
+#endif
   }
 }
 
