@@ -18,6 +18,7 @@ import numpy as np
 
 from . import _native
 from ._pack import ptr
+from .kes import periods_u32
 
 HDR_OCERT_OK = _native.HDR_OCERT_OK
 HDR_KES_OK = _native.HDR_KES_OK
@@ -68,7 +69,11 @@ class HeaderBatch:
     def __post_init__(self):
         for f in fields(self):
             dt, w = LAYOUT[f.name]
-            a = np.ascontiguousarray(getattr(self, f.name), dtype=dt)
+            if f.name == "kes_t":
+                # a Word period saturates (kes.periods_u32), never wraps
+                a = periods_u32(np.asarray(getattr(self, f.name)).ravel())
+            else:
+                a = np.ascontiguousarray(getattr(self, f.name), dtype=dt)
             if w is not None:
                 a = a.reshape(-1, w)
             setattr(self, f.name, a)

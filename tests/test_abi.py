@@ -104,3 +104,22 @@ def test_kes_period_saturation_keeps_word_semantics():
     assert list(periods_u32(np.array(ts, np.uint64))) == list(sat)
     with pytest.raises(ValueError):
         periods_u32([3, -1])
+
+
+def test_header_batch_saturates_kes_t():
+    """HeaderBatch coerces kes_t through kes.periods_u32 (no silent uint32 wrap)."""
+    import numpy as np
+
+    from ouroboros_network_amd.tpraos import HeaderBatch
+
+    n = 3
+    z = lambda w: np.zeros((n, w), np.uint8)  # noqa: E731
+    hb = HeaderBatch(issuer_vk=z(32), vrf_vk=z(32), eta_proof=z(80), leader_proof=z(80),
+                     eta_alpha=z(32), leader_alpha=z(32), hot_vk=z(32),
+                     ocert_counter=np.zeros(n, np.uint64), ocert_kes_period=np.zeros(n, np.uint64),
+                     ocert_sigma=z(64), kes_t=np.array([5, 1 << 32, (1 << 64) - 1], np.uint64),
+                     kes_sig=z(448), body=np.zeros(1, np.uint8), body_off=np.zeros(n, np.uint64),
+                     body_len=np.zeros(n, np.uint32))
+    assert hb.kes_t.dtype == np.uint32
+    assert list(hb.kes_t) == [5, 0xFFFFFFFF, 0xFFFFFFFF]
+    assert list(hb.slice(1, 3).kes_t) == [0xFFFFFFFF, 0xFFFFFFFF]
