@@ -214,6 +214,15 @@ constexpr uint32_t dsm_cfg(int nw1, int nw2, bool useB, int tab1 = 0, int tab2 =
 #ifndef OURO_DSM_SKIP_ID
 #define OURO_DSM_SKIP_ID 1  // A/B switch: 0 = doublings/addition from the identity kept
 #endif
+// A/B switches: doublings per loop trip in a window.  One lane per item: 1
+// (72.7 ms vs 73.2 / 73.8 for 2 / 4, I-cache); lane quads (latency mode, few
+// waves): 4 (configs[4] p50 0.647 -> 0.636 ms).  profiles/r01h/ab_unroll*.json
+#ifndef OURO_DBL_UNROLL
+#define OURO_DBL_UNROLL 1
+#endif
+#ifndef OURO_DBL_UNROLL_QUAD
+#define OURO_DBL_UNROLL_QUAD 4
+#endif
 template <bool kQuad>
 OURO_FI void dsm_body(int32_t* lane, const int32_t* btab, uint32_t cfg) {
   const int nw1 = (int)(cfg & 0x7f), nw2 = (int)((cfg >> 8) & 0x7f);
@@ -282,9 +291,13 @@ OURO_FI void dsm_body(int32_t* lane, const int32_t* btab, uint32_t cfg) {
     }
     // (the top window starts from the identity: its doublings are skipped)
     if (!OURO_DSM_SKIP_ID || j != top - 1) {
-#pragma unroll 1
-      for (int k = 0; k < 4; k++)
-        t = kQuad ? ge_dbl_from_p1p1_quad(t) : ge_p2_dbl(ge_p1p1_to_p2(t));
+      if constexpr (kQuad) {
+#pragma unroll OURO_DBL_UNROLL_QUAD
+        for (int k = 0; k < 4; k++) t = ge_dbl_from_p1p1_quad(t);
+      } else {
+#pragma unroll OURO_DBL_UNROLL
+        for (int k = 0; k < 4; k++) t = ge_p2_dbl(ge_p1p1_to_p2(t));
+      }
     }
     prefetch ^= pf1 ^ pf2 ^ pf3 ^ pf4 ^ pf5 ^ pf6;
     // up to four additions, each from a wave-uniform source
