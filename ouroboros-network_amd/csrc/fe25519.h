@@ -457,8 +457,11 @@ OURO_FI bool fe_isnegative(const fe& f) {
 }
 
 // ---- exponentiations (kept out of line: code size) ----------
+#ifndef OURO_SQN_UNROLL
+#define OURO_SQN_UNROLL 1  // A/B switch: squarings per loop trip in the chains
+#endif
 OURO_FI fe fe_sqn(fe t, int n) {
-#pragma unroll 1
+#pragma unroll OURO_SQN_UNROLL
   for (int i = 0; i < n; i++) t = fe_sq(t);
   return t;
 }
