@@ -223,6 +223,11 @@ constexpr uint32_t dsm_cfg(int nw1, int nw2, bool useB, int tab1 = 0, int tab2 =
 #ifndef OURO_DBL_UNROLL_QUAD
 #define OURO_DBL_UNROLL_QUAD 4
 #endif
+#ifndef OURO_ADD_UNROLL_QUAD
+// the four addition sources unrolled in lane-quad mode: configs[4] p50
+// 0.643 -> 0.638 ms (two runs each); lane mode keeps the rolled loop
+#define OURO_ADD_UNROLL_QUAD 4
+#endif
 template <bool kQuad>
 OURO_FI void dsm_body(int32_t* lane, const int32_t* btab, uint32_t cfg) {
   const int nw1 = (int)(cfg & 0x7f), nw2 = (int)((cfg >> 8) & 0x7f);
@@ -301,7 +306,8 @@ OURO_FI void dsm_body(int32_t* lane, const int32_t* btab, uint32_t cfg) {
     }
     prefetch ^= pf1 ^ pf2 ^ pf3 ^ pf4 ^ pf5 ^ pf6;
     // up to four additions, each from a wave-uniform source
-#pragma unroll 1
+    constexpr int kAddUnroll = kQuad ? OURO_ADD_UNROLL_QUAD : 1;
+#pragma unroll kAddUnroll
     for (int src = 0; src < 4; src++) {
       const bool active = src == 0 ? act1 : src == 1 ? act2 : src == 2 ? actB : actB2;
       if (!active) continue;
