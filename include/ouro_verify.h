@@ -41,7 +41,18 @@ extern "C" {
 #define OURO_HDR_KES_OK 0x02u        /* Sum6KES over the header body          */
 #define OURO_HDR_VRF_ETA_OK 0x04u    /* nonce VRF proof                       */
 #define OURO_HDR_VRF_LEADER_OK 0x08u /* leader VRF proof                      */
-#define OURO_HDR_ALL_OK 0x0fu
+/* The header's claimed certifiedOutput equals the output computed from the
+ * proof (set only when the proof verified and the batch carries the claimed
+ * outputs).  The reference ("ref2020") accepts on the proof alone and then
+ * uses the CLAIMED output downstream: the leader check
+ * (ouroboros-consensus-shelley/src/Ouroboros/Consensus/Shelley/Protocol.hs:484-486,
+ * SL.checkLeaderValue (VRF.certifiedOutput certNat)), the nonce update and the
+ * chain-selection tiebreak (.../Shelley/Ledger/TPraos.hs:40).  "strict"
+ * callers require these bits too (OURO_HDR_STRICT_OK). */
+#define OURO_HDR_ETA_CLAIM_OK 0x10u
+#define OURO_HDR_LEADER_CLAIM_OK 0x20u
+#define OURO_HDR_ALL_OK 0x0fu    /* ref2020: every proof / signature valid    */
+#define OURO_HDR_STRICT_OK 0x3fu /* strict: and both claimed outputs correct  */
 
 /* ------------------------------------------------------------------ setup */
 
@@ -86,6 +97,21 @@ int ouro_vrf03_verify(unsigned char *output, const unsigned char *pk,
  * Shelley/Ledger/TPraos.hs:40).  Does not verify the proof. */
 int ouro_vrf03_proof_to_hash(unsigned char *output, const unsigned char *proof);
 
+/* The library also exports the cardano-crypto-praos names themselves, with
+ * these exact signatures, so a maintainer can satisfy PraosVRF's
+ * `foreign import ccall "crypto_vrf_ietfdraft03_verify"` (and the
+ * version-less crypto_vrf_* names, which the fork maps to draft-03) by link
+ * order instead of editing the Haskell:
+ *   int crypto_vrf_ietfdraft03_verify(unsigned char *output, const unsigned char *pk,
+ *                                     const unsigned char *proof, const unsigned char *m,
+ *                                     unsigned long long mlen);
+ *   int crypto_vrf_ietfdraft03_proof_to_hash(unsigned char *output,
+ *                                            const unsigned char *proof);
+ *   int crypto_vrf_verify(...);         same as crypto_vrf_ietfdraft03_verify
+ *   int crypto_vrf_proof_to_hash(...);  same as crypto_vrf_ietfdraft03_proof_to_hash
+ * Ed25519 is NOT exported under libsodium's name (libsodium itself is still
+ * linked for key generation); use --defsym for it if wanted. */
+
 /* Replaces SumKES.verifyKES (Sum6KES Ed25519DSIGN Blake2b_256), called via
  * SL.verifySignedKES at ouroboros-consensus-shelley/src/Ouroboros/Consensus/
  * Shelley/Ledger/Integrity.hs:27.  t = KES period relative to the opcert.
@@ -125,8 +151,25 @@ int ouro_sum6kes_verify_batch(size_t n, const uint8_t *vk /* n x 32 */,
  * reached in the reference via TPraos.updateChainDepState
  * (ouroboros-consensus-shelley/src/Ouroboros/Consensus/Shelley/Protocol.hs:433-442):
  * OCERT (Ed25519 over hotVk || BE64(counter) || BE64(kesPeriod), then Sum6KES
- * over the raw header body) and OVERLAY (the eta and leader VRFs over the
- * caller's mkSeed values).  Structure-of-arrays, one entry per header. */
+ * over the raw header body) and OVERLAY (the eta and leader VRFs over
+ * mkSeed seedEta/seedL slot eta0).  Structure-of-arrays, one entry per header.
+ *
+ * The first 16 members are required (eta_alpha / leader_alpha only when
+ * `slot` is NULL).  The last five are optional -- NULL = not used; a caller
+ * that zero-initialises the struct gets the round-1 behaviour:
+ *   eta_output / leader_output: the header's claimed certifiedOutputs (the
+ *     first element of bheaderEta / bheaderL); enables the *_CLAIM_OK bits.
+ *   slot + epoch_nonce: the VRF inputs are derived on the device exactly as
+ *     the OVERLAY rule does (Shelley/Protocol.hs:409-410, ledger-specs mkSeed):
+ *       alpha = Blake2b-256(BE64(slot) || eta0) XOR seed,
+ *       seedEta = Blake2b-256(BE64(0)), seedL = Blake2b-256(BE64(1))
+ *     (mkNonceFromNumber 0 / 1); epoch_nonce = NULL is NeutralNonce (nothing
+ *     appended after the slot).  eta_alpha / leader_alpha are then ignored.
+ *     One eta0 per call: a window that crosses an epoch boundary is split.
+ *   eta_nonce (OUTPUT, n x 32): mkNonceFromOutputVRF of the eta output the
+ *     nonce update consumes = Blake2b-256(claimed eta output) when
+ *     eta_output is given (the reference's choice), else of the computed
+ *     beta_eta.  ouro_nonce_fold folds these into eta_v / eta_c. */
 typedef struct ouro_tpraos_batch {
   size_t n;
   const uint8_t *issuer_vk;        /* n x 32  bheaderVk (cold key)            */
@@ -144,12 +187,32 @@ typedef struct ouro_tpraos_batch {
   const uint8_t *body;             /* concatenated raw header-body CBOR       */
   const uint64_t *body_off;        /* n                                       */
   const uint32_t *body_len;        /* n                                       */
+  /* optional (NULL = not used) */
+  const uint8_t *eta_output;       /* n x 64  claimed certifiedOutput (eta)   */
+  const uint8_t *leader_output;    /* n x 64  claimed certifiedOutput (leader)*/
+  const uint64_t *slot;            /* n       bheaderSlotNo: seeds on device  */
+  const uint8_t *epoch_nonce;      /* 32      eta0 (NULL: NeutralNonce)       */
+  uint8_t *eta_nonce;              /* n x 32  OUT: Blake2b-256(eta output)    */
 } ouro_tpraos_batch;
 
 /* verdict[i] = OURO_HDR_* bits; beta_eta / beta_leader (n x 64, may be NULL)
  * receive the computed VRF outputs (zeros where a proof fails). */
 int ouro_tpraos_verify_batch(const ouro_tpraos_batch *b, uint8_t *verdict,
                              uint8_t *beta_eta, uint8_t *beta_leader);
+
+/* The host-side UPDN fold (ledger-specs; the per-header step of
+ * SL.updateChainDepState after the crypto): for i = 0..n-1
+ *   eta_v <- eta_v (*) eta_nonce[i]
+ *   eta_c <- eta_v            if slot[i] + stability_window < first_slot_next_epoch
+ *            (unchanged)      otherwise
+ * with a (*) b = Blake2b-256(a || b) (Nonce composition; the 32-byte values are
+ * Nonce hashes).  The caller stops at the first invalid header itself (pass
+ * n = that index).  eta_v / eta_c are updated in place (32 B each);
+ * is_neutral[0..1] (may be NULL) say eta_v / eta_c start as NeutralNonce and
+ * receive whether they still are.  Host-only, no device.  Returns OURO_OK. */
+int ouro_nonce_fold(size_t n, const uint8_t *eta_nonce, const uint64_t *slot,
+                    uint64_t first_slot_next_epoch, uint64_t stability_window,
+                    uint8_t *eta_v, uint8_t *eta_c, int *is_neutral);
 
 /* Latency-oriented variant for small batches (ChainSync windows of up to 300
  * pipelined headers, ouroboros-network/src/Ouroboros/Network/NodeToNode.hs:197-200):
@@ -160,13 +223,13 @@ int ouro_tpraos_verify_batch_lowlat(const ouro_tpraos_batch *b, uint8_t *verdict
 
 /* One process, several GPUs: the batch is cut into
  * contiguous shards, shard k verified on devices[k] (devices = NULL: every
- * visible device) by a persistent per-shard worker thread with its own
- * streams and pinned staging -- the pipelined path of ouro_tpraos_verify_batch
- * -- writing straight into the caller's buffers (no collective is needed
- * inside one process).  A device may be listed more than once (two pipelines
- * on one GPU).  Calls are serialised process-wide; the first shard error is
- * returned after every shard has finished.  Same results as
- * ouro_tpraos_verify_batch. */
+ * visible device) by a persistent worker thread -- one per (device, k-th
+ * listing of that device) -- with its own streams and pinned staging (the
+ * pipelined path of ouro_tpraos_verify_batch), writing straight into the
+ * caller's buffers (no collective is needed inside one process).  A device
+ * may be listed more than once (two pipelines on one GPU).  Calls are
+ * serialised process-wide; the first shard error is returned after every
+ * shard has finished.  Same results as ouro_tpraos_verify_batch. */
 int ouro_device_count(void);
 int ouro_tpraos_verify_batch_multi(const ouro_tpraos_batch *b, const int *devices, int ndev,
                                    uint8_t *verdict, uint8_t *beta_eta, uint8_t *beta_leader);

@@ -90,6 +90,12 @@ typedef struct orc_tpraos_batch {
   const uint8_t *body;        /* concatenated header-body CBOR              */
   const uint64_t *body_off;   /* n                                          */
   const uint32_t *body_len;   /* n                                          */
+  /* optional (NULL = not used), as include/ouro_verify.h */
+  const uint8_t *eta_output;  /* n x 64  claimed certifiedOutput (eta)      */
+  const uint8_t *leader_output; /* n x 64 claimed certifiedOutput (leader)  */
+  const uint64_t *slot;       /* n  -> alphas = mkSeed seedEta/seedL slot eta0 */
+  const uint8_t *epoch_nonce; /* 32  eta0 (NULL: NeutralNonce)              */
+  uint8_t *eta_nonce;         /* n x 32 OUT  mkNonceFromOutputVRF           */
 } orc_tpraos_batch;
 
 #define ORC_HDR_OCERT_OK 1u
@@ -97,6 +103,16 @@ typedef struct orc_tpraos_batch {
 #define ORC_HDR_VRF_ETA_OK 4u
 #define ORC_HDR_VRF_LEADER_OK 8u
 #define ORC_HDR_ALL_OK 15u
+#define ORC_HDR_ETA_CLAIM_OK 16u
+#define ORC_HDR_LEADER_CLAIM_OK 32u
+
+/* ledger-specs mkNonceFromNumber: Blake2b-256(BE64(k)) (a Nonce hash) */
+void orc_mk_nonce_from_number(uint8_t out[32], uint64_t k);
+/* ledger-specs mkSeed ucNonce slot eta0 (called at
+ * ouroboros-consensus-shelley/src/Ouroboros/Consensus/Shelley/Protocol.hs:409-410):
+ * Blake2b-256(BE64(slot) || eta0) XOR ucNonce; eta0 = NULL is NeutralNonce
+ * (nothing appended); uc = NULL is a NeutralNonce ucNonce (no XOR). */
+void orc_mk_seed(uint8_t out[32], const uint8_t *uc, uint64_t slot, const uint8_t *eta0);
 
 void orc_tpraos_verify_one(const orc_tpraos_batch *b, size_t i, uint8_t *verdict,
                            uint8_t beta_eta[64], uint8_t beta_leader[64]);

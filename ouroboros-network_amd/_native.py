@@ -24,7 +24,10 @@ HDR_OCERT_OK = 0x01
 HDR_KES_OK = 0x02
 HDR_VRF_ETA_OK = 0x04
 HDR_VRF_LEADER_OK = 0x08
-HDR_ALL_OK = 0x0F
+HDR_ETA_CLAIM_OK = 0x10
+HDR_LEADER_CLAIM_OK = 0x20
+HDR_ALL_OK = 0x0F      # ref2020: every proof and signature valid
+HDR_STRICT_OK = 0x3F   # strict: and both claimed outputs equal the computed ones
 
 LEADER_NO = 0
 LEADER_YES = 1
@@ -59,6 +62,12 @@ class TPraosBatch(ctypes.Structure):
         ("body", ctypes.c_void_p),
         ("body_off", ctypes.c_void_p),
         ("body_len", ctypes.c_void_p),
+        # optional (NULL = not used)
+        ("eta_output", ctypes.c_void_p),
+        ("leader_output", ctypes.c_void_p),
+        ("slot", ctypes.c_void_p),
+        ("epoch_nonce", ctypes.c_void_p),
+        ("eta_nonce", ctypes.c_void_p),
     ]
 
 
@@ -96,6 +105,15 @@ SIGNATURES = {
     "ouro_leader_check_batch": (_I, [_SZ, _P, _P, _P, ctypes.c_int64, ctypes.c_uint64, _I, _P]),
     "ouro_leader_check_batch_device": (_I, [_P, _SZ, _P, _P, _P, ctypes.c_int64, ctypes.c_uint64,
                                             _I, _P]),
+    "ouro_nonce_fold": (_I, [_SZ, _P, _P, ctypes.c_uint64, ctypes.c_uint64, _P, _P, _P]),
+}
+
+# the cardano-crypto-praos names the library also exports (include/ouro_verify.h)
+VRF_ALIASES = {
+    "crypto_vrf_ietfdraft03_verify": (_I, [_P, _P, _P, _P, _ULL]),
+    "crypto_vrf_ietfdraft03_proof_to_hash": (_I, [_P, _P]),
+    "crypto_vrf_verify": (_I, [_P, _P, _P, _P, _ULL]),
+    "crypto_vrf_proof_to_hash": (_I, [_P, _P]),
 }
 
 _lib = None
@@ -116,7 +134,7 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
             lib = ctypes.CDLL(path)
         except OSError as e:  # pragma: no cover - depends on the image
             raise NativeUnavailable(f"cannot load {path}: {e}") from e
-        for name, (res, args) in SIGNATURES.items():
+        for name, (res, args) in list(SIGNATURES.items()) + list(VRF_ALIASES.items()):
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args

@@ -24,8 +24,11 @@ constexpr uint8_t kB2bSigma[12][16] = {
 
 OURO_FI uint64_t b2b_rotr(uint64_t x, int n) { return (x >> n) | (x << (64 - n)); }
 
-// out = Blake2b-256(in), in = 16 little-endian 32-bit words (64 bytes)
-OURO_FI void blake2b256_64(uint32_t out[8], const uint32_t in[16]) {
+// out = Blake2b-256 of the first `len` <= 64 bytes of in (16 little-endian
+// 32-bit words; bytes past len must be zero).  One final compression with
+// counter t = len: the KES Merkle pairs (64 B), mkSeed's BE64(slot) || eta0
+// (40 B, or 8 B for NeutralNonce), mkNonceFromOutputVRF (64 B).
+OURO_FI void blake2b256_short(uint32_t out[8], const uint32_t in[16], uint32_t len) {
   const uint64_t IV[8] = {0x6a09e667f3bcc908ULL, 0xbb67ae8584caa73bULL, 0x3c6ef372fe94f82bULL,
                           0xa54ff53a5f1d36f1ULL, 0x510e527fade682d1ULL, 0x9b05688c2b3e6c1fULL,
                           0x1f83d9abfb41bd6bULL, 0x5be0cd19137e2179ULL};
@@ -44,7 +47,7 @@ OURO_FI void blake2b256_64(uint32_t out[8], const uint32_t in[16]) {
     v[i] = h[i];
     v[i + 8] = IV[i];
   }
-  v[12] ^= 64;    // t0 = bytes hashed
+  v[12] ^= len;   // t0 = bytes hashed
   v[14] = ~v[14]; // final block
 #define OURO_B2G(a, b, c, d, x, y)                     \
   v[a] = v[a] + v[b] + (x);                            \
@@ -74,6 +77,41 @@ OURO_FI void blake2b256_64(uint32_t out[8], const uint32_t in[16]) {
     out[2 * i] = (uint32_t)x;
     out[2 * i + 1] = (uint32_t)(x >> 32);
   }
+}
+
+OURO_FI void blake2b256_64(uint32_t out[8], const uint32_t in[16]) { blake2b256_short(out, in, 64); }
+
+// ---- mkSeed / mkNonceFromNumber ----------------------
+// seedEta = mkNonceFromNumber 0, seedL = mkNonceFromNumber 1, i.e.
+// Blake2b-256(BE64(0 / 1)) as little-endian words.  Pinned by
+// tests/test_nonce.py: seedL against the Nonce values of the reference's golden
+// ChainDepState (ouroboros-consensus-shelley-test/test/golden/disk/ChainDepState,
+// built from SL.mkNonceFromNumber 1 at Examples.hs:531-537), both against the
+// device routine below compiled for the host.
+constexpr uint32_t kSeedEta[8] = {0x197ae481u, 0x0a9bb2e6u, 0x1759b965u, 0x4351ce62u,
+                                  0x26d030edu, 0xa3245d1eu, 0x50521720u, 0x5cf1206bu};
+constexpr uint32_t kSeedL[8] = {0x6a0add12u, 0x2a220e7du, 0xa06d9297u, 0x775adb3au,
+                                0xc71cd368u, 0x68bdc2c5u, 0x7d4ae128u, 0x603afa25u};
+
+OURO_FI uint32_t bswap32_b2(uint32_t x) {
+  return (x >> 24) | ((x >> 8) & 0xff00u) | ((x << 8) & 0xff0000u) | (x << 24);
+}
+
+// The hash half of ledger-specs mkSeed (called at
+// ouroboros-consensus-shelley/src/Ouroboros/Consensus/Shelley/Protocol.hs:409-410):
+// Blake2b-256(BE64(slot) || eta0), eta0 = 8 words or NULL (NeutralNonce: the
+// slot bytes alone).  The caller XORs seedEta / seedL.
+OURO_FI void mkseed_hash(uint32_t out[8], uint64_t slot, const uint32_t* eta0) {
+  uint32_t in[16];
+#pragma unroll
+  for (int i = 0; i < 16; i++) in[i] = 0;
+  in[0] = bswap32_b2((uint32_t)(slot >> 32));
+  in[1] = bswap32_b2((uint32_t)slot);
+  if (eta0) {
+#pragma unroll
+    for (int i = 0; i < 8; i++) in[2 + i] = eta0[i];
+  }
+  blake2b256_short(out, in, eta0 ? 40u : 8u);
 }
 
 }  // namespace ouro

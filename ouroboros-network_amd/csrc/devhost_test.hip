@@ -210,6 +210,19 @@ int dh_sum6kes_verify(const uint8_t* vk, uint32_t t, const uint8_t* m, uint32_t 
   Lane lane;
   return sum6kes_verify_lane(v, t, sw, ShaGlobalTail{m}, mlen, lane.w, host_btab()) ? 0 : -1;
 }
+// mkSeed through the header kernels' own path (tpraos.h hdr_seed: blake2b.h
+// mkseed_hash and the seedEta / seedL constants); eta0 = NULL: NeutralNonce.
+void dh_mk_seed(uint8_t* out, int leader, uint64_t slot, const uint8_t* eta0) {
+  alignas(16) uint8_t e0[32];
+  if (eta0) memcpy(e0, eta0, 32);
+  ouro_tpraos_batch b{};
+  b.n = 1;
+  b.slot = &slot;
+  b.epoch_nonce = eta0 ? e0 : nullptr;
+  SeedMsg a;
+  hdr_seed(a, b, 0, leader != 0, batch_opts(b));
+  memcpy(out, a.w, 32);
+}
 // The header drivers of tpraos.h for every header of a host SoA batch.
 // mode 0 = throughput (one lane, key table shared), 1 = latency (a fresh lane
 // per core, no sharing), 2 = latency on lane quads (the four products of each
@@ -220,18 +233,19 @@ int dh_tpraos_verify(const ouro_tpraos_batch* b, int mode, uint8_t* verdict, uin
   std::vector<Lane> lanes(kLatCores);
   std::vector<int32_t> res(kLatResWords + 4);
   int32_t* r = reinterpret_cast<int32_t*>((reinterpret_cast<uintptr_t>(res.data()) + 15) & ~uintptr_t(15));
+  const uint32_t opts = batch_opts(*b);
   for (size_t i = 0; i < b->n; i++) {
     memset(r, 0, kLatResWords * sizeof(int32_t));
     const int cores = mode ? kLatCores : kHdrCores;
     for (int core = 0; core < cores; core++)
-      hdr_core(*b, i, core, lanes[mode ? core : 0].w, r, host_btab(), mode == 0, mode != 0,
+      hdr_core(*b, i, opts, core, lanes[mode ? core : 0].w, r, host_btab(), mode == 0, mode != 0,
                mode == 2);
     if (mode == 2) {
-      hdr_finish_item_split(*b, i, r, verdict, beta_eta, beta_leader);
+      hdr_finish_item_split(*b, i, opts, r, verdict, beta_eta, beta_leader);
       continue;
     }
     if (mode) hdr_combine_split(r);
-    hdr_finish_item(*b, i, r, lanes[0].w, verdict, beta_eta, beta_leader);
+    hdr_finish_item(*b, i, opts, r, lanes[0].w, verdict, beta_eta, beta_leader);
   }
   return 0;
 }

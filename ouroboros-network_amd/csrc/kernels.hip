@@ -32,18 +32,6 @@ constexpr int kBlock = 256;
 constexpr int kHdrLaneWords = kLaneWords + kResWords;
 constexpr int kLatBlock = 64;  // default latency-mode workgroup (lat_block(); A/B: tools/ab_latency.py)
 
-// message bytes held in registers (the 48-byte OCertSignable); a select chain
-// keeps a dynamic byte index out of scratch
-struct RegTail48 {
-  uint32_t w[12];
-  OURO_FI uint32_t tail(uint32_t q) const {
-    uint32_t r = w[0];
-#pragma unroll
-    for (int i = 1; i < 12; i++) r = ((q >> 2) == (uint32_t)i) ? w[i] : r;
-    return (r >> (8 * (q & 3))) & 0xffu;
-  }
-};
-
 __device__ __forceinline__ void load_words(uint32_t* w, const uint8_t* p, int nwords16) {
   const uint4* q = reinterpret_cast<const uint4*>(p);
 #pragma unroll
@@ -127,9 +115,10 @@ __global__ void __launch_bounds__(kBlock, OURO_WAVES) k_sum6kes_verify(
 #if OURO_HDR_FINISH_NI
 // A/B: the finish (inversion, encodings, hashes) with its own register allocation
 __device__ __noinline__ void hdr_finish_item_ni(const ouro_tpraos_batch& b, size_t i,
-                                                const int32_t* res, int32_t* tmp, uint8_t* verdict,
-                                                uint8_t* beta_eta, uint8_t* beta_leader) {
-  hdr_finish_item(b, i, res, tmp, verdict, beta_eta, beta_leader);
+                                                uint32_t opts, const int32_t* res, int32_t* tmp,
+                                                uint8_t* verdict, uint8_t* beta_eta,
+                                                uint8_t* beta_leader) {
+  hdr_finish_item(b, i, opts, res, tmp, verdict, beta_eta, beta_leader);
 }
 #endif
 
@@ -145,23 +134,24 @@ __global__ void __launch_bounds__(kBlock, OURO_WAVES) k_tpraos_verify(ouro_tprao
   const size_t nth = (size_t)gridDim.x * blockDim.x;
   int32_t* lane = scratch + tid * kHdrLaneWords;
   int32_t* res = lane + kLaneWords;
+  const uint32_t opts = batch_opts(b);
   for (size_t i = tid; i < b.n; i += nth) {
 #if OURO_HDR_LOOP
     // A/B: one copy of the core dispatch, the core chosen at run time
 #pragma unroll 1
-    for (int c = kCoreOcert; c <= kCoreVl; c++) hdr_core(b, i, c, lane, res, btab);
+    for (int c = kCoreOcert; c <= kCoreVl; c++) hdr_core(b, i, opts, c, lane, res, btab);
 #else
-    hdr_core(b, i, kCoreOcert, lane, res, btab);
-    hdr_core(b, i, kCoreKes, lane, res, btab);
-    hdr_core(b, i, kCoreUe, lane, res, btab);
-    hdr_core(b, i, kCoreUl, lane, res, btab);
-    hdr_core(b, i, kCoreVe, lane, res, btab);
-    hdr_core(b, i, kCoreVl, lane, res, btab);
+    hdr_core(b, i, opts, kCoreOcert, lane, res, btab);
+    hdr_core(b, i, opts, kCoreKes, lane, res, btab);
+    hdr_core(b, i, opts, kCoreUe, lane, res, btab);
+    hdr_core(b, i, opts, kCoreUl, lane, res, btab);
+    hdr_core(b, i, opts, kCoreVe, lane, res, btab);
+    hdr_core(b, i, opts, kCoreVl, lane, res, btab);
 #endif
 #if OURO_HDR_FINISH_NI
-    hdr_finish_item_ni(b, i, res, lane, verdict, beta_eta, beta_leader);
+    hdr_finish_item_ni(b, i, opts, res, lane, verdict, beta_eta, beta_leader);
 #else
-    hdr_finish_item(b, i, res, lane, verdict, beta_eta, beta_leader);
+    hdr_finish_item(b, i, opts, res, lane, verdict, beta_eta, beta_leader);
 #endif
   }
 }
@@ -170,14 +160,16 @@ __global__ void __launch_bounds__(kBlock, OURO_WAVES) k_tpraos_verify(ouro_tprao
 // so each wave runs one core type), results to a per-header record.
 // quad = 1: each work item runs on the four lanes of a DPP quad, which share
 // its scratch slot and split every group operation's products (ge25519.h);
-// quad = 0: one lane per item.  n is read from device memory so a captured
-// graph serves any n <= capacity.
+// quad = 0: one lane per item.  n (d_n[0]) and the batch's optional members
+// (d_n[1], tpraos.h kOpt*) are read from device memory so a captured graph
+// serves any batch of n <= capacity.
 __global__ void __launch_bounds__(kBlock, OURO_WAVES) k_tpraos_cores(ouro_tpraos_batch b,
                                                             const uint32_t* __restrict__ d_n,
                                                             int32_t* res_buf, int32_t* scratch,
                                                             const int32_t* __restrict__ btab,
                                                             int quad) {
-  const size_t n = *d_n;
+  const size_t n = d_n[0];
+  const uint32_t opts = d_n[1];
   const int sh = quad ? 2 : 0;
   const size_t tid = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) >> sh;
   const size_t nth = ((size_t)gridDim.x * blockDim.x) >> sh;
@@ -185,7 +177,7 @@ __global__ void __launch_bounds__(kBlock, OURO_WAVES) k_tpraos_cores(ouro_tpraos
   for (size_t w = tid; w < (size_t)kLatCores * n; w += nth) {
     const int core = (int)(w / n);
     const size_t i = w - (size_t)core * n;
-    hdr_core(b, i, core, lane, res_buf + i * kLatResWords, btab, /*share_key=*/false,
+    hdr_core(b, i, opts, core, lane, res_buf + i * kLatResWords, btab, /*share_key=*/false,
              /*split=*/true, quad != 0);
   }
 }
@@ -201,7 +193,8 @@ __global__ void __launch_bounds__(kBlock, OURO_WAVES) k_tpraos_finish(ouro_tprao
                                                              uint8_t* __restrict__ beta_eta,
                                                              uint8_t* __restrict__ beta_leader,
                                                              int32_t* scratch, int quad) {
-  const size_t n = *d_n;
+  const size_t n = d_n[0];
+  const uint32_t opts = d_n[1];
   const int sh = quad ? 2 : 0;
   const size_t tid = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) >> sh;
   const size_t nth = ((size_t)gridDim.x * blockDim.x) >> sh;
@@ -211,14 +204,16 @@ __global__ void __launch_bounds__(kBlock, OURO_WAVES) k_tpraos_finish(ouro_tprao
     int32_t* res = res_buf + i * kLatResWords;
     if (!quad) {
       hdr_combine_split(res);
-      hdr_finish_item(b, i, res, lane, verdict, beta_eta, beta_leader);
+      hdr_finish_item(b, i, opts, res, lane, verdict, beta_eta, beta_leader);
       continue;
     }
     const int which = (int)(q >> 1);
     uint32_t pi[20], beta[16];
     load_words(pi, (which ? b.leader_proof : b.eta_proof) + 80 * i, 5);
-    const uint32_t bit = vrf_finish_split(res, which, pi, beta);
-    // quad position 0 takes position 2's (the leader VRF's) bit
+    uint32_t bit = vrf_finish_split(res, which, pi, beta);
+    bit |= hdr_claim_bit(b, i, opts, which, bit != 0, beta);
+    if (q == 0) hdr_eta_nonce(b, i, opts, beta);
+    // quad position 0 takes position 2's (the leader VRF's) bits
     const uint32_t other = (uint32_t)__builtin_amdgcn_mov_dpp((int)bit, 0x0a, 0xf, 0xf, true);
     uint8_t* dst = which ? beta_leader : beta_eta;
     if ((q & 1u) == 0 && dst) store_words(dst + 64 * i, beta, 4);
@@ -365,21 +360,29 @@ int device_state(DeviceState** out) {
   return OURO_OK;
 }
 
-// per-thread stream + growable device buffers
+// Per-thread, per-DEVICE stream and growable device buffers: a buffer
+// allocated on one GPU is never handed to a launch on another, whatever the
+// order of ouro_set_device calls or of a multi-GPU call's device list.
 struct Buf {
   void* p = nullptr;
   size_t cap = 0;
 };
 struct ThreadCtx {
-  int dev = -1;
   hipStream_t stream = nullptr;
   std::map<hipStream_t, Buf> scratch;  // per stream: concurrent launches never share slots
-  Buf in[32];  // staging slots; the header batch uses 18
-  ~ThreadCtx() {
-    // process teardown: the runtime may already be gone; leak rather than fault
-  }
+  Buf in[32];  // staging slots; a header batch uses up to 24
 };
-thread_local ThreadCtx t_ctx;
+// process teardown: the runtime may already be gone; the contexts leak rather
+// than free into it
+thread_local std::map<int, ThreadCtx>* t_ctx = nullptr;
+
+// the calling thread's context on device `dev`
+ThreadCtx& ctx_of(int dev) {
+  if (!t_ctx) t_ctx = new std::map<int, ThreadCtx>;
+  return (*t_ctx)[dev];
+}
+// ... on its current device (valid after current_device())
+ThreadCtx& ctx() { return ctx_of(t_device); }
 
 int ensure(Buf& b, size_t bytes) {
   if (b.cap >= bytes) return OURO_OK;
@@ -396,11 +399,9 @@ int thread_stream(hipStream_t* s) {
   int dev;
   int rc = current_device(&dev);
   if (rc) return rc;
-  if (t_ctx.stream == nullptr || t_ctx.dev != dev) {
-    OURO_HIP(hipStreamCreateWithFlags(&t_ctx.stream, hipStreamNonBlocking));
-    t_ctx.dev = dev;
-  }
-  *s = t_ctx.stream;
+  ThreadCtx& c = ctx_of(dev);
+  if (c.stream == nullptr) OURO_HIP(hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking));
+  *s = c.stream;
   return OURO_OK;
 }
 
@@ -411,7 +412,7 @@ int plan(DeviceState* ds, int id, size_t n, hipStream_t stream, int* grid, int32
   blocks = std::max<size_t>(1, std::min<size_t>(blocks, (size_t)ds->max_blocks[id]));
   *grid = (int)blocks;
   if (scratch) {
-    Buf& b = t_ctx.scratch[stream];
+    Buf& b = ctx().scratch[stream];
     int rc = ensure(b, blocks * kBlock * sizeof(int32_t) * lane_words);
     if (rc) return rc;
     *scratch = static_cast<int32_t*>(b.p);
@@ -512,7 +513,7 @@ int lat_quad() {
 }
 
 // latency mode: eight cores per header (x4 lanes in quad mode), then the
-// finish; n read from d_n.
+// finish; n and the option bits read from d_n[0..1].
 // Lanes used <= the kBlock-rounded count lowlat_scratch_words provides for.
 int launch_lowlat(hipStream_t st, const ouro_tpraos_batch& b, const uint32_t* d_n, size_t n_cap,
                   int32_t* res_buf, int32_t* scratch, uint8_t* verdict, uint8_t* be,
@@ -549,33 +550,61 @@ struct Stager {
   hipStream_t st;
   int slot = 0;
   int rc = OURO_OK;
-  Buf* bufs = t_ctx.in;  // device buffers, one per up()/out() call
+  Buf* bufs = ctx().in;  // device buffers, one per up()/out() call
+  int nbufs = 32;
+  Buf* next() {
+    if (slot >= nbufs) {
+      rc = fail(OURO_EDEVICE, "staging slots exhausted");
+      return nullptr;
+    }
+    return &bufs[slot++];
+  }
   template <class T>
   T* up(const T* host, size_t count) {
     if (rc) return nullptr;
     const size_t bytes = std::max<size_t>(count * sizeof(T), 16);
-    Buf& b = bufs[slot++];
-    if ((rc = ensure(b, bytes))) return nullptr;
+    Buf* b = next();
+    if (!b || (rc = ensure(*b, bytes))) return nullptr;
     if (count) {
-      hipError_t e = hipMemcpyAsync(b.p, host, count * sizeof(T), hipMemcpyHostToDevice, st);
+      hipError_t e = hipMemcpyAsync(b->p, host, count * sizeof(T), hipMemcpyHostToDevice, st);
       if (e != hipSuccess) rc = fail(OURO_EDEVICE, std::string("H2D: ") + hipGetErrorString(e));
     }
-    return static_cast<T*>(b.p);
+    return static_cast<T*>(b->p);
   }
   template <class T>
   T* out(size_t count) {
     if (rc) return nullptr;
-    Buf& b = bufs[slot++];
-    if ((rc = ensure(b, std::max<size_t>(count * sizeof(T), 16)))) return nullptr;
-    return static_cast<T*>(b.p);
+    Buf* b = next();
+    if (!b || (rc = ensure(*b, std::max<size_t>(count * sizeof(T), 16)))) return nullptr;
+    return static_cast<T*>(b->p);
   }
 };
 
-// total bytes addressed by (off, len) pairs
-size_t span_of(size_t n, const uint64_t* off, const uint32_t* len) {
-  size_t hi = 0;
-  for (size_t i = 0; i < n; i++) hi = std::max<size_t>(hi, off[i] + len[i]);
-  return hi;
+// The bytes a batch addresses by (offset, length) pairs: the window
+// [lo, hi) over the items with length > 0, and the offsets rebased to lo, so
+// only that window is uploaded (a slice or shard of a larger batch with
+// absolute offsets does not drag the bytes before it along).  EINVAL when an
+// offset + length overflows.
+struct Window {
+  uint64_t lo = 0, hi = 0;
+  std::vector<uint64_t> off;  // rebased; alive until the upload has completed
+  size_t span() const { return (size_t)(hi - lo); }
+};
+int window_of(size_t n, const uint64_t* off, const uint32_t* len, Window* w) {
+  uint64_t lo = ~0ull, hi = 0;
+  for (size_t i = 0; i < n; i++) {
+    if (!len[i]) continue;
+    const uint64_t e = off[i] + len[i];
+    if (e < off[i]) return fail(OURO_EINVAL, "offset + length overflows");
+    lo = std::min(lo, off[i]);
+    hi = std::max(hi, e);
+  }
+  if (hi == 0) lo = 0;
+  w->lo = lo;
+  w->hi = hi;
+  w->off.resize(n);
+  for (size_t i = 0; i < n; i++) w->off[i] = len[i] ? off[i] - lo : 0;
+  return OURO_OK;
 }
 
 int finish(hipStream_t st) {
@@ -587,6 +616,63 @@ int download(hipStream_t st, void* host, const void* dev, size_t bytes) {
   if (!host || !bytes) return OURO_OK;
   OURO_HIP(hipMemcpyAsync(host, dev, bytes, hipMemcpyDeviceToHost, st));
   return OURO_OK;
+}
+
+// ---- header batches ----
+// The required members present?  (The alphas only when the batch has no slots.)
+int check_hdr_batch(const ouro_tpraos_batch* b) {
+  if (!b->issuer_vk || !b->vrf_vk || !b->eta_proof || !b->leader_proof || !b->hot_vk ||
+      !b->ocert_counter || !b->ocert_kes_period || !b->ocert_sigma || !b->kes_t || !b->kes_sig ||
+      !b->body_off || !b->body_len)
+    return fail(OURO_EINVAL, "null argument");
+  if (!b->slot && (!b->eta_alpha || !b->leader_alpha))
+    return fail(OURO_EINVAL, "null alpha (and no slots to derive it from)");
+  return OURO_OK;
+}
+
+// rows [lo, lo + m) of a host batch on the device: `d` points at the copies
+// (optional members only when given), ver/be/bl/nonce at the result buffers
+struct StagedHdr {
+  ouro_tpraos_batch d{};
+  uint8_t *ver = nullptr, *be = nullptr, *bl = nullptr, *nonce = nullptr;
+  Window body;
+};
+
+int stage_hdr(Stager& sg, const ouro_tpraos_batch* b, size_t lo, size_t m, StagedHdr* s) {
+  int rc = window_of(m, b->body_off + lo, b->body_len + lo, &s->body);
+  if (rc) return rc;
+  const size_t span = s->body.span();
+  if (span && !b->body) return fail(OURO_EINVAL, "null body buffer");
+  ouro_tpraos_batch& d = s->d;
+  d = ouro_tpraos_batch{};
+  d.n = m;
+  d.issuer_vk = sg.up(b->issuer_vk + 32 * lo, 32 * m);
+  d.vrf_vk = sg.up(b->vrf_vk + 32 * lo, 32 * m);
+  d.eta_proof = sg.up(b->eta_proof + 80 * lo, 80 * m);
+  d.leader_proof = sg.up(b->leader_proof + 80 * lo, 80 * m);
+  if (b->slot) {
+    d.slot = sg.up(b->slot + lo, m);
+    if (b->epoch_nonce) d.epoch_nonce = sg.up(b->epoch_nonce, 32);
+  } else {
+    d.eta_alpha = sg.up(b->eta_alpha + 32 * lo, 32 * m);
+    d.leader_alpha = sg.up(b->leader_alpha + 32 * lo, 32 * m);
+  }
+  d.hot_vk = sg.up(b->hot_vk + 32 * lo, 32 * m);
+  d.ocert_counter = sg.up(b->ocert_counter + lo, m);
+  d.ocert_kes_period = sg.up(b->ocert_kes_period + lo, m);
+  d.ocert_sigma = sg.up(b->ocert_sigma + 64 * lo, 64 * m);
+  d.kes_t = sg.up(b->kes_t + lo, m);
+  d.kes_sig = sg.up(b->kes_sig + 448 * lo, 448 * m);
+  d.body = sg.up(span ? b->body + s->body.lo : b->body, span);
+  d.body_off = sg.up(s->body.off.data(), m);
+  d.body_len = sg.up(b->body_len + lo, m);
+  if (b->eta_output) d.eta_output = sg.up(b->eta_output + 64 * lo, 64 * m);
+  if (b->leader_output) d.leader_output = sg.up(b->leader_output + 64 * lo, 64 * m);
+  s->ver = sg.out<uint8_t>(m);
+  s->be = sg.out<uint8_t>(64 * m);
+  s->bl = sg.out<uint8_t>(64 * m);
+  if (b->eta_nonce) d.eta_nonce = s->nonce = sg.out<uint8_t>(32 * m);
+  return sg.rc;
 }
 
 }  // namespace
@@ -615,13 +701,14 @@ int ed_batch_host(size_t n, const uint8_t* pk, const uint8_t* sig, const uint8_t
   hipStream_t st;
   int rc = thread_stream(&st);
   if (rc) return rc;
-  const size_t span = span_of(n, msg_off, msg_len);
-  if (span && !msg) return fail(OURO_EINVAL, "null message buffer");
+  Window w;
+  if ((rc = window_of(n, msg_off, msg_len, &w))) return rc;
+  if (w.span() && !msg) return fail(OURO_EINVAL, "null message buffer");
   Stager sg{st};
   auto dpk = sg.up(pk, 32 * n);
   auto dsig = sg.up(sig, 64 * n);
-  auto dmsg = sg.up(msg, span);
-  auto doff = sg.up(msg_off, n);
+  auto dmsg = sg.up(w.span() ? msg + w.lo : msg, w.span());
+  auto doff = sg.up(w.off.data(), n);
   auto dlen = sg.up(msg_len, n);
   auto dver = sg.out<uint8_t>(n);
   if (sg.rc) return sg.rc;
@@ -655,13 +742,14 @@ int ouro_vrf03_verify_batch(size_t n, const uint8_t* pk, const uint8_t* proof, c
   hipStream_t st;
   int rc = thread_stream(&st);
   if (rc) return rc;
-  const size_t span = span_of(n, alpha_off, alpha_len);
-  if (span && !alpha) return fail(OURO_EINVAL, "null alpha buffer");
+  Window w;
+  if ((rc = window_of(n, alpha_off, alpha_len, &w))) return rc;
+  if (w.span() && !alpha) return fail(OURO_EINVAL, "null alpha buffer");
   Stager sg{st};
   auto dpk = sg.up(pk, 32 * n);
   auto dpi = sg.up(proof, 80 * n);
-  auto dal = sg.up(alpha, span);
-  auto doff = sg.up(alpha_off, n);
+  auto dal = sg.up(w.span() ? alpha + w.lo : alpha, w.span());
+  auto doff = sg.up(w.off.data(), n);
   auto dlen = sg.up(alpha_len, n);
   auto dbeta = sg.out<uint8_t>(64 * n);
   auto dver = sg.out<uint8_t>(n);
@@ -684,13 +772,14 @@ int ouro_sum6kes_verify_batch(size_t n, const uint8_t* vk, const uint32_t* t, co
   hipStream_t st;
   int rc = thread_stream(&st);
   if (rc) return rc;
-  const size_t span = span_of(n, msg_off, msg_len);
-  if (span && !msg) return fail(OURO_EINVAL, "null message buffer");
+  Window w;
+  if ((rc = window_of(n, msg_off, msg_len, &w))) return rc;
+  if (w.span() && !msg) return fail(OURO_EINVAL, "null message buffer");
   Stager sg{st};
   auto dvk = sg.up(vk, 32 * n);
   auto dt = sg.up(t, n);
-  auto dmsg = sg.up(msg, span);
-  auto doff = sg.up(msg_off, n);
+  auto dmsg = sg.up(w.span() ? msg + w.lo : msg, w.span());
+  auto doff = sg.up(w.off.data(), n);
   auto dlen = sg.up(msg_len, n);
   auto dsig = sg.up(sig, 448 * n);
   auto dver = sg.out<uint8_t>(n);
@@ -712,89 +801,74 @@ namespace {
 // turns: while chunk c's kernel runs on one stream, the host uploads chunk
 // c + 1 on the other and copies chunk c - 1's results out, so PCIe and the
 // host copies hide behind the kernel instead of adding to it.
+constexpr size_t kOutRow = 1 + 64 + 64 + 32;  // verdict | beta_eta | beta_leader | eta_nonce
 struct PipeSlot {
   hipStream_t st = nullptr;
   hipEvent_t done = nullptr;
-  Buf in[18];
-  uint8_t* h_out = nullptr;  // pinned: verdict (m) | beta_eta (64 m) | beta_leader (64 m)
+  Buf in[28];
+  uint8_t* h_out = nullptr;  // pinned: verdict (m) | beta_eta (64 m) | beta_leader (64 m) | eta_nonce (32 m)
   size_t h_cap = 0;
-  std::vector<uint64_t> off;  // body offsets rebased to the chunk's body span
+  StagedHdr staged;  // its rebased body offsets stay alive for the async upload
   size_t lo = 0, m = 0;
   bool busy = false;
 };
 struct Pipe {
-  int dev = -1;
+  bool ready = false;
   PipeSlot s[2];
 };
-thread_local Pipe t_pipe;
+thread_local std::map<int, Pipe>* t_pipe = nullptr;  // per device, like t_ctx
 
-int pipe_slots(int dev) {
-  if (t_pipe.dev == dev) return OURO_OK;
-  for (PipeSlot& p : t_pipe.s) {
-    OURO_HIP(hipStreamCreateWithFlags(&p.st, hipStreamNonBlocking));
-    OURO_HIP(hipEventCreateWithFlags(&p.done, hipEventDisableTiming));
+int pipe_of(int dev, Pipe** out) {
+  if (!t_pipe) t_pipe = new std::map<int, Pipe>;
+  Pipe& p = (*t_pipe)[dev];
+  if (!p.ready) {
+    for (PipeSlot& q : p.s) {
+      if (!q.st) OURO_HIP(hipStreamCreateWithFlags(&q.st, hipStreamNonBlocking));
+      if (!q.done) OURO_HIP(hipEventCreateWithFlags(&q.done, hipEventDisableTiming));
+    }
+    p.ready = true;
   }
-  t_pipe.dev = dev;
+  *out = &p;
   return OURO_OK;
 }
 
-int pipe_drain(PipeSlot& p, uint8_t* verdict, uint8_t* beta_eta, uint8_t* beta_leader) {
+struct HdrOut {
+  uint8_t *verdict, *beta_eta, *beta_leader, *eta_nonce;
+};
+
+int pipe_drain(PipeSlot& p, const HdrOut& o) {
   if (!p.busy) return OURO_OK;
   p.busy = false;
   OURO_HIP(hipEventSynchronize(p.done));
-  memcpy(verdict + p.lo, p.h_out, p.m);
-  if (beta_eta) memcpy(beta_eta + 64 * p.lo, p.h_out + p.m, 64 * p.m);
-  if (beta_leader) memcpy(beta_leader + 64 * p.lo, p.h_out + 65 * p.m, 64 * p.m);
+  const size_t m = p.m;
+  memcpy(o.verdict + p.lo, p.h_out, m);
+  if (o.beta_eta) memcpy(o.beta_eta + 64 * p.lo, p.h_out + m, 64 * m);
+  if (o.beta_leader) memcpy(o.beta_leader + 64 * p.lo, p.h_out + 65 * m, 64 * m);
+  if (o.eta_nonce) memcpy(o.eta_nonce + 32 * p.lo, p.h_out + 129 * m, 32 * m);
   return OURO_OK;
 }
 
-int pipe_chunk(PipeSlot& p, const ouro_tpraos_batch* b, size_t lo, size_t m, bool be, bool bl) {
-  uint64_t blo = ~0ull, bhi = 0;
-  for (size_t i = lo; i < lo + m; i++) {
-    if (b->body_len[i] == 0) continue;
-    blo = std::min<uint64_t>(blo, b->body_off[i]);
-    bhi = std::max<uint64_t>(bhi, b->body_off[i] + b->body_len[i]);
-  }
-  if (bhi == 0) blo = 0;
-  if (bhi > blo && !b->body) return fail(OURO_EINVAL, "null body buffer");
-  p.off.resize(m);
-  for (size_t i = 0; i < m; i++)
-    p.off[i] = b->body_len[lo + i] ? b->body_off[lo + i] - blo : 0;
+int pipe_chunk(PipeSlot& p, const ouro_tpraos_batch* b, size_t lo, size_t m, const HdrOut& o) {
   Stager sg{p.st};
   sg.bufs = p.in;
-  ouro_tpraos_batch d;
-  d.n = m;
-  d.issuer_vk = sg.up(b->issuer_vk + 32 * lo, 32 * m);
-  d.vrf_vk = sg.up(b->vrf_vk + 32 * lo, 32 * m);
-  d.eta_proof = sg.up(b->eta_proof + 80 * lo, 80 * m);
-  d.leader_proof = sg.up(b->leader_proof + 80 * lo, 80 * m);
-  d.eta_alpha = sg.up(b->eta_alpha + 32 * lo, 32 * m);
-  d.leader_alpha = sg.up(b->leader_alpha + 32 * lo, 32 * m);
-  d.hot_vk = sg.up(b->hot_vk + 32 * lo, 32 * m);
-  d.ocert_counter = sg.up(b->ocert_counter + lo, m);
-  d.ocert_kes_period = sg.up(b->ocert_kes_period + lo, m);
-  d.ocert_sigma = sg.up(b->ocert_sigma + 64 * lo, 64 * m);
-  d.kes_t = sg.up(b->kes_t + lo, m);
-  d.kes_sig = sg.up(b->kes_sig + 448 * lo, 448 * m);
-  d.body = sg.up(bhi > blo ? b->body + blo : b->body, (size_t)(bhi - blo));
-  d.body_off = sg.up(p.off.data(), m);
-  d.body_len = sg.up(b->body_len + lo, m);
-  uint8_t* dver = sg.out<uint8_t>(m);
-  uint8_t* dbe = sg.out<uint8_t>(64 * m);
-  uint8_t* dbl = sg.out<uint8_t>(64 * m);
-  if (sg.rc) return sg.rc;
-  int rc = launch_hdr(p.st, d, dver, dbe, dbl);
+  sg.nbufs = (int)(sizeof(p.in) / sizeof(p.in[0]));
+  int rc = stage_hdr(sg, b, lo, m, &p.staged);
   if (rc) return rc;
-  if (p.h_cap < 129 * m) {
+  const StagedHdr& s = p.staged;
+  if ((rc = launch_hdr(p.st, s.d, s.ver, s.be, s.bl))) return rc;
+  if (p.h_cap < kOutRow * m) {
     if (p.h_out) OURO_HIP(hipHostFree(p.h_out));
     p.h_out = nullptr;
     p.h_cap = 0;
-    OURO_HIP(hipHostMalloc(reinterpret_cast<void**>(&p.h_out), 129 * m, hipHostMallocDefault));
-    p.h_cap = 129 * m;
+    OURO_HIP(hipHostMalloc(reinterpret_cast<void**>(&p.h_out), kOutRow * m, hipHostMallocDefault));
+    p.h_cap = kOutRow * m;
   }
-  OURO_HIP(hipMemcpyAsync(p.h_out, dver, m, hipMemcpyDeviceToHost, p.st));
-  if (be) OURO_HIP(hipMemcpyAsync(p.h_out + m, dbe, 64 * m, hipMemcpyDeviceToHost, p.st));
-  if (bl) OURO_HIP(hipMemcpyAsync(p.h_out + 65 * m, dbl, 64 * m, hipMemcpyDeviceToHost, p.st));
+  OURO_HIP(hipMemcpyAsync(p.h_out, s.ver, m, hipMemcpyDeviceToHost, p.st));
+  if (o.beta_eta) OURO_HIP(hipMemcpyAsync(p.h_out + m, s.be, 64 * m, hipMemcpyDeviceToHost, p.st));
+  if (o.beta_leader)
+    OURO_HIP(hipMemcpyAsync(p.h_out + 65 * m, s.bl, 64 * m, hipMemcpyDeviceToHost, p.st));
+  if (o.eta_nonce)
+    OURO_HIP(hipMemcpyAsync(p.h_out + 129 * m, s.nonce, 32 * m, hipMemcpyDeviceToHost, p.st));
   OURO_HIP(hipEventRecord(p.done, p.st));
   p.lo = lo;
   p.m = m;
@@ -809,30 +883,65 @@ size_t host_chunk(DeviceState* ds) {
   return (size_t)ds->max_blocks[kHdr] * kBlock;
 }
 
-int hdr_batch_pipelined(const ouro_tpraos_batch* b, size_t chunk, uint8_t* verdict,
-                        uint8_t* beta_eta, uint8_t* beta_leader) {
+int hdr_batch_pipelined(const ouro_tpraos_batch* b, size_t chunk, const HdrOut& o) {
   int dev, rc = current_device(&dev);
   if (rc) return rc;
-  if ((rc = pipe_slots(dev))) return rc;
+  Pipe* pp;
+  if ((rc = pipe_of(dev, &pp))) return rc;
   size_t c = 0;
   for (size_t lo = 0; lo < b->n && !rc; lo += chunk, c++) {
-    PipeSlot& p = t_pipe.s[c & 1];
-    rc = pipe_drain(p, verdict, beta_eta, beta_leader);
-    if (!rc)
-      rc = pipe_chunk(p, b, lo, std::min(chunk, b->n - lo), beta_eta != nullptr,
-                      beta_leader != nullptr);
+    PipeSlot& p = pp->s[c & 1];
+    rc = pipe_drain(p, o);
+    if (!rc) rc = pipe_chunk(p, b, lo, std::min(chunk, b->n - lo), o);
   }
   // older chunk first; on an error, still wait for everything in flight
   for (int k = 0; k < 2; k++) {
-    PipeSlot& p = t_pipe.s[(c + k) & 1];
+    PipeSlot& p = pp->s[(c + k) & 1];
     if (rc) {
       (void)hipStreamSynchronize(p.st);
       p.busy = false;
     } else {
-      rc = pipe_drain(p, verdict, beta_eta, beta_leader);
+      rc = pipe_drain(p, o);
     }
   }
   return rc;
+}
+
+// one synchronous launch of the whole batch (throughput kernel, or the
+// latency-mode kernels with lowlat), results copied out after the sync
+int hdr_batch_once(const ouro_tpraos_batch* b, const HdrOut& o, bool lowlat) {
+  const size_t n = b->n;
+  hipStream_t st;
+  int rc = thread_stream(&st);
+  if (rc) return rc;
+  DeviceState* ds;
+  if ((rc = device_state(&ds))) return rc;
+  Stager sg{st};
+  StagedHdr s;
+  if ((rc = stage_hdr(sg, b, 0, n, &s))) return rc;
+  if (lowlat) {
+    const uint32_t nw[4] = {(uint32_t)n, batch_opts(s.d), 0u, 0u};
+    const uint32_t* d_n = sg.up(nw, 4);
+    int32_t* res = sg.out<int32_t>(n * kLatResWords);
+    int32_t* scr = sg.out<int32_t>(lowlat_scratch_words(ds, n));
+    if (sg.rc) return sg.rc;
+    // (nw is read by the H2D above; this frame outlives the sync below)
+    if ((rc = launch_lowlat(st, s.d, d_n, n, res, scr, s.ver, s.be, s.bl))) return rc;
+  } else if ((rc = launch_hdr(st, s.d, s.ver, s.be, s.bl))) {
+    return rc;
+  }
+  std::vector<uint8_t> tv(n), te(o.beta_eta ? 64 * n : 0), tl(o.beta_leader ? 64 * n : 0),
+      tn(o.eta_nonce ? 32 * n : 0);
+  if ((rc = download(st, tv.data(), s.ver, n))) return rc;
+  if (o.beta_eta && (rc = download(st, te.data(), s.be, 64 * n))) return rc;
+  if (o.beta_leader && (rc = download(st, tl.data(), s.bl, 64 * n))) return rc;
+  if (o.eta_nonce && (rc = download(st, tn.data(), s.nonce, 32 * n))) return rc;
+  if ((rc = finish(st))) return rc;
+  memcpy(o.verdict, tv.data(), n);
+  if (o.beta_eta) memcpy(o.beta_eta, te.data(), 64 * n);
+  if (o.beta_leader) memcpy(o.beta_leader, tl.data(), 64 * n);
+  if (o.eta_nonce) memcpy(o.eta_nonce, tn.data(), 32 * n);
+  return OURO_OK;
 }
 }  // namespace
 
@@ -841,52 +950,62 @@ extern "C" {
 int ouro_tpraos_verify_batch(const ouro_tpraos_batch* b, uint8_t* verdict, uint8_t* beta_eta,
                              uint8_t* beta_leader) {
   if (!b) return fail(OURO_EINVAL, "null batch");
-  const size_t n = b->n;
-  if (n == 0) return OURO_OK;
-  if (!b->issuer_vk || !b->vrf_vk || !b->eta_proof || !b->leader_proof || !b->eta_alpha ||
-      !b->leader_alpha || !b->hot_vk || !b->ocert_counter || !b->ocert_kes_period ||
-      !b->ocert_sigma || !b->kes_t || !b->kes_sig || !b->body_off || !b->body_len || !verdict)
-    return fail(OURO_EINVAL, "null argument");
-  DeviceState* ds;
-  int rc = device_state(&ds);
+  if (b->n == 0) return OURO_OK;
+  if (!verdict) return fail(OURO_EINVAL, "null verdict");
+  int rc = check_hdr_batch(b);
   if (rc) return rc;
+  DeviceState* ds;
+  if ((rc = device_state(&ds))) return rc;
+  const HdrOut o{verdict, beta_eta, beta_leader, b->eta_nonce};
   const size_t chunk = host_chunk(ds);
-  if (chunk && n > chunk) return hdr_batch_pipelined(b, chunk, verdict, beta_eta, beta_leader);
-  hipStream_t st;
-  if ((rc = thread_stream(&st))) return rc;
-  const size_t span = span_of(n, b->body_off, b->body_len);
-  if (span && !b->body) return fail(OURO_EINVAL, "null body buffer");
-  Stager sg{st};
-  ouro_tpraos_batch d;
-  d.n = n;
-  d.issuer_vk = sg.up(b->issuer_vk, 32 * n);
-  d.vrf_vk = sg.up(b->vrf_vk, 32 * n);
-  d.eta_proof = sg.up(b->eta_proof, 80 * n);
-  d.leader_proof = sg.up(b->leader_proof, 80 * n);
-  d.eta_alpha = sg.up(b->eta_alpha, 32 * n);
-  d.leader_alpha = sg.up(b->leader_alpha, 32 * n);
-  d.hot_vk = sg.up(b->hot_vk, 32 * n);
-  d.ocert_counter = sg.up(b->ocert_counter, n);
-  d.ocert_kes_period = sg.up(b->ocert_kes_period, n);
-  d.ocert_sigma = sg.up(b->ocert_sigma, 64 * n);
-  d.kes_t = sg.up(b->kes_t, n);
-  d.kes_sig = sg.up(b->kes_sig, 448 * n);
-  d.body = sg.up(b->body, span);
-  d.body_off = sg.up(b->body_off, n);
-  d.body_len = sg.up(b->body_len, n);
-  uint8_t* dver = sg.out<uint8_t>(n);
-  uint8_t* dbe = sg.out<uint8_t>(64 * n);
-  uint8_t* dbl = sg.out<uint8_t>(64 * n);
-  if (sg.rc) return sg.rc;
-  if ((rc = launch_hdr(st, d, dver, dbe, dbl))) return rc;
-  std::vector<uint8_t> tv(n), te(beta_eta ? 64 * n : 0), tl(beta_leader ? 64 * n : 0);
-  if ((rc = download(st, tv.data(), dver, n))) return rc;
-  if (beta_eta && (rc = download(st, te.data(), dbe, 64 * n))) return rc;
-  if (beta_leader && (rc = download(st, tl.data(), dbl, 64 * n))) return rc;
-  if ((rc = finish(st))) return rc;
-  memcpy(verdict, tv.data(), n);
-  if (beta_eta) memcpy(beta_eta, te.data(), 64 * n);
-  if (beta_leader) memcpy(beta_leader, tl.data(), 64 * n);
+  if (chunk && b->n > chunk) return hdr_batch_pipelined(b, chunk, o);
+  return hdr_batch_once(b, o, false);
+}
+
+// ---- latency mode (ChainSync windows) ----
+int ouro_tpraos_verify_batch_lowlat(const ouro_tpraos_batch* b, uint8_t* verdict,
+                                    uint8_t* beta_eta, uint8_t* beta_leader) {
+  if (!b) return fail(OURO_EINVAL, "null batch");
+  if (b->n == 0) return OURO_OK;
+  if (b->n > 0xffffffffu) return fail(OURO_EINVAL, "batch too large");
+  if (!verdict) return fail(OURO_EINVAL, "null verdict");
+  int rc = check_hdr_batch(b);
+  if (rc) return rc;
+  return hdr_batch_once(b, HdrOut{verdict, beta_eta, beta_leader, b->eta_nonce}, true);
+}
+
+int ouro_nonce_fold(size_t n, const uint8_t* eta_nonce, const uint64_t* slot,
+                    uint64_t first_slot_next_epoch, uint64_t stability_window, uint8_t* eta_v,
+                    uint8_t* eta_c, int* is_neutral) {
+  if (n == 0) return OURO_OK;
+  if (!eta_nonce || !slot || !eta_v || !eta_c) return fail(OURO_EINVAL, "null argument");
+  bool v_neutral = is_neutral && is_neutral[0], c_neutral = is_neutral && is_neutral[1];
+  uint32_t v[8], c[8];
+  memcpy(v, eta_v, 32);
+  memcpy(c, eta_c, 32);
+  for (size_t i = 0; i < n; i++) {
+    // eta_v <- eta_v (*) eta, with NeutralNonce (*) x = x
+    uint32_t in[16];
+    memcpy(in + 8, eta_nonce + 32 * i, 32);
+    if (v_neutral) {
+      memcpy(v, in + 8, 32);
+    } else {
+      memcpy(in, v, 32);
+      blake2b256_64(v, in);
+    }
+    v_neutral = false;
+    // UPDN: s +* Duration sp < firstSlotNextEpoch (Word64 arithmetic, as SlotNo)
+    if (slot[i] + stability_window < first_slot_next_epoch) {
+      memcpy(c, v, 32);
+      c_neutral = false;
+    }
+  }
+  memcpy(eta_v, v, 32);
+  memcpy(eta_c, c, 32);
+  if (is_neutral) {
+    is_neutral[0] = v_neutral;
+    is_neutral[1] = c_neutral;
+  }
   return OURO_OK;
 }
 
@@ -978,6 +1097,25 @@ int ouro_vrf03_proof_to_hash(unsigned char* output, const unsigned char* proof) 
   return OURO_OK;
 }
 
+// The cardano-crypto-praos names (PraosVRF's foreign imports), so the shim can
+// satisfy them by link order; the version-less names are the fork's aliases
+// of draft-03.
+int crypto_vrf_ietfdraft03_verify(unsigned char* output, const unsigned char* pk,
+                                  const unsigned char* proof, const unsigned char* m,
+                                  unsigned long long mlen) {
+  return ouro_vrf03_verify(output, pk, proof, m, mlen);
+}
+int crypto_vrf_ietfdraft03_proof_to_hash(unsigned char* output, const unsigned char* proof) {
+  return ouro_vrf03_proof_to_hash(output, proof);
+}
+int crypto_vrf_verify(unsigned char* output, const unsigned char* pk, const unsigned char* proof,
+                      const unsigned char* m, unsigned long long mlen) {
+  return ouro_vrf03_verify(output, pk, proof, m, mlen);
+}
+int crypto_vrf_proof_to_hash(unsigned char* output, const unsigned char* proof) {
+  return ouro_vrf03_proof_to_hash(output, proof);
+}
+
 int ouro_sum6kes_verify(const unsigned char* vk, unsigned int t, const unsigned char* m,
                         unsigned long long mlen, const unsigned char* sig) {
   if (!vk || !sig || (mlen && !m)) return OURO_INVALID;
@@ -1032,6 +1170,9 @@ int ouro_tpraos_verify_batch_device(void* stream, const ouro_tpraos_batch* b, ui
   if (!b) return fail(OURO_EINVAL, "null batch");
   if (b->n == 0) return OURO_OK;
   if (!beta_eta || !beta_leader) return fail(OURO_EINVAL, "device API needs both beta buffers");
+  if (!verdict) return fail(OURO_EINVAL, "null verdict");
+  int rc = check_hdr_batch(b);
+  if (rc) return rc;
   hipStream_t st = static_cast<hipStream_t>(stream);  // NULL = HIP's default stream
   return launch_hdr(st, *b, verdict, beta_eta, beta_leader);
 }
@@ -1046,65 +1187,22 @@ int ouro_leader_check_batch_device(void* stream, size_t n, const uint8_t* beta,
                        verdict);
 }
 
-// ---- latency mode (ChainSync windows) ----
-int ouro_tpraos_verify_batch_lowlat(const ouro_tpraos_batch* b, uint8_t* verdict,
-                                    uint8_t* beta_eta, uint8_t* beta_leader) {
-  if (!b) return fail(OURO_EINVAL, "null batch");
-  const size_t n = b->n;
-  if (n == 0) return OURO_OK;
-  if (n > 0xffffffffu) return fail(OURO_EINVAL, "batch too large");
-  if (!b->issuer_vk || !b->vrf_vk || !b->eta_proof || !b->leader_proof || !b->eta_alpha ||
-      !b->leader_alpha || !b->hot_vk || !b->ocert_counter || !b->ocert_kes_period ||
-      !b->ocert_sigma || !b->kes_t || !b->kes_sig || !b->body_off || !b->body_len || !verdict)
-    return fail(OURO_EINVAL, "null argument");
-  hipStream_t st;
-  int rc = thread_stream(&st);
-  if (rc) return rc;
-  DeviceState* ds;
-  if ((rc = device_state(&ds))) return rc;
-  const size_t span = span_of(n, b->body_off, b->body_len);
-  if (span && !b->body) return fail(OURO_EINVAL, "null body buffer");
-  Stager sg{st};
-  ouro_tpraos_batch d;
-  d.n = n;
-  d.issuer_vk = sg.up(b->issuer_vk, 32 * n);
-  d.vrf_vk = sg.up(b->vrf_vk, 32 * n);
-  d.eta_proof = sg.up(b->eta_proof, 80 * n);
-  d.leader_proof = sg.up(b->leader_proof, 80 * n);
-  d.eta_alpha = sg.up(b->eta_alpha, 32 * n);
-  d.leader_alpha = sg.up(b->leader_alpha, 32 * n);
-  d.hot_vk = sg.up(b->hot_vk, 32 * n);
-  d.ocert_counter = sg.up(b->ocert_counter, n);
-  d.ocert_kes_period = sg.up(b->ocert_kes_period, n);
-  d.ocert_sigma = sg.up(b->ocert_sigma, 64 * n);
-  d.kes_t = sg.up(b->kes_t, n);
-  d.kes_sig = sg.up(b->kes_sig, 448 * n);
-  d.body = sg.up(b->body, span);
-  d.body_off = sg.up(b->body_off, n);
-  d.body_len = sg.up(b->body_len, n);
-  const uint32_t n32 = (uint32_t)n;
-  const uint32_t* d_n = sg.up(&n32, 1);
-  int32_t* res = sg.out<int32_t>(n * kLatResWords);
-  int32_t* scr = sg.out<int32_t>(lowlat_scratch_words(ds, n));
-  uint8_t* dver = sg.out<uint8_t>(n);
-  uint8_t* dbe = sg.out<uint8_t>(64 * n);
-  uint8_t* dbl = sg.out<uint8_t>(64 * n);
-  if (sg.rc) return sg.rc;
-  if ((rc = launch_lowlat(st, d, d_n, n, res, scr, dver, dbe, dbl))) return rc;
-  std::vector<uint8_t> tv(n), te(beta_eta ? 64 * n : 0), tl(beta_leader ? 64 * n : 0);
-  if ((rc = download(st, tv.data(), dver, n))) return rc;
-  if (beta_eta && (rc = download(st, te.data(), dbe, 64 * n))) return rc;
-  if (beta_leader && (rc = download(st, tl.data(), dbl, 64 * n))) return rc;
-  if ((rc = finish(st))) return rc;
-  memcpy(verdict, tv.data(), n);
-  if (beta_eta) memcpy(beta_eta, te.data(), 64 * n);
-  if (beta_leader) memcpy(beta_leader, tl.data(), 64 * n);
-  return OURO_OK;
-}
-
 }  // extern "C"
 
 // ---- captured plans: pinned staging + hipGraph (H2D, 2 kernels, D2H) --------
+// The packed input block: 16 bytes {n, option bits (tpraos.h kOpt*)}, then
+// every member of ouro_tpraos_batch in order, each 16-byte aligned at
+// capacity size; the output block: verdict | beta_eta | beta_leader | eta_nonce.
+namespace {
+constexpr int kPlanFields = 19;
+// bytes per header of each member; 0 = the body (capacity-sized), -1 = a
+// fixed 32 bytes (epoch_nonce)
+constexpr int kFieldBytes[kPlanFields] = {32, 32, 80, 80, 32, 32, 32, 8, 8, 64,
+                                          4,  448, 0, 8, 4, 64, 64, 8, -1};
+enum PlanField { kFBody = 12, kFBodyOff = 13, kFEtaAlpha = 4, kFLeaderAlpha = 5, kFEpochNonce = 18 };
+constexpr size_t align16(size_t x) { return (x + 15) & ~(size_t)15; }
+}  // namespace
+
 struct ouro_tpraos_plan {
   int dev = -1;
   size_t cap = 0, body_cap = 0;
@@ -1114,18 +1212,14 @@ struct ouro_tpraos_plan {
   uint8_t *h_in = nullptr, *d_in = nullptr, *h_out = nullptr, *d_out = nullptr;
   size_t in_bytes = 0, out_bytes = 0;
   int32_t *res = nullptr, *scratch = nullptr;
-  size_t off[16] = {0};  // byte offsets of the 15 fields + n in the packed input block
+  size_t off[kPlanFields] = {0};  // byte offsets of the members in the packed input block
   ouro_tpraos_batch dev_batch{};
-  size_t pending = 0;     // headers of the batch in flight (submit .. wait)
+  size_t pending = 0;           // headers of the batch in flight (submit .. wait)
+  uint8_t* nonce_dst = nullptr;  // that batch's eta_nonce (written by wait)
   bool inflight = false;
 };
 
 namespace {
-constexpr size_t align16(size_t x) { return (x + 15) & ~(size_t)15; }
-// widths (bytes per header) of the 15 SoA fields, in ouro_tpraos_batch order;
-// 0 marks the body (capacity-sized)
-constexpr size_t kFieldBytes[15] = {32, 32, 80, 80, 32, 32, 32, 8, 8, 64, 4, 448, 0, 8, 4};
-
 void plan_free(ouro_tpraos_plan* p) {
   if (!p) return;
   if (p->inflight && p->st) (void)hipStreamSynchronize(p->st);  // no DMA into freed staging
@@ -1141,19 +1235,24 @@ void plan_free(ouro_tpraos_plan* p) {
   delete p;
 }
 
+size_t field_cap_bytes(const ouro_tpraos_plan* p, int f) {
+  return kFieldBytes[f] > 0 ? (size_t)kFieldBytes[f] * p->cap
+                            : (kFieldBytes[f] == 0 ? p->body_cap : 32);
+}
+
 int plan_build(ouro_tpraos_plan* p) {
   DeviceState* ds;
   int rc = device_state(&ds);
   if (rc) return rc;
   if ((rc = current_device(&p->dev))) return rc;
   OURO_HIP(hipStreamCreateWithFlags(&p->st, hipStreamNonBlocking));
-  size_t o = 16;  // n lives in the first 16 bytes
-  for (int f = 0; f < 15; f++) {
+  size_t o = 16;  // n and the option bits live in the first 16 bytes
+  for (int f = 0; f < kPlanFields; f++) {
     p->off[f] = o;
-    o += align16(kFieldBytes[f] ? kFieldBytes[f] * p->cap : p->body_cap);
+    o += align16(field_cap_bytes(p, f));
   }
   p->in_bytes = o;
-  p->out_bytes = align16(p->cap) + 128 * p->cap;
+  p->out_bytes = align16(p->cap) + 160 * p->cap;
   OURO_HIP(hipHostMalloc(&p->h_in, p->in_bytes, hipHostMallocDefault));
   OURO_HIP(hipHostMalloc(&p->h_out, p->out_bytes, hipHostMallocDefault));
   OURO_HIP(hipMalloc(&p->d_in, p->in_bytes));
@@ -1179,9 +1278,14 @@ int plan_build(ouro_tpraos_plan* p) {
   b.body = d + p->off[12];
   b.body_off = reinterpret_cast<const uint64_t*>(d + p->off[13]);
   b.body_len = reinterpret_cast<const uint32_t*>(d + p->off[14]);
+  b.eta_output = d + p->off[15];
+  b.leader_output = d + p->off[16];
+  b.slot = reinterpret_cast<const uint64_t*>(d + p->off[17]);
+  b.epoch_nonce = d + p->off[18];
   uint8_t* dver = p->d_out;
   uint8_t* dbe = dver + align16(p->cap);
   uint8_t* dbl = dbe + 64 * p->cap;
+  b.eta_nonce = dbl + 64 * p->cap;  // written only when the option bit says so
   OURO_HIP(hipStreamBeginCapture(p->st, hipStreamCaptureModeThreadLocal));
   OURO_HIP(hipMemcpyAsync(p->d_in, p->h_in, p->in_bytes, hipMemcpyHostToDevice, p->st));
   rc = launch_lowlat(p->st, b, reinterpret_cast<const uint32_t*>(p->d_in), p->cap, p->res,
@@ -1222,27 +1326,35 @@ int ouro_tpraos_plan_submit(ouro_tpraos_plan* p, const ouro_tpraos_batch* b) {
   if (n > p->cap) return fail(OURO_EINVAL, "batch larger than the plan");
   if (n == 0) {
     p->pending = 0;
+    p->nonce_dst = nullptr;
     p->inflight = true;
     return OURO_OK;
   }
-  const size_t span = span_of(n, b->body_off, b->body_len);
-  if (span > p->body_cap) return fail(OURO_EINVAL, "body bytes exceed the plan");
-  const void* src[15] = {b->issuer_vk, b->vrf_vk, b->eta_proof, b->leader_proof, b->eta_alpha,
-                         b->leader_alpha, b->hot_vk, b->ocert_counter, b->ocert_kes_period,
-                         b->ocert_sigma, b->kes_t, b->kes_sig, b->body, b->body_off, b->body_len};
-  for (int f = 0; f < 15; f++) {
-    const size_t bytes = kFieldBytes[f] ? kFieldBytes[f] * n : span;
-    if (bytes && !src[f]) return fail(OURO_EINVAL, "null field");
+  int rc = check_hdr_batch(b);
+  if (rc) return rc;
+  Window w;
+  if ((rc = window_of(n, b->body_off, b->body_len, &w))) return rc;
+  if (w.span() > p->body_cap) return fail(OURO_EINVAL, "body bytes exceed the plan");
+  if (w.span() && !b->body) return fail(OURO_EINVAL, "null body buffer");
+  const void* src[kPlanFields] = {
+      b->issuer_vk,  b->vrf_vk,           b->eta_proof,   b->leader_proof, b->eta_alpha,
+      b->leader_alpha, b->hot_vk,         b->ocert_counter, b->ocert_kes_period,
+      b->ocert_sigma, b->kes_t,           b->kes_sig,     w.span() ? b->body + w.lo : nullptr,
+      w.off.data(),  b->body_len,         b->eta_output,  b->leader_output, b->slot,
+      b->epoch_nonce};
+  if (b->slot) src[kFEtaAlpha] = src[kFLeaderAlpha] = nullptr;  // derived on the device
+  else src[kFEpochNonce] = nullptr;
+  for (int f = 0; f < kPlanFields; f++) {
+    const size_t bytes = kFieldBytes[f] > 0 ? (size_t)kFieldBytes[f] * n
+                                            : (kFieldBytes[f] == 0 ? w.span() : 32);
+    if (bytes && src[f]) memcpy(p->h_in + p->off[f], src[f], bytes);
   }
-  for (int f = 0; f < 15; f++) {
-    const size_t bytes = kFieldBytes[f] ? kFieldBytes[f] * n : span;
-    if (bytes) memcpy(p->h_in + p->off[f], src[f], bytes);
-  }
-  const uint32_t n32 = (uint32_t)n;
-  memcpy(p->h_in, &n32, sizeof n32);
+  const uint32_t nw[2] = {(uint32_t)n, batch_opts(*b)};
+  memcpy(p->h_in, nw, sizeof nw);
   OURO_HIP(hipSetDevice(p->dev));
   OURO_HIP(hipGraphLaunch(p->exec, p->st));
   p->pending = n;
+  p->nonce_dst = b->eta_nonce;
   p->inflight = true;
   return OURO_OK;
 }
@@ -1257,9 +1369,12 @@ int ouro_tpraos_plan_wait(ouro_tpraos_plan* p, uint8_t* verdict, uint8_t* beta_e
   if (n == 0) return OURO_OK;
   OURO_HIP(hipSetDevice(p->dev));
   OURO_HIP(hipStreamSynchronize(p->st));
+  const uint8_t* o = p->h_out + align16(p->cap);
   memcpy(verdict, p->h_out, n);
-  if (beta_eta) memcpy(beta_eta, p->h_out + align16(p->cap), 64 * n);
-  if (beta_leader) memcpy(beta_leader, p->h_out + align16(p->cap) + 64 * p->cap, 64 * n);
+  if (beta_eta) memcpy(beta_eta, o, 64 * n);
+  if (beta_leader) memcpy(beta_leader, o + 64 * p->cap, 64 * n);
+  if (p->nonce_dst) memcpy(p->nonce_dst, o + 128 * p->cap, 32 * n);
+  p->nonce_dst = nullptr;
   return OURO_OK;
 }
 
@@ -1277,11 +1392,12 @@ void ouro_tpraos_plan_destroy(ouro_tpraos_plan* p) { plan_free(p); }
 }  // extern "C"
 
 // ---- one process, several GPUs ----------------------------
-// A persistent worker thread per shard slot: its thread-local streams, device
-// buffers and pinned staging (the pipelined host path) live as long as the
-// process, so repeated calls allocate nothing.  Each worker verifies one
-// contiguous shard straight into the caller's buffers; in one process no
-// collective is needed.
+// A persistent worker thread per (device, k-th listing of that device): its
+// thread-local streams, device buffers and pinned staging (the pipelined host
+// path) belong to that one device and live as long as the process, so
+// repeated calls allocate nothing and a reordered device list never sends a
+// worker's buffers to another GPU.  Each worker verifies one contiguous shard
+// straight into the caller's buffers; in one process no collective is needed.
 namespace {
 struct Worker {
   std::mutex mu;
@@ -1309,27 +1425,29 @@ struct Worker {
   }
 };
 
-std::mutex g_multi_mu;                 // one multi-device call at a time
-std::vector<Worker*> g_workers;        // never freed: threads outlive every call
+std::mutex g_multi_mu;                              // one multi-device call at a time
+std::map<std::pair<int, int>, Worker*> g_workers;  // never freed: threads outlive every call
 
-Worker* worker(size_t k) {
-  while (g_workers.size() <= k) {
-    Worker* w = new Worker;
-    std::thread([w] { w->loop(); }).detach();
-    g_workers.push_back(w);
+Worker* worker(int dev, int ordinal) {
+  Worker*& w = g_workers[{dev, ordinal}];
+  if (!w) {
+    w = new Worker;
+    w->dev = dev;
+    Worker* self = w;
+    std::thread([self] { self->loop(); }).detach();
   }
-  return g_workers[k];
+  return w;
 }
 
 ouro_tpraos_batch shard_of(const ouro_tpraos_batch& b, size_t lo, size_t m) {
-  ouro_tpraos_batch s = b;  // body + absolute offsets shared
+  ouro_tpraos_batch s = b;  // body + absolute offsets shared, epoch_nonce shared
   s.n = m;
   s.issuer_vk = b.issuer_vk + 32 * lo;
   s.vrf_vk = b.vrf_vk + 32 * lo;
   s.eta_proof = b.eta_proof + 80 * lo;
   s.leader_proof = b.leader_proof + 80 * lo;
-  s.eta_alpha = b.eta_alpha + 32 * lo;
-  s.leader_alpha = b.leader_alpha + 32 * lo;
+  if (b.eta_alpha) s.eta_alpha = b.eta_alpha + 32 * lo;
+  if (b.leader_alpha) s.leader_alpha = b.leader_alpha + 32 * lo;
   s.hot_vk = b.hot_vk + 32 * lo;
   s.ocert_counter = b.ocert_counter + lo;
   s.ocert_kes_period = b.ocert_kes_period + lo;
@@ -1338,6 +1456,10 @@ ouro_tpraos_batch shard_of(const ouro_tpraos_batch& b, size_t lo, size_t m) {
   s.kes_sig = b.kes_sig + 448 * lo;
   s.body_off = b.body_off + lo;
   s.body_len = b.body_len + lo;
+  if (b.eta_output) s.eta_output = b.eta_output + 64 * lo;
+  if (b.leader_output) s.leader_output = b.leader_output + 64 * lo;
+  if (b.slot) s.slot = b.slot + lo;
+  if (b.eta_nonce) s.eta_nonce = b.eta_nonce + 32 * lo;
   return s;
 }
 }  // namespace
@@ -1355,12 +1477,16 @@ int ouro_tpraos_verify_batch_multi(const ouro_tpraos_batch* b, const int* device
   if (!b) return fail(OURO_EINVAL, "null batch");
   if (b->n == 0) return OURO_OK;
   if (!verdict) return fail(OURO_EINVAL, "null verdict");
+  int rc = check_hdr_batch(b);
+  if (rc) return rc;
   std::vector<int> devs;
+  const int count = ouro_device_count();
   if (devices) {
     if (ndev <= 0 || ndev > 64) return fail(OURO_EINVAL, "bad device count");
     devs.assign(devices, devices + ndev);
+    for (int d : devs)
+      if (d < 0 || d >= count) return fail(OURO_ENODEV, "no such device " + std::to_string(d));
   } else {
-    const int count = ouro_device_count();
     for (int d = 0; d < count; d++) devs.push_back(d);
     if (devs.empty()) return fail(OURO_ENODEV, "no device");
   }
@@ -1368,14 +1494,14 @@ int ouro_tpraos_verify_batch_multi(const ouro_tpraos_batch* b, const int* device
   const size_t per = (b->n + g - 1) / g;
   std::lock_guard<std::mutex> guard(g_multi_mu);
   std::vector<Worker*> used;
+  std::map<int, int> listed;  // device -> listings so far
   for (size_t k = 0; k < g; k++) {
     const size_t lo = k * per;
     if (lo >= b->n) break;
     const size_t m = std::min(per, b->n - lo);
-    Worker* w = worker(k);
+    Worker* w = worker(devs[k], listed[devs[k]]++);
     {
       std::lock_guard<std::mutex> lk(w->mu);
-      w->dev = devs[k];
       w->shard = shard_of(*b, lo, m);
       w->verdict = verdict + lo;
       w->be = beta_eta ? beta_eta + 64 * lo : nullptr;
@@ -1386,7 +1512,6 @@ int ouro_tpraos_verify_batch_multi(const ouro_tpraos_batch* b, const int* device
     w->cv.notify_all();
     used.push_back(w);
   }
-  int rc = OURO_OK;
   for (Worker* w : used) {  // wait for every shard, errors included
     std::unique_lock<std::mutex> lk(w->mu);
     w->cv.wait(lk, [&] { return w->done; });

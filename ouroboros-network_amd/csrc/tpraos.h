@@ -40,6 +40,21 @@ enum HdrCore { kCoreOcert = 0, kCoreKes, kCoreUe, kCoreUl, kCoreVe, kCoreVl, kHd
 constexpr int32_t kFlagOk = 1;        // the core's acceptance checks passed
 constexpr int32_t kFlagGammaX0 = 2;   // Gamma decoded with x = 0 (re-encodes with sign 0)
 
+// ---- optional members of a batch (include/ouro_verify.h) -------------------
+// As bits: taken from the pointers (throughput kernel, host paths) or read
+// from device memory next to n (latency kernels replayed from a captured
+// graph, whose device struct always points somewhere).
+constexpr uint32_t kOptEtaClaim = 1u;     // eta_output given
+constexpr uint32_t kOptLeaderClaim = 2u;  // leader_output given
+constexpr uint32_t kOptSeeds = 4u;        // slot given: alphas = mkSeed on device
+constexpr uint32_t kOptEpochNonce = 8u;   // epoch_nonce given (else NeutralNonce)
+constexpr uint32_t kOptEtaNonce = 16u;    // eta_nonce output wanted
+OURO_HD inline uint32_t batch_opts(const ouro_tpraos_batch& b) {
+  return (b.eta_output ? kOptEtaClaim : 0u) | (b.leader_output ? kOptLeaderClaim : 0u) |
+         (b.slot ? kOptSeeds : 0u) | (b.slot && b.epoch_nonce ? kOptEpochNonce : 0u) |
+         (b.eta_nonce ? kOptEtaNonce : 0u);
+}
+
 OURO_FI void st_point_at(int32_t* p, const fe& X, const fe& Y, const fe& Z) {
   st_fe(p, X);
   st_fe(p + 12, Y);
@@ -57,16 +72,23 @@ OURO_FI void st_point_from_dsm(int32_t* res, int which, const int32_t* lane) {
 }
 
 // ---- cores ---------------------------------------------------------------
-// OCERT signature: message hotVk || BE64(counter) || BE64(c0) in registers
-struct OcertMsg {
-  uint32_t w[12];
+// Message bytes held in registers (W words); a select chain keeps a dynamic
+// byte index out of scratch -- in every SHA-512 call here the index is a
+// compile-time constant after unrolling, so the chain folds away.
+template <int W>
+struct RegMsg {
+  uint32_t w[W];
   OURO_FI uint32_t tail(uint32_t q) const {
     uint32_t r = w[0];
 #pragma unroll
-    for (int i = 1; i < 12; i++) r = ((q >> 2) == (uint32_t)i) ? w[i] : r;
+    for (int i = 1; i < W; i++) r = ((q >> 2) == (uint32_t)i) ? w[i] : r;
     return (r >> (8 * (q & 3))) & 0xffu;
   }
 };
+// OCERT signature: message hotVk || BE64(counter) || BE64(c0)
+using OcertMsg = RegMsg<12>;
+// a 32-byte VRF input (the Seed)
+using SeedMsg = RegMsg<8>;
 
 OURO_FI uint32_t bswap32_hd(uint32_t x) {
   return (x >> 24) | ((x >> 8) & 0xff00u) | ((x << 8) & 0xff0000u) | (x << 24);
@@ -338,12 +360,28 @@ OURO_FI void st_words(uint8_t* p, const uint32_t* w, int n16) {
   for (int i = 0; i < n16; i++) q[i] = make_uint4(w[4 * i], w[4 * i + 1], w[4 * i + 2], w[4 * i + 3]);
 }
 
+// The VRF input of header i: mkSeed seedEta / seedL slot eta0 on the device
+// (Shelley/Protocol.hs:409-410; blake2b.h mkseed_hash) when the batch carries
+// slots, else the caller's 32 bytes.
+OURO_HD inline void hdr_seed(SeedMsg& a, const ouro_tpraos_batch& b, size_t i, bool leader,
+                             uint32_t opts) {
+  if (opts & kOptSeeds) {
+    uint32_t e0[8];
+    if (opts & kOptEpochNonce) ld_words(e0, b.epoch_nonce, 2);
+    mkseed_hash(a.w, b.slot[i], (opts & kOptEpochNonce) ? e0 : nullptr);
+#pragma unroll
+    for (int k = 0; k < 8; k++) a.w[k] ^= leader ? kSeedL[k] : kSeedEta[k];
+  } else {
+    ld_words(a.w, (leader ? b.leader_alpha : b.eta_alpha) + 32 * i, 2);
+  }
+}
+
 // One core of header i (tpraos.h); throughput mode reuses the VRF key table
 // built by the eta U core (table slot 2) for the leader U core.
-OURO_HD inline void hdr_core(const ouro_tpraos_batch& b, size_t i, int core,
-                                         int32_t* lane, int32_t* res, const int32_t* btab,
-                                         bool share_key = true, bool split = false,
-                                         bool quad = false) {
+// opts: the batch's optional members (batch_opts / the latency launches' word).
+OURO_HD inline void hdr_core(const ouro_tpraos_batch& b, size_t i, uint32_t opts, int core,
+                             int32_t* lane, int32_t* res, const int32_t* btab,
+                             bool share_key = true, bool split = false, bool quad = false) {
   int32_t flag = 0;
   switch (core) {
     case kCoreOcert: {
@@ -382,8 +420,9 @@ OURO_HD inline void hdr_core(const ouro_tpraos_batch& b, size_t i, int core,
       uint32_t p[8], pi[20];
       ld_words(p, b.vrf_vk + 32 * i, 2);
       ld_words(pi, (leader ? b.leader_proof : b.eta_proof) + 80 * i, 5);
-      const uint8_t* a = (leader ? b.leader_alpha : b.eta_alpha) + 32 * i;
-      flag = vrf_v_core(p, pi, ShaGlobalTail{a}, 32, lane, btab, res,
+      SeedMsg a{};  // the 32-byte VRF input, in registers
+      if (!gamma) hdr_seed(a, b, i, leader, opts);
+      flag = vrf_v_core(p, pi, a, 32, lane, btab, res,
                         leader ? kPtHl : kPtHe, leader ? kPtVl : kPtVe,
                         leader ? kPtG8l : kPtG8e, gamma ? 2 : (split ? 1 : 0),
                         res + kLatPart + (leader ? kPtWords : 0), quad);
@@ -393,32 +432,67 @@ OURO_HD inline void hdr_core(const ouro_tpraos_batch& b, size_t i, int core,
   res[kResFlags + core] = flag;
 }
 
+// The claimed-output bit of one VRF (OURO_HDR_ETA_CLAIM_OK / _LEADER_CLAIM_OK):
+// the header's certifiedOutput equals the output computed from a valid proof.
+OURO_HD inline uint32_t hdr_claim_bit(const ouro_tpraos_batch& b, size_t i, uint32_t opts,
+                                      int which, bool proof_ok, const uint32_t beta[16]) {
+  if (!proof_ok || !(opts & (which ? kOptLeaderClaim : kOptEtaClaim))) return 0u;
+  uint32_t cl[16];
+  ld_words(cl, (which ? b.leader_output : b.eta_output) + 64 * i, 4);
+  uint32_t diff = 0;
+#pragma unroll
+  for (int k = 0; k < 16; k++) diff |= cl[k] ^ beta[k];
+  return diff ? 0u : (which ? 0x20u : 0x10u);
+}
+
+// eta_nonce[i] = mkNonceFromOutputVRF of the eta output the nonce update
+// consumes: Blake2b-256 of the CLAIMED output when the batch carries it (the
+// reference's PRTCL rule hashes VRF.certifiedOutput of bheaderEta), else of
+// the computed beta_eta (zeros for a failed proof: the header is invalid).
+OURO_HD inline void hdr_eta_nonce(const ouro_tpraos_batch& b, size_t i, uint32_t opts,
+                                  const uint32_t beta_e[16]) {
+  if (!(opts & kOptEtaNonce)) return;
+  uint32_t in[16], h[8];
+  if (opts & kOptEtaClaim) {
+    ld_words(in, b.eta_output + 64 * i, 4);
+  } else {
+#pragma unroll
+    for (int k = 0; k < 16; k++) in[k] = beta_e[k];
+  }
+  blake2b256_64(h, in);
+  st_words(b.eta_nonce + 32 * i, h, 2);
+}
+
 // latency-mode finish of header i, VRF by VRF (the host form of the lane-pair
 // finish in k_tpraos_finish)
-OURO_HD inline void hdr_finish_item_split(const ouro_tpraos_batch& b, size_t i, const int32_t* res,
-                                          uint8_t* verdict, uint8_t* beta_eta,
-                                          uint8_t* beta_leader) {
+OURO_HD inline void hdr_finish_item_split(const ouro_tpraos_batch& b, size_t i, uint32_t opts,
+                                          const int32_t* res, uint8_t* verdict,
+                                          uint8_t* beta_eta, uint8_t* beta_leader) {
   uint32_t v = 0;
   if (res[kResFlags + kCoreOcert] & kFlagOk) v |= 0x01u;
   if (res[kResFlags + kCoreKes] & kFlagOk) v |= 0x02u;
   for (int which = 0; which < 2; which++) {
     uint32_t pi[20], beta[16];
     ld_words(pi, (which ? b.leader_proof : b.eta_proof) + 80 * i, 5);
-    v |= vrf_finish_split(res, which, pi, beta);
+    const uint32_t bit = vrf_finish_split(res, which, pi, beta);
+    v |= bit | hdr_claim_bit(b, i, opts, which, bit != 0, beta);
+    if (!which) hdr_eta_nonce(b, i, opts, beta);
     uint8_t* dst = which ? beta_leader : beta_eta;
     if (dst) st_words(dst + 64 * i, beta, 4);
   }
   verdict[i] = (uint8_t)v;
 }
 
-OURO_HD inline void hdr_finish_item(const ouro_tpraos_batch& b, size_t i,
-                                                const int32_t* res, int32_t* tmp,
-                                                uint8_t* verdict, uint8_t* beta_eta,
-                                                uint8_t* beta_leader) {
+OURO_HD inline void hdr_finish_item(const ouro_tpraos_batch& b, size_t i, uint32_t opts,
+                                     const int32_t* res, int32_t* tmp, uint8_t* verdict,
+                                     uint8_t* beta_eta, uint8_t* beta_leader) {
   uint32_t pie[20], pil[20], be[16], bl[16];
   ld_words(pie, b.eta_proof + 80 * i, 5);
   ld_words(pil, b.leader_proof + 80 * i, 5);
-  const uint32_t v = hdr_finish(res, tmp, pie, pil, be, bl);
+  uint32_t v = hdr_finish(res, tmp, pie, pil, be, bl);
+  v |= hdr_claim_bit(b, i, opts, 0, (v & 0x04u) != 0, be);
+  v |= hdr_claim_bit(b, i, opts, 1, (v & 0x08u) != 0, bl);
+  hdr_eta_nonce(b, i, opts, be);
   if (beta_eta) st_words(beta_eta + 64 * i, be, 4);
   if (beta_leader) st_words(beta_leader + 64 * i, bl, 4);
   verdict[i] = (uint8_t)v;

@@ -17,8 +17,9 @@ spans instead of re-encoding anything.
 """
 from __future__ import annotations
 
+import hashlib
 from dataclasses import dataclass
-from typing import List, Sequence, Tuple
+from typing import List, Optional, Sequence, Tuple
 
 import numpy as np
 
@@ -182,12 +183,23 @@ def kes_t(slot: int, slots_per_kes_period: int, c0: int) -> int:
     return cur - c0 if cur >= c0 else 0
 
 
-def pack(headers: Sequence[ShelleyHeader], eta_alpha: Sequence[bytes],
-         leader_alpha: Sequence[bytes], slots_per_kes_period: int) -> HeaderBatch:
-    """SoA batch from parsed headers and the caller's VRF inputs (mkSeed values)."""
+def pack(headers: Sequence[ShelleyHeader], eta_alpha: Optional[Sequence[bytes]] = None,
+         leader_alpha: Optional[Sequence[bytes]] = None, slots_per_kes_period: int = 129600,
+         *, claimed: bool = True, seeds: bool = False,
+         epoch_nonce: Optional[bytes] = None) -> HeaderBatch:
+    """SoA batch from parsed headers.
+
+    VRF inputs: the caller's alphas (mkSeed values), or with seeds=True the
+    header slots and `epoch_nonce` (eta0; None = NeutralNonce), from which the
+    device derives them exactly as OVERLAY does.  claimed=True carries the
+    headers' certifiedOutputs, so the verdict has the *_CLAIM_OK bits and the
+    nonce output hashes the claimed eta output (the reference's semantics)."""
     n = len(headers)
-    if len(eta_alpha) != n or len(leader_alpha) != n:
-        raise ValueError("one eta/leader alpha per header")
+    if not seeds and (eta_alpha is None or leader_alpha is None
+                      or len(eta_alpha) != n or len(leader_alpha) != n):
+        raise ValueError("one eta/leader alpha per header (or seeds=True)")
+    if epoch_nonce is not None and len(epoch_nonce) != 32:
+        raise ValueError("epoch_nonce: 32 bytes")
 
     def rows(get, w):
         return np.frombuffer(b"".join(get(h) for h in headers), np.uint8).reshape(n, w) if n \
@@ -197,13 +209,16 @@ def pack(headers: Sequence[ShelleyHeader], eta_alpha: Sequence[bytes],
     offs = np.zeros(n, np.uint64)
     if n > 1:
         offs[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
+    alphas = (None, None) if seeds else (
+        np.frombuffer(b"".join(eta_alpha), np.uint8).reshape(n, 32),
+        np.frombuffer(b"".join(leader_alpha), np.uint8).reshape(n, 32))
     return HeaderBatch(
         issuer_vk=rows(lambda h: h.issuer_vk, 32),
         vrf_vk=rows(lambda h: h.vrf_vk, 32),
         eta_proof=rows(lambda h: h.eta_proof, 80),
         leader_proof=rows(lambda h: h.leader_proof, 80),
-        eta_alpha=np.frombuffer(b"".join(eta_alpha), np.uint8).reshape(n, 32),
-        leader_alpha=np.frombuffer(b"".join(leader_alpha), np.uint8).reshape(n, 32),
+        eta_alpha=alphas[0],
+        leader_alpha=alphas[1],
         hot_vk=rows(lambda h: h.hot_vk, 32),
         ocert_counter=np.array([h.ocert_counter for h in headers], np.uint64),
         ocert_kes_period=np.array([h.ocert_kes_period for h in headers], np.uint64),
@@ -214,15 +229,27 @@ def pack(headers: Sequence[ShelleyHeader], eta_alpha: Sequence[bytes],
         body=np.frombuffer(b"".join(h.body for h in headers) or b"\0", np.uint8),
         body_off=offs,
         body_len=lens,
+        eta_output=rows(lambda h: h.eta_output, 64) if claimed else None,
+        leader_output=rows(lambda h: h.leader_output, 64) if claimed else None,
+        slot=np.array([h.slot for h in headers], np.uint64) if seeds else None,
+        epoch_nonce=np.frombuffer(epoch_nonce, np.uint8) if (seeds and epoch_nonce) else None,
     )
 
 
-def mk_seed(universal_nonce: bytes, slot: int, epoch_nonce: bytes, blake2b_256) -> bytes:
-    """ledger-specs mkSeed (as recalled; PARITY UNPINNED in this container,
-    SURVEY.md §8(f) row 2): Blake2b_256(BE64(slot) || eta0) XOR ucNonce, where
-    seedEta/seedL = Blake2b_256(BE64(0/1)).  `blake2b_256` is injected so the
-    host picks its own hash implementation."""
-    h = blake2b_256(slot.to_bytes(8, "big") + (epoch_nonce or b""))
+def _blake2b_256(m: bytes) -> bytes:
+    return hashlib.blake2b(m, digest_size=32).digest()
+
+
+SEED_ETA = _blake2b_256((0).to_bytes(8, "big"))  # mkNonceFromNumber 0
+SEED_L = _blake2b_256((1).to_bytes(8, "big"))    # mkNonceFromNumber 1
+
+
+def mk_seed(universal_nonce: Optional[bytes], slot: int, epoch_nonce: Optional[bytes]) -> bytes:
+    """ledger-specs mkSeed on the host (the device computes the same when a
+    batch carries slots): Blake2b_256(BE64(slot) || eta0) XOR ucNonce, eta0 =
+    None for NeutralNonce; ucNonce = SEED_ETA / SEED_L (mkNonceFromNumber 0/1,
+    pinned by the reference's golden ChainDepState, tests/test_nonce.py)."""
+    h = _blake2b_256(slot.to_bytes(8, "big") + (epoch_nonce or b""))
     if universal_nonce is None:
         return h
     return bytes(a ^ b for a, b in zip(h, universal_nonce))

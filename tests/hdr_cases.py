@@ -1,0 +1,75 @@
+"""Header batches for the header-combiner tests (CPU and GPU), built from the
+reference's golden headers (tests/golden/reference_kats.json).
+
+* golden_variants: the 7 golden headers plus decodable single-byte
+  corruptions of the first (every `stride`-th byte of its body and KES
+  signature), VRF inputs as the golden examples use them
+  (Examples.hs:457-458), claimed outputs carried (or not);
+* seeded: the golden headers re-proved for mkSeed inputs -- the golden VRF
+  key is the seed 32 x 0x01 key -- so the device derives
+  alpha from (slot, eta0); plus rows with a wrong slot, a wrong proof and
+  forged claimed outputs;
+* forge_claims: valid proofs with the claimed output changed (the
+  ref2020-vs-strict split of SURVEY.md App. B.3).
+"""
+import numpy as np
+
+import oracle_ffi as O
+from ouroboros_network_amd import header as H
+
+GOLDEN_VRF_SEED = b"\x01" * 32
+
+
+def golden_variants(kats, stride=1, claimed=True):
+    hs = kats["headers"]
+    parsed = [H.parse_header(bytes.fromhex(h["raw"])) for h in hs]
+    ea = [bytes.fromhex(h["eta_alpha"]) for h in hs]
+    la = [bytes.fromhex(h["leader_alpha"]) for h in hs]
+    raw = bytes.fromhex(hs[0]["raw"])
+    for off in range(parsed[0].body_span[0], len(raw), stride):
+        r = bytearray(raw)
+        r[off] = (r[off] + 1) & 0xFF
+        try:
+            parsed.append(H.parse_header(bytes(r)))
+        except Exception:
+            continue  # no longer decodes: the reference rejects before crypto
+        ea.append(ea[0])
+        la.append(la[0])
+    return H.pack(parsed, ea, la, slots_per_kes_period=100, claimed=claimed)
+
+
+def forge_claims(batch, rng, frac=4):
+    """Copy of `batch` with one byte of the claimed eta or leader output
+    changed on 1/frac of the rows; returns (batch, forged row indices)."""
+    eo, lo = batch.eta_output.copy(), batch.leader_output.copy()
+    idx = np.nonzero(rng.integers(0, frac, len(batch)) == 0)[0]
+    idx = np.union1d(idx, [0])  # a golden row: valid proofs, forged output
+    for i in idx:
+        a = eo if rng.integers(0, 2) else lo
+        a[i, rng.integers(0, 64)] ^= 1 << int(rng.integers(0, 8))
+    return batch.with_(eta_output=eo, leader_output=lo), idx
+
+
+def seeded(kats, epoch_nonce, copies=4, rng=None):
+    """Golden headers with VRF proofs over mkSeed seedEta/seedL slot eta0, the
+    slots varied per copy (epoch_nonce None = NeutralNonce)."""
+    rng = rng or np.random.default_rng(3)
+    _, sk = O.vrf_keypair(GOLDEN_VRF_SEED)
+    hs = kats["headers"]
+    parsed = [H.parse_header(bytes.fromhex(h["raw"])) for h in hs] * copies
+    slots = [int(x) for x in rng.integers(0, 2**40, len(parsed))]
+    slots[0], slots[1] = 0, 2**64 - 1
+    batch = H.pack(parsed, seeds=True, epoch_nonce=epoch_nonce, slots_per_kes_period=100)
+    ep, lp = batch.eta_proof.copy(), batch.leader_proof.copy()
+    eo, lo = batch.eta_output.copy(), batch.leader_output.copy()
+    for i, s in enumerate(slots):
+        for uc, proofs, outs in ((H.SEED_ETA, ep, eo), (H.SEED_L, lp, lo)):
+            pi = O.vrf_prove(sk, O.mk_seed(uc, s, epoch_nonce))
+            proofs[i] = np.frombuffer(pi, np.uint8)
+            outs[i] = np.frombuffer(O.vrf_proof_to_hash(pi), np.uint8)
+    sl = np.array(slots, np.uint64)
+    sl[2] += 1            # proofs for another slot: both VRFs fail
+    ep[3, 70] ^= 4        # a corrupted eta proof
+    lo[4, 5] ^= 1         # a forged claimed leader output on a valid proof
+    eo[5, 63] ^= 0x80     # a forged claimed eta output on a valid proof
+    return batch.with_(eta_proof=ep, leader_proof=lp, eta_output=eo, leader_output=lo, slot=sl)

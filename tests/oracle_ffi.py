@@ -47,6 +47,8 @@ def lib() -> ctypes.CDLL:
             "orc_tpraos_verify_batch": (None, [P, P, P, P, I]),
             "orc_synth_ed25519": (None, [SZ, ctypes.c_uint64, P, P, P, I]),
             "orc_synth_vrf": (None, [SZ, ctypes.c_uint64, P, P, P, I]),
+            "orc_mk_nonce_from_number": (None, [P, ctypes.c_uint64]),
+            "orc_mk_seed": (None, [P, P, ctypes.c_uint64, P]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(_lib, name)
@@ -69,6 +71,30 @@ def blake2b_256(m: bytes) -> bytes:
     out = _b(32)
     lib().orc_blake2b_256(out, m, len(m))
     return out.raw
+
+
+def mk_nonce_from_number(k: int) -> bytes:
+    out = _b(32)
+    lib().orc_mk_nonce_from_number(out, k)
+    return out.raw
+
+
+def mk_seed(uc, slot: int, eta0) -> bytes:
+    """ledger-specs mkSeed (uc / eta0 = None: NeutralNonce)."""
+    out = _b(32)
+    lib().orc_mk_seed(out, uc, slot, eta0)
+    return out.raw
+
+
+def nonce_module():
+    """oracle/nonce.py (the UPDN fold restated; test infrastructure)."""
+    import importlib.util
+
+    spec = importlib.util.spec_from_file_location("oracle_nonce",
+                                                  os.path.join(ROOT, "oracle", "nonce.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
 
 
 def ed25519_keypair(seed: bytes):

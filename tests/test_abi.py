@@ -54,7 +54,48 @@ def test_struct_layout_matches_header():
     body = text[text.index("typedef struct ouro_tpraos_batch"):text.index("} ouro_tpraos_batch;")]
     names = re.findall(r"\*?\s*\b([a-z_]+);", body)
     assert [f[0] for f in _native.TPraosBatch._fields_] == names
-    assert ctypes.sizeof(_native.TPraosBatch) == 16 * 8
+    assert ctypes.sizeof(_native.TPraosBatch) == 21 * 8
+
+
+def test_struct_offsets_match_the_c_compiler(tmp_path):
+    """Every member's offset as gcc lays out the C header = the ctypes mirror's
+    (and the oracle's orc_tpraos_batch, which tests hand the same struct)."""
+    import subprocess
+
+    from ouroboros_network_amd import _native
+
+    names = [f[0] for f in _native.TPraosBatch._fields_]
+    src = tmp_path / "off.c"
+    src.write_text(
+        '#include <stdio.h>\n#include <stddef.h>\n#include "ouro_verify.h"\n'
+        '#include "oracle.h"\nint main(void){\n'
+        'printf("%zu %zu\\n", sizeof(ouro_tpraos_batch), sizeof(orc_tpraos_batch));\n'
+        + "".join(f'printf("%zu %zu\\n", offsetof(ouro_tpraos_batch, {n}), '
+                  f'offsetof(orc_tpraos_batch, {n}));\n' for n in names)
+        + "return 0;}\n")
+    exe = tmp_path / "off"
+    subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), "-I", os.path.join(ROOT, "oracle"),
+                    str(src), "-o", str(exe)], check=True)
+    rows = [tuple(map(int, ln.split())) for ln in
+            subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split("\n")
+            if ln]
+    assert rows[0] == (ctypes.sizeof(_native.TPraosBatch),) * 2
+    for (name, _), (c_off, orc_off) in zip(_native.TPraosBatch._fields_, rows[1:]):
+        assert getattr(_native.TPraosBatch, name).offset == c_off == orc_off, name
+
+
+def test_library_exports_the_vrf_aliases():
+    """crypto_vrf_ietfdraft03_{verify,proof_to_hash} and crypto_vrf_{verify,
+    proof_to_hash}: the cardano-crypto-praos names PraosVRF binds, exported so
+    a link-order drop-in needs no Haskell edit."""
+    from ouroboros_network_amd import _native
+
+    lib = ctypes.CDLL(LIB)
+    for name in _native.VRF_ALIASES:
+        assert hasattr(lib, name), name
+    text = open(os.path.join(ROOT, "include", "ouro_verify.h")).read()
+    for name in _native.VRF_ALIASES:
+        assert name in text
 
 
 def test_no_device_is_an_error_not_an_accept():

@@ -12,6 +12,7 @@ import subprocess
 import numpy as np
 import pytest
 
+import hdr_cases as HC
 import oracle_ffi as O
 from edge_cases import ed25519_edge_cases, vrf_edge_cases
 
@@ -196,48 +197,68 @@ def test_kes_lane_golden(dh, kats):
         assert dh.dh_sum6kes_verify(hd.hot_vk, 1, hd.body, len(hd.body), hd.kes_sig) != 0
 
 
-def _hdr_variants(kats, stride):
-    """The golden headers plus single-byte corruptions of the first one (every
-    `stride`-th byte of its body and signature region)."""
-    from ouroboros_network_amd import header as H
-
-    hs = kats["headers"]
-    parsed = [H.parse_header(bytes.fromhex(h["raw"])) for h in hs]
-    ea = [bytes.fromhex(h["eta_alpha"]) for h in hs]
-    la = [bytes.fromhex(h["leader_alpha"]) for h in hs]
-    raw = bytes.fromhex(hs[0]["raw"])
-    for off in range(parsed[0].body_span[0], len(raw), stride):
-        r = bytearray(raw)
-        r[off] = (r[off] + 1) & 0xFF
-        try:
-            parsed.append(H.parse_header(bytes(r)))
-        except Exception:
-            continue
-        ea.append(ea[0])
-        la.append(la[0])
-    return H.pack(parsed, ea, la, slots_per_kes_period=100)
-
-
-@pytest.mark.parametrize("mode", [0, 1, 2], ids=["throughput", "latency", "latency_quad"])
-def test_header_drivers(dh, kats, mode):
-    """tpraos.h's cores + single-inversion finish, in the throughput schedule
-    (one lane, VRF key table shared) and the latency schedule (a lane per
-    core), equal the oracle's verdict bits and outputs."""
-    batch = _hdr_variants(kats, stride=7)
+def _run_drivers(dh, batch, mode, nonce=False):
     n = len(batch)
-    s = batch.c_struct()
+    en = np.zeros((n, 32), np.uint8) if nonce else None
+    s = batch.c_struct(en)
     verdict = np.zeros(n, np.uint8)
     be = np.zeros((n, 64), np.uint8)
     bl = np.zeros((n, 64), np.uint8)
     dh.dh_tpraos_verify.argtypes = [ctypes.c_void_p, ctypes.c_int] + [ctypes.c_void_p] * 3
     assert dh.dh_tpraos_verify(ctypes.addressof(s), mode, O.p(verdict), O.p(be), O.p(bl)) == 0
-    wv, wbe, wbl = O.tpraos_verify_batch(batch)
-    np.testing.assert_array_equal(verdict, wv)
-    np.testing.assert_array_equal(be, wbe)
-    np.testing.assert_array_equal(bl, wbl)
-    for h, v in zip(kats["headers"], verdict):
-        assert int(v) == h["expect_verdict"]
-    assert (verdict != 15).sum() > 10
+    return verdict, be, bl, en
+
+
+def _oracle(batch, nonce=False):
+    n = len(batch)
+    en = np.zeros((n, 32), np.uint8) if nonce else None
+    s = batch.c_struct(en)
+    verdict = np.zeros(n, np.uint8)
+    be = np.zeros((n, 64), np.uint8)
+    bl = np.zeros((n, 64), np.uint8)
+    O.lib().orc_tpraos_verify_batch(ctypes.addressof(s), O.p(verdict), O.p(be), O.p(bl), 8)
+    return verdict, be, bl, en
+
+
+MODES = pytest.mark.parametrize("mode", [0, 1, 2], ids=["throughput", "latency", "latency_quad"])
+
+
+@MODES
+def test_header_drivers(dh, kats, mode):
+    """tpraos.h's cores + single-inversion finish, in the throughput schedule
+    (one lane, VRF key table shared) and the latency schedule (a lane per
+    core), equal the oracle's verdict bits and outputs."""
+    batch = HC.golden_variants(kats, stride=7)
+    got = _run_drivers(dh, batch, mode)
+    want = _oracle(batch)
+    for g, w in zip(got[:3], want[:3]):
+        np.testing.assert_array_equal(g, w)
+    for h, v in zip(kats["headers"], got[0]):
+        assert int(v) & 0x0F == h["expect_verdict"]
+        assert int(v) & 0x30 == 0x30  # claimed outputs = computed (golden)
+    assert (got[0] & 0x0F != 15).sum() > 10
+
+
+@MODES
+def test_header_drivers_claims_seeds_nonces(dh, kats, mode):
+    """The optional members: forged claimed outputs on valid proofs (PROOF bit
+    set, CLAIM bit clear), no claimed outputs (no CLAIM bits), VRF inputs
+    derived on the device from (slot, eta0) incl. NeutralNonce, and the
+    eta_nonce output -- all equal to the oracle."""
+    rng = np.random.default_rng(21)
+    forged, idx = HC.forge_claims(HC.golden_variants(kats, stride=23), rng)
+    cases = [forged, HC.golden_variants(kats, stride=23, claimed=False),
+             HC.seeded(kats, bytes(range(32)), copies=2),
+             HC.seeded(kats, None, copies=1)]
+    for batch in cases:
+        got = _run_drivers(dh, batch, mode, nonce=True)
+        want = _oracle(batch, nonce=True)
+        for g, w in zip(got, want):
+            np.testing.assert_array_equal(g, w)
+    v = _run_drivers(dh, forged, mode)[0]
+    assert ((v[idx] & 0x0F) == 15).sum() > 0 and ((v[idx] & 0x30) != 0x30).all()
+    sv = _run_drivers(dh, cases[2], mode)[0]
+    assert list(sv[:6]) == [0x3F, 0x3F, 0x03, 0x2B, 0x1F, 0x2F]
 
 
 def test_zero_bound_violations(dh):

@@ -1,0 +1,120 @@
+"""GPU parity of the header boundary's optional members (include/ouro_verify.h):
+
+* claimed VRF outputs -> OURO_HDR_ETA_CLAIM_OK / _LEADER_CLAIM_OK.  The
+  reference accepts on the proof (verifyCertified) and then uses the CLAIMED
+  output (Shelley/Protocol.hs:484-486, Shelley/Ledger/TPraos.hs:40); a forged
+  claimed output on a valid proof must give PROOF ok and CLAIM clear;
+* VRF inputs derived on the device from (slot, eta0) by mkSeed;
+* the eta_nonce output (mkNonceFromOutputVRF of the claimed eta output),
+  folded by ouro_nonce_fold exactly as oracle/nonce.py's UPDN.
+
+Every path -- throughput kernel (one piece and pipelined chunks), latency
+kernels (lane quads and one lane), captured plans (run, submit/wait) and the
+multi-device workers -- against the oracle (oracle/tpraos.c), bit for bit.
+"""
+import numpy as np
+import pytest
+
+import hdr_cases as HC
+import oracle_ffi as O
+
+pytestmark = pytest.mark.gpu
+
+
+def _oracle(batch):
+    import ctypes
+
+    n = len(batch)
+    en = np.zeros((n, 32), np.uint8)
+    s = batch.c_struct(en)
+    v = np.zeros(n, np.uint8)
+    be = np.zeros((n, 64), np.uint8)
+    bl = np.zeros((n, 64), np.uint8)
+    O.lib().orc_tpraos_verify_batch(ctypes.addressof(s), O.p(v), O.p(be), O.p(bl), 8)
+    return v, be, bl, en
+
+
+def _cases(kats):
+    rng = np.random.default_rng(31)
+    forged, _ = HC.forge_claims(HC.golden_variants(kats, stride=3), rng)
+    return {
+        "forged_claims": forged,
+        "no_claims": HC.golden_variants(kats, stride=5, claimed=False),
+        "seeded_eta0": HC.seeded(kats, bytes(range(100, 132)), copies=6),
+        "seeded_neutral": HC.seeded(kats, None, copies=3),
+    }
+
+
+def _check(got, want):
+    for g, w in zip(got, want):
+        np.testing.assert_array_equal(g, w)
+
+
+@pytest.mark.parametrize("chunk", ["0", "5"], ids=["one_piece", "pipelined"])
+def test_throughput_paths(gpu_lib, kats, monkeypatch, chunk):
+    from ouroboros_network_amd.tpraos import verify_headers
+
+    monkeypatch.setenv("OURO_HOST_CHUNK", chunk)
+    for name, batch in _cases(kats).items():
+        want = _oracle(batch)
+        _check(verify_headers(batch, nonce=True), want)
+        v = verify_headers(batch)[0]
+        np.testing.assert_array_equal(v, want[0])
+    seeded = _cases(kats)["seeded_eta0"]
+    v = verify_headers(seeded)[0]
+    assert list(v[:6]) == [0x3F, 0x3F, 0x03, 0x2B, 0x1F, 0x2F]
+
+
+@pytest.mark.parametrize("quad", ["1", "0"], ids=["lane_quads", "one_lane"])
+def test_latency_paths(gpu_lib, kats, monkeypatch, quad):
+    from ouroboros_network_amd.tpraos import HeaderPlan, verify_headers_lowlat
+
+    monkeypatch.setenv("OURO_LAT_QUAD", quad)
+    cases = _cases(kats)
+    for name, batch in cases.items():
+        want = _oracle(batch)
+        _check(verify_headers_lowlat(batch, nonce=True), want)
+    # one plan serves batches with and without each optional member in turn
+    plan = HeaderPlan(max_headers=64, max_body_bytes=64 * 1400)
+    try:
+        for _ in range(2):
+            for name, batch in cases.items():
+                want = _oracle(batch)
+                for lo in range(0, len(batch), 64):
+                    hi = min(len(batch), lo + 64)
+                    w = batch.slice(lo, hi)
+                    got = plan.run(w, nonce=True)
+                    _check(got, tuple(x[lo:hi] for x in want))
+                    plan.submit(w, nonce=(lo // 64) % 2 == 0)
+                    got = plan.wait()
+                    _check(got, tuple(x[lo:hi] for x in want)[:len(got)])
+    finally:
+        plan.close()
+
+
+def test_multi_device_paths(gpu_lib, kats):
+    from ouroboros_network_amd.tpraos import verify_headers_multi
+
+    for name, batch in _cases(kats).items():
+        want = _oracle(batch)
+        for devices in ([0], [0, 0, 0]):
+            _check(verify_headers_multi(batch, devices, nonce=True), want)
+
+
+def test_nonce_fold_from_device_outputs(gpu_lib, kats):
+    """eta_nonce rows from the kernel, folded by ouro_nonce_fold, equal the
+    oracle's UPDN fold over Blake2b-256 of the CLAIMED outputs; with claimed
+    outputs forged, the fold follows the claimed (not the computed) output,
+    as the reference's PRTCL rule does."""
+    from ouroboros_network_amd.tpraos import nonce_fold, verify_headers
+
+    ON = O.nonce_module()
+    batch = HC.seeded(kats, bytes(32), copies=2)
+    v, be, bl, en = verify_headers(batch, nonce=True)
+    claimed = [bytes(r) for r in batch.eta_output]
+    assert [bytes(r) for r in en] == [ON.mk_nonce_from_output_vrf(c) for c in claimed]
+    assert bytes(en[5]) != ON.mk_nonce_from_output_vrf(bytes(be[5]))  # forged claim row
+    slots = np.sort(batch.slot)
+    for fsne in (int(slots[len(slots) // 2]) + 10, 2**63):
+        got = nonce_fold(en, slots, fsne, 7, None, b"\x11" * 32)
+        assert got == ON.fold(None, b"\x11" * 32, [bytes(r) for r in en], slots, fsne, 7)

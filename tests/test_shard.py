@@ -1,8 +1,9 @@
-"""Multi-rank sharding + result all-gather on CPU (gloo, world_size 2 and 3).
+"""Multi-rank sharding + result all-gather (gloo, world_size 2 and 3).
 
-The per-shard verifier is injected: here the CPU oracle stands in for the
+On CPU the per-shard verifier is injected: the CPU oracle stands in for the
 gfx950 kernel so the distributed plumbing (shard bounds, padding, gather order)
-is tested without a GPU; the GPU path of the same function runs in bench.py.
+is tested without a GPU.  The -m gpu tests run the same function with the HIP
+kernel per shard (gloo world of 2 on the box's GPU) and the RCCL gather branch.
 """
 import os
 import socket
@@ -31,7 +32,7 @@ def test_shard_range_covers_exactly():
                 assert b == c and a <= b
 
 
-def _worker(rank, world, port, out_dir):
+def _worker(rank, world, port, out_dir, use_gpu=False):
     import sys
 
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -55,7 +56,13 @@ def _worker(rank, world, port, out_dir):
     la = [bytes.fromhex(h["leader_alpha"]) for h in hs]
     la[3] = bytes(32)  # one leader VRF fails
     batch = H.pack(parsed, ea, la, slots_per_kes_period=100)
-    v, be, bl = verify_sharded(batch, verify=lambda b: O.tpraos_verify_batch(b, threads=1))
+    if use_gpu:  # the gfx950 kernel per shard (every rank on GPU 0 of the box)
+        import torch
+
+        torch.cuda.set_device(0)
+        v, be, bl = verify_sharded(batch)
+    else:
+        v, be, bl = verify_sharded(batch, verify=lambda b: O.tpraos_verify_batch(b, threads=1))
     np.save(os.path.join(out_dir, f"v{rank}.npy"), v)
     np.save(os.path.join(out_dir, f"be{rank}.npy"), be)
     np.save(os.path.join(out_dir, f"bl{rank}.npy"), bl)
@@ -78,7 +85,29 @@ def test_verify_sharded_gloo(tmp_path, world, kats):
         np.testing.assert_array_equal(np.load(tmp_path / f"v{r}.npy"), want[0])
         np.testing.assert_array_equal(np.load(tmp_path / f"be{r}.npy"), want[1])
         np.testing.assert_array_equal(np.load(tmp_path / f"bl{r}.npy"), want[2])
-    assert want[0][3] == 0x07 and (np.delete(want[0], 3) == 0x0F).all()
+    assert want[0][3] & 0x0F == 0x07 and (np.delete(want[0], 3) & 0x0F == 0x0F).all()
+
+
+@pytest.mark.gpu
+def test_verify_sharded_hip_per_shard_gloo(tmp_path, kats):
+    """shard.verify_sharded with the REAL per-shard verifier (the HIP kernel
+    through the C ABI, both ranks on the box's one GPU) over a gloo world of 2:
+    every rank's gathered results equal the oracle over the whole batch."""
+    import oracle_ffi as O
+    from ouroboros_network_amd import header as H
+
+    world = 2
+    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path), True), nprocs=world, join=True)
+    hs = kats["headers"] * 2
+    parsed = [H.parse_header(bytes.fromhex(h["raw"])) for h in hs]
+    ea = [bytes.fromhex(h["eta_alpha"]) for h in hs]
+    la = [bytes.fromhex(h["leader_alpha"]) for h in hs]
+    la[3] = bytes(32)
+    want = O.tpraos_verify_batch(H.pack(parsed, ea, la, slots_per_kes_period=100))
+    for r in range(world):
+        np.testing.assert_array_equal(np.load(tmp_path / f"v{r}.npy"), want[0])
+        np.testing.assert_array_equal(np.load(tmp_path / f"be{r}.npy"), want[1])
+        np.testing.assert_array_equal(np.load(tmp_path / f"bl{r}.npy"), want[2])
 
 
 def _nccl_worker(rank, world, port, out_dir):

@@ -51,7 +51,7 @@ def main():
     v, be, bl = np.zeros(1, np.uint8), np.zeros((1, 64), np.uint8), np.zeros((1, 64), np.uint8)
     d.dh_tpraos_verify.argtypes = [ctypes.c_void_p, ctypes.c_int] + [ctypes.c_void_p] * 3
     hdr = measure(lambda: d.dh_tpraos_verify(ctypes.addressof(st), 0, O.p(v), O.p(be), O.p(bl)))
-    assert int(v[0]) == 15
+    assert int(v[0]) & 0x0F == 15
     res = {"ed25519_verify": ed, "vrf03_verify": vrf, "sum6kes_verify": kes,
            "tpraos_header (throughput schedule)": hdr,
            "canonical_M (SURVEY.md §8(d))": {"ed25519": 2983, "vrf": 7325, "header": 20616}}
