@@ -19,8 +19,11 @@ from __future__ import annotations
 
 import argparse
 import ctypes
+import hashlib
 import json
+import math
 import os
+import subprocess
 import sys
 import time
 
@@ -135,6 +138,66 @@ class DeviceHeaders:
             body_len=h("body_len", np.uint32))
 
 
+def source_hash() -> str:
+    """sha256 over the product's device/host sources (csrc/, include/): ties a
+    committed PMC traffic figure to the code it was measured on."""
+    h = hashlib.sha256()
+    for d in (os.path.join(ROOT, "ouroboros-network_amd", "csrc"), os.path.join(ROOT, "include")):
+        for name in sorted(os.listdir(d)):
+            if name.endswith((".h", ".hip")) and not name.startswith(("devhost", "synth")):
+                with open(os.path.join(d, name), "rb") as f:
+                    h.update(name.encode() + b"\0" + f.read())
+    return h.hexdigest()[:16]
+
+
+def host_cpu_info() -> dict:
+    """The host the CPU baselines run on: model, nproc, the
+    CPUs this process may run on (affinity) and the cgroup CPU quota; `usable`
+    = the cores the baselines use (the box gives a job a share of a larger
+    machine, so nproc alone would oversubscribe it)."""
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    nproc = os.cpu_count() or 1
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = nproc
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+            if q != "max":
+                quota = int(q) / int(per)
+    except (OSError, ValueError):
+        pass
+    usable = min(aff, math.ceil(quota)) if quota else aff
+    return {"model": model, "nproc": nproc, "affinity_cpus": aff, "cgroup_cpu_quota": quota,
+            "usable": max(1, usable)}
+
+
+def native_oracle(O) -> str:
+    """Load the oracle built -O3 -march=native on THIS host (make -C oracle
+    native); falls back to the shipped x86-64-v2 build."""
+    try:
+        r = subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle"), "native"],
+                           capture_output=True, timeout=180)
+        path = os.path.join(ROOT, "oracle", "build", "liboracle_native.so")
+        if r.returncode == 0 and os.path.exists(path):
+            O.lib(path)
+            return "gcc -O3 -march=native (built on this host)"
+    except (OSError, subprocess.SubprocessError):
+        pass
+    O.lib()
+    return "gcc -O3 -march=x86-64-v2 (native build failed)"
+
+
 def measure_peak_mac(device) -> float:
     """Live v_mad_u64_u32 rate (TMAC/s) from the microbenchmark kernel."""
     lib = ctypes.CDLL(SYNTH_SO)
@@ -144,7 +207,8 @@ def measure_peak_mac(device) -> float:
 
 
 def ed25519_rate(device, n: int, reps: int):
-    """Ed25519 verifies/s on n device-resident synthetic signatures."""
+    """Ed25519 verifies/s on n device-resident synthetic signatures; returns
+    (result, (pk, sig, msg) device tensors)."""
     import torch
 
     from ouroboros_network_amd import _native
@@ -180,59 +244,48 @@ def ed25519_rate(device, n: int, reps: int):
     out = {"value": n / (ms * 1e-3), "unit": "verifies/s", "n": n, "ms_per_launch": ms,
            "all_valid": ok == n,
            "roofline_frac": (n * MACS_PER_ED25519 / (ms * 1e-3) / 1e12)}
-    m = min(n, 65536)
-    try:
-        out["cpu_libsodium"] = libsodium_ed25519_rate(pk[: m * 32].cpu().numpy(),
-                                                      sig[: m * 64].cpu().numpy(),
-                                                      msg[: m * 32].cpu().numpy(),
-                                                      min(16, os.cpu_count() or 1))
-    except Exception as e:  # noqa: BLE001
-        out["cpu_libsodium"] = {"error": str(e)}
-    return out
+    return out, (pk, sig, msg)
 
 
 SODIUM_SO = "/opt/conda/lib/libsodium.so.23"
 
 
-def libsodium_ed25519_rate(pk, sig, msg, threads: int):
+def libsodium_ed25519_rate(pk, sig, msg, cpu: dict, n: int):
     """the function the reference calls for Ed25519,
     libsodium 1.0.18's crypto_sign_ed25519_verify_detached (the CI pin), timed
-    on the host cores over the same synthetic signatures the GPU leg verified.
-    ctypes drops the GIL for the call, so one Python thread per core runs the
-    library concurrently.  A CPU baseline only -- never the measured path."""
-    from concurrent.futures import ThreadPoolExecutor
+    on the host cores over the first n of the same synthetic signatures the
+    GPU leg verified, by the oracle library's C pthread pool (dlopen of the
+    library; no Python per item).  A CPU baseline only -- never the measured
+    path."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_ffi as O
 
     if not os.path.exists(SODIUM_SO):
         return {"error": f"{SODIUM_SO} absent on this host"}
-    so = ctypes.CDLL(SODIUM_SO)
-    if so.sodium_init() < 0:
-        return {"error": "sodium_init failed"}
-    fn = so.crypto_sign_ed25519_verify_detached
-    fn.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_ulonglong, ctypes.c_char_p]
-    fn.restype = ctypes.c_int
-    m = len(pk) // 32
-    pkb, sgb, msb = pk.tobytes(), sig.tobytes(), msg.tobytes()
-    items = [(sgb[i * 64:(i + 1) * 64], msb[i * 32:(i + 1) * 32], pkb[i * 32:(i + 1) * 32])
-             for i in range(m)]
+    pk, sig, msg = (np.ascontiguousarray(x[: n * w].cpu().numpy()) for x, w in
+                    ((pk, 32), (sig, 64), (msg, 32)))
+    ver = np.zeros(n, np.uint8)
 
-    def run(lo, hi):
-        return sum(1 for s, g, p in items[lo:hi] if fn(s, g, 32, p) == 0)
-
-    def timed(k, nthreads):
-        step = (k + nthreads - 1) // nthreads
+    def timed(k, threads):
         t0 = time.perf_counter()
-        with ThreadPoolExecutor(nthreads) as ex:
-            acc = sum(ex.map(lambda j: run(j * step, min(k, (j + 1) * step)), range(nthreads)))
-        return k / (time.perf_counter() - t0), acc
+        rc = O.lib().orc_sodium_ed25519_verify_batch(SODIUM_SO.encode(), k, O.p(pk), O.p(sig),
+                                                     O.p(msg), O.p(ver), threads)
+        dt = time.perf_counter() - t0
+        if rc != 0:
+            raise RuntimeError("dlopen of libsodium failed")
+        return k / dt, int(ver[:k].sum())
 
-    rate, acc = timed(m, threads)
-    m1 = min(m, 4096)
-    rate1, acc1 = timed(m1, 1)
+    threads = cpu["usable"]
+    timed(min(n, 4096), threads)  # warm: pages, library init
+    rate, acc = timed(n, threads)
+    n1 = max(1, n // 16)
+    rate1, acc1 = timed(n1, 1)
     return {"value": round(rate, 1), "unit": "verifies/s", "cores": threads, "kind": "reference",
-            "sample": f"first {m} of the same synthetic signatures (32-B messages), "
-                      f"libsodium 1.0.18 crypto_sign_ed25519_verify_detached via ctypes",
-            "one_core": round(rate1, 1), "one_core_sample": m1,
-            "accepts_all": acc == m and acc1 == m1}
+            "sample": f"first {n} of the same synthetic signatures (32-B messages), libsodium "
+                      f"1.0.18 crypto_sign_ed25519_verify_detached from a C pthread pool",
+            "one_core": round(rate1, 1), "one_core_sample": n1,
+            "thread_scaling": round(rate / rate1, 2),
+            "accepts_all": acc == n and acc1 == n1}
 
 
 def component_rates(hdr, n: int, reps: int = 3):
@@ -404,7 +457,8 @@ def e2e_leg(hdr, n: int, reps: int = 3):
     from ouroboros_network_amd.tpraos import verify_headers
 
     hb = hdr.host_sample(n)
-    in_bytes = sum(getattr(hb, k).nbytes for k in hb.__dataclass_fields__)
+    in_bytes = sum(getattr(hb, k).nbytes for k in hb.__dataclass_fields__
+                   if getattr(hb, k) is not None)
     dv = hdr.verdict.cpu().numpy()
     dbe = hdr.beta_eta.cpu().numpy().reshape(n, 64)
     dbl = hdr.beta_leader.cpu().numpy().reshape(n, 64)
@@ -437,14 +491,65 @@ def e2e_leg(hdr, n: int, reps: int = 3):
 
 
 def load_pmc_traffic():
-    """HBM bytes per launch of the header kernel from the committed PMC run."""
+    """HBM bytes per header of one header-kernel launch from the committed PMC
+    run (profiles/pmc_traffic.json, tools/summarize_profile.py), with whether
+    that run measured THIS source (its stamped source_hash)."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         with open(path) as f:
             d = json.load(f)
-        return d.get("k_tpraos_verify_bytes_per_launch_per_header")
     except (OSError, ValueError):
-        return None
+        return None, {}
+    return d.get("k_tpraos_verify_bytes_per_launch_per_header"), {
+        "traffic_round": d.get("round"), "traffic_source_hash": d.get("source_hash"),
+        "traffic_matches_source": d.get("source_hash") == source_hash()}
+
+
+def single_item_leg(ed, hdr, iters: int = 300):
+    """Per-call wall latency of the ABI-identical single-item symbols (each a
+    one-item GPU batch: H2D, launch, D2H) next to the reference's own
+    libsodium call on the host -- the number a per-item Haskell FFI caller
+    would see (INTEGRATION.md steers such callers to batches)."""
+    from ouroboros_network_amd import _native
+
+    lib = _native.load()
+    pk, sig, msg = (x[: iters * w].cpu().numpy().tobytes() for x, w in
+                    ((ed[0], 32), (ed[1], 64), (ed[2], 32)))
+    items = [(sig[64 * i:64 * i + 64], msg[32 * i:32 * i + 32], pk[32 * i:32 * i + 32])
+             for i in range(iters)]
+    vk = hdr.t["vrf_vk"][: iters * 32].cpu().numpy().tobytes()
+    pi = hdr.t["eta_proof"][: iters * 80].cpu().numpy().tobytes()
+    al = hdr.t["eta_alpha"][: iters * 32].cpu().numpy().tobytes()
+    vitems = [(vk[32 * i:32 * i + 32], pi[80 * i:80 * i + 80], al[32 * i:32 * i + 32])
+              for i in range(iters)]
+    out = ctypes.create_string_buffer(64)
+
+    def lat(fn):
+        fn(0)
+        t = np.empty(iters)
+        for i in range(iters):
+            t0 = time.perf_counter()
+            rc = fn(i)
+            t[i] = time.perf_counter() - t0
+            if rc != 0:
+                raise RuntimeError(f"single-item call rejected a valid item ({rc})")
+        return {"p50_us": round(float(np.percentile(t, 50)) * 1e6, 1),
+                "p99_us": round(float(np.percentile(t, 99)) * 1e6, 1)}
+
+    res = {"workload": f"{iters} single-item calls, valid synthetic items, one thread",
+           "ouro_ed25519_verify": lat(lambda i: lib.ouro_ed25519_verify(
+               items[i][0], items[i][1], 32, items[i][2])),
+           "crypto_vrf_ietfdraft03_verify": lat(lambda i: lib.crypto_vrf_ietfdraft03_verify(
+               out, vitems[i][0], vitems[i][1], vitems[i][2], 32))}
+    if os.path.exists(SODIUM_SO):
+        so = ctypes.CDLL(SODIUM_SO)
+        so.sodium_init()
+        fn = so.crypto_sign_ed25519_verify_detached
+        fn.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_ulonglong, ctypes.c_char_p]
+        res["libsodium_ed25519_host"] = lat(lambda i: fn(items[i][0], items[i][1], 32,
+                                                         items[i][2]))
+        res["libsodium_ed25519_host"]["kind"] = "reference (ctypes per call, ~1 us of it)"
+    return res
 
 
 def main():
@@ -452,7 +557,11 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--headers", type=int, default=1 << 20, help="headers per GPU per step")
+    ap.add_argument("--headers", type=int, default=1 << 20,
+                    help="headers per GPU per step (weak scaling)")
+    ap.add_argument("--global-headers", type=int, default=0,
+                    help="strong scaling: ONE batch of this many headers per step, cut into "
+                         "N/G contiguous shards (configs[3] as written: 1,048,576 over G GPUs)")
     ap.add_argument("--pools", type=int, default=1024)
     ap.add_argument("--cpu-sample", type=int, default=65536)
     ap.add_argument("--no-cpu", action="store_true")
@@ -490,16 +599,23 @@ def main():
         else:
             dist.init_process_group(args.dist_backend)
 
-    n = args.headers
-    # each rank synthesises its own contiguous shard: global headers
-    # [rank*n, (rank+1)*n), seeds indexed by the global header number
+    from ouroboros_network_amd.shard import all_gather_results, pack_results, shard_range
+
+    strong = args.global_headers > 0
+    if strong:
+        # one global batch, N/G contiguous headers per rank
+        lo, hi = shard_range(args.global_headers, world, rank)
+        n, first, n_global = hi - lo, lo, args.global_headers
+        if n == 0:
+            raise SystemExit("more ranks than headers")
+    else:
+        # each rank its own shard of n: global headers [rank*n, (rank+1)*n)
+        n, first, n_global = args.headers, rank * args.headers, args.headers * world
     t_syn = time.perf_counter()
-    tensors, blen = synth_headers(n, args.pools, device, first=rank * n)
+    tensors, blen = synth_headers(n, args.pools, device, first=first)
     syn_s = time.perf_counter() - t_syn
     hdr = DeviceHeaders(tensors, n, device)
     stream = torch.cuda.current_stream()
-
-    from ouroboros_network_amd.shard import all_gather_results, pack_results
 
     def gather():
         # the one collective of the path: every rank receives all verdicts and
@@ -507,7 +623,7 @@ def main():
         local = pack_results(hdr.verdict, hdr.beta_eta, hdr.beta_leader)
         if args.dist_backend != "nccl":
             local = local.cpu()
-        return all_gather_results(local, n * world, world)
+        return all_gather_results(local, n_global, world)
 
     # the collective of step k runs on its own stream, overlapped with the
     # kernel of step k+1 (double-buffered outputs); a set is rewritten only
@@ -522,9 +638,6 @@ def main():
         hdr.use(s)
         hdr.launch(stream)
         if world > 1:
-            if comm is None:
-                gather()
-                return
             kev = torch.cuda.Event()
             kev.record(stream)
             with torch.cuda.stream(comm):
@@ -555,15 +668,12 @@ def main():
         hdr.launch(stream)
         ev[k][1].record(stream)
         if world > 1:
-            if comm is None:
+            with torch.cuda.stream(comm):
+                comm.wait_event(ev[k][1])
                 gather()
-            else:
-                with torch.cuda.stream(comm):
-                    comm.wait_event(ev[k][1])
-                    gather()
-                    done = torch.cuda.Event()
-                    done.record(comm)
-                    gdone[s] = done
+                done = torch.cuda.Event()
+                done.record(comm)
+                gdone[s] = done
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -578,7 +688,7 @@ def main():
         dist.all_reduce(ok_t, op=dist.ReduceOp.MIN)
         all_ok = bool(ok_t.item())
 
-    total = n * world * args.steps
+    total = n_global * args.steps
     value = total / elapsed
     ms_per_step = elapsed / args.steps * 1e3
 
@@ -589,7 +699,7 @@ def main():
         except Exception as e:  # noqa: BLE001
             print(f"# peak microbench failed: {e}", file=sys.stderr)
         achieved = n * MACS_PER_HEADER / (kern_ms * 1e-3) / 1e12
-        traffic_per_header = load_pmc_traffic()
+        traffic_per_header, traffic_meta = load_pmc_traffic()
         roof = {
             "bound": "valu",
             "kernel": "k_tpraos_verify",
@@ -597,9 +707,13 @@ def main():
             "peak": round(peak, 3) if peak else None,
             "unit": "TMAC/s",
             "frac": round(achieved / peak, 4) if peak else None,
-            "traffic": (traffic_per_header * n if traffic_per_header else None),
+            "traffic": (round(traffic_per_header * n) if traffic_per_header else None),
+            "traffic_per_header": (round(traffic_per_header, 1) if traffic_per_header else None),
+            "algorithmic_bytes_per_header": 1537,
             "macs_per_header": MACS_PER_HEADER,
             "kernel_ms_per_launch": round(kern_ms, 3),
+            "source_hash": source_hash(),
+            **traffic_meta,
         }
         out = {
             "metric": METRIC,
@@ -610,23 +724,31 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 3),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if strong else "weak",
             "vs_baseline": None,
             "dtype": "u32/u64 (GF(2^255-19) int limbs)",
             "data": "synthetic (device-signed, deterministic seeds)",
             "config": {"workload": "tpraos_header_batch (configs[3])",
-                       "headers_per_gpu": n, "global_batch": n * world,
+                       "headers_per_gpu": n, "global_batch": n_global,
                        "pools": args.pools, "body_bytes": blen,
                        "parallelism": f"shard{world}"},
             "all_valid": all_ok,
             "synth_s": round(syn_s, 2),
             "roofline": roof,
         }
+        cpu = host_cpu_info()
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import oracle_ffi as O
+
+        oracle_build = native_oracle(O) if not args.no_cpu else None
+        ed = None
         if not args.no_extras:
             try:
-                out["ed25519"] = ed25519_rate(device, 1 << 20, 3)
+                out["ed25519"], ed = ed25519_rate(device, 1 << 20, 3)
                 if peak:
                     out["ed25519"]["roofline_frac"] = round(out["ed25519"]["roofline_frac"] / peak, 4)
+                if not args.no_cpu and world == 1:
+                    out["ed25519"]["cpu_libsodium"] = libsodium_ed25519_rate(*ed, cpu, 262144)
             except Exception as e:  # noqa: BLE001
                 out["ed25519"] = {"error": str(e)}
             try:
@@ -637,6 +759,11 @@ def main():
                     out[k] = val
             except Exception as e:  # noqa: BLE001
                 out["components_error"] = str(e)
+            if ed is not None and world == 1:
+                try:
+                    out["single_item"] = single_item_leg(ed, hdr)
+                except Exception as e:  # noqa: BLE001
+                    out["single_item"] = {"error": str(e)}
         if not args.no_e2e and world == 1:
             try:
                 out["e2e"] = e2e_leg(hdr, n)
@@ -644,25 +771,31 @@ def main():
                 out["e2e"] = {"error": str(e)}
         if not args.no_latency and world == 1:
             try:
-                out["latency"] = latency_leg(hdr, 64, args.lat_iters, min(16, os.cpu_count() or 1),
+                out["latency"] = latency_leg(hdr, 64, args.lat_iters, cpu["usable"],
                                              args.lat_cpu_iters)
             except Exception as e:  # noqa: BLE001
                 out["latency"] = {"error": str(e)}
         if not args.no_cpu and world == 1:
-            threads = min(16, os.cpu_count() or 1)
+            threads = cpu["usable"]
             m = min(args.cpu_sample, n)
             hb = hdr.host_sample(m)
             rate, dt, (cv, cbe, cbl) = cpu_baseline(hb, threads)
-            rate1, dt1, _ = cpu_baseline(hb.slice(0, min(512, m)), 1)
+            m1 = min(2048, m)
+            rate1, dt1, _ = cpu_baseline(hb.slice(0, m1), 1)
             gv = hdr.verdict[:m].cpu().numpy()
             gbe = hdr.beta_eta[: m * 64].cpu().numpy().reshape(m, 64)
             gbl = hdr.beta_leader[: m * 64].cpu().numpy().reshape(m, 64)
             out["cpu_baseline"] = {
                 "value": round(rate, 1), "unit": "headers/s", "cores": threads,
                 "kind": "port",
-                "sample": f"first {m} of the same synthetic headers, oracle/ C port, "
-                          f"{threads} threads, {dt:.1f} s wall",
-                "one_core": round(rate1, 1),
+                "sample": f"first {m} of the same synthetic headers, oracle/ C port "
+                          f"({oracle_build}), {threads} pthreads, {dt:.1f} s wall",
+                "one_core": round(rate1, 1), "one_core_sample": m1,
+                "thread_scaling": round(rate / rate1, 2),
+                "host": cpu,
+                "why_port": "the reference's VRF C (cardano-crypto-praos) is not in the image; "
+                            "the oracle restates it and is pinned to libsodium 1.0.18 + golden "
+                            "vectors (DESIGN.md §2)",
                 "gpu_equals_cpu_on_sample": bool((gv == cv).all() and (gbe == cbe).all()
                                                  and (gbl == cbl).all()),
             }

@@ -9,6 +9,7 @@
  *   seed(tag, i) = SHA-512("ouro-mi355x/" || tag || LE64(i))[0:32]
  */
 #include "internal.h"
+#include <dlfcn.h>
 #include <pthread.h>
 #include <stdatomic.h>
 #include <stdlib.h>
@@ -140,6 +141,37 @@ void orc_tpraos_verify_batch(const orc_tpraos_batch *b, uint8_t *verdict, uint8_
                              uint8_t *beta_leader, int threads) {
   hdr_ctx c = {b, verdict, beta_eta, beta_leader};
   run_pool(hdr_item, &c, b->n, threads);
+}
+
+/* --------------------------------------- libsodium (the reference's) ---- */
+/* bench.py's cpu_baseline for Ed25519: the function the
+ * reference's Ed25519DSIGN binds, libsodium 1.0.18's
+ * crypto_sign_ed25519_verify_detached, driven by the same pthread pool (no
+ * Python per item).  `so_path` is dlopen()ed; returns -1 if it cannot be. */
+typedef int (*sodium_verify_fn)(const unsigned char *, const unsigned char *,
+                                unsigned long long, const unsigned char *);
+typedef struct {
+  sodium_verify_fn fn;
+  const uint8_t *pk, *sig, *msg;
+  uint8_t *verdict;
+} sodium_ctx;
+
+static void sodium_item(void *c, size_t i) {
+  sodium_ctx *x = (sodium_ctx *)c;
+  x->verdict[i] = x->fn(x->sig + 64 * i, x->msg + 32 * i, 32, x->pk + 32 * i) == 0;
+}
+
+int orc_sodium_ed25519_verify_batch(const char *so_path, size_t n, const uint8_t *pk,
+                                    const uint8_t *sig, const uint8_t *msg32, uint8_t *verdict,
+                                    int threads) {
+  void *h = dlopen(so_path, RTLD_NOW | RTLD_LOCAL);
+  if (!h) return -1;
+  int (*init)(void) = (int (*)(void))dlsym(h, "sodium_init");
+  sodium_verify_fn fn = (sodium_verify_fn)dlsym(h, "crypto_sign_ed25519_verify_detached");
+  if (!init || !fn || init() < 0) return -1;
+  sodium_ctx c = {fn, pk, sig, msg32, verdict};
+  run_pool(sodium_item, &c, n, threads);
+  return 0; /* the handle stays open: the library is process-wide */
 }
 
 /* ---------------------------------------------------------- synthesis ---- */

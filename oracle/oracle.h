@@ -131,6 +131,12 @@ void orc_sum6kes_verify_batch(size_t n, const uint8_t *vk, const uint32_t *t,
 void orc_tpraos_verify_batch(const orc_tpraos_batch *b, uint8_t *verdict, uint8_t *beta_eta,
                              uint8_t *beta_leader, int threads);
 
+/* libsodium's crypto_sign_ed25519_verify_detached over a batch (dlopen of
+ * so_path), the reference's own Ed25519 for the CPU baseline; -1 if absent */
+int orc_sodium_ed25519_verify_batch(const char *so_path, size_t n, const uint8_t *pk,
+                                    const uint8_t *sig, const uint8_t *msg32, uint8_t *verdict,
+                                    int threads);
+
 /* synthesis helpers (threaded) used by tests to build inputs;
  * seed(tag, i) = SHA-512("ouro-mi355x/" || tag zero-padded to 12 B || LE64(i))[0:32] */
 void orc_seed(uint8_t out[32], const char *tag, uint64_t i);

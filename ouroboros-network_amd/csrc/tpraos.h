@@ -363,14 +363,19 @@ OURO_FI void st_words(uint8_t* p, const uint32_t* w, int n16) {
 // The VRF input of header i: mkSeed seedEta / seedL slot eta0 on the device
 // (Shelley/Protocol.hs:409-410; blake2b.h mkseed_hash) when the batch carries
 // slots, else the caller's 32 bytes.
+// (out of line: the Blake2b state stays out of the cores' register budget)
+OURO_NI void hdr_mkseed(uint32_t a[8], const ouro_tpraos_batch& b, size_t i, bool leader,
+                        uint32_t opts) {
+  uint32_t e0[8];
+  if (opts & kOptEpochNonce) ld_words(e0, b.epoch_nonce, 2);
+  mkseed_hash(a, b.slot[i], (opts & kOptEpochNonce) ? e0 : nullptr);
+#pragma unroll
+  for (int k = 0; k < 8; k++) a[k] ^= leader ? kSeedL[k] : kSeedEta[k];
+}
 OURO_HD inline void hdr_seed(SeedMsg& a, const ouro_tpraos_batch& b, size_t i, bool leader,
                              uint32_t opts) {
   if (opts & kOptSeeds) {
-    uint32_t e0[8];
-    if (opts & kOptEpochNonce) ld_words(e0, b.epoch_nonce, 2);
-    mkseed_hash(a.w, b.slot[i], (opts & kOptEpochNonce) ? e0 : nullptr);
-#pragma unroll
-    for (int k = 0; k < 8; k++) a.w[k] ^= leader ? kSeedL[k] : kSeedEta[k];
+    hdr_mkseed(a.w, b, i, leader, opts);
   } else {
     ld_words(a.w, (leader ? b.leader_alpha : b.eta_alpha) + 32 * i, 2);
   }
@@ -420,9 +425,16 @@ OURO_HD inline void hdr_core(const ouro_tpraos_batch& b, size_t i, uint32_t opts
       uint32_t p[8], pi[20];
       ld_words(p, b.vrf_vk + 32 * i, 2);
       ld_words(pi, (leader ? b.leader_proof : b.eta_proof) + 80 * i, 5);
-      SeedMsg a{};  // the 32-byte VRF input, in registers
-      if (!gamma) hdr_seed(a, b, i, leader, opts);
-      flag = vrf_v_core(p, pi, a, 32, lane, btab, res,
+      // the 32-byte VRF input: the caller's alpha, or mkSeed's output staged
+      // in the lane slot's (still free) result area
+      const uint8_t* a = (leader ? b.leader_alpha : b.eta_alpha) + 32 * i;
+      if ((opts & kOptSeeds) && !gamma) {
+        uint32_t w[8];
+        hdr_mkseed(w, b, i, leader, opts);
+        st_words8(lane + kSlotOut, w);
+        a = reinterpret_cast<const uint8_t*>(lane + kSlotOut);
+      }
+      flag = vrf_v_core(p, pi, ShaGlobalTail{a}, 32, lane, btab, res,
                         leader ? kPtHl : kPtHe, leader ? kPtVl : kPtVe,
                         leader ? kPtG8l : kPtG8e, gamma ? 2 : (split ? 1 : 0),
                         res + kLatPart + (leader ? kPtWords : 0), quad);
@@ -449,8 +461,8 @@ OURO_HD inline uint32_t hdr_claim_bit(const ouro_tpraos_batch& b, size_t i, uint
 // consumes: Blake2b-256 of the CLAIMED output when the batch carries it (the
 // reference's PRTCL rule hashes VRF.certifiedOutput of bheaderEta), else of
 // the computed beta_eta (zeros for a failed proof: the header is invalid).
-OURO_HD inline void hdr_eta_nonce(const ouro_tpraos_batch& b, size_t i, uint32_t opts,
-                                  const uint32_t beta_e[16]) {
+OURO_NI void hdr_eta_nonce(const ouro_tpraos_batch& b, size_t i, uint32_t opts,
+                           const uint32_t beta_e[16]) {
   if (!(opts & kOptEtaNonce)) return;
   uint32_t in[16], h[8];
   if (opts & kOptEtaClaim) {
@@ -461,6 +473,21 @@ OURO_HD inline void hdr_eta_nonce(const ouro_tpraos_batch& b, size_t i, uint32_t
   }
   blake2b256_64(h, in);
   st_words(b.eta_nonce + 32 * i, h, 2);
+}
+
+// The claimed-output bits and the eta nonce of header i, re-reading the
+// outputs the finish has just stored: out of line, so neither the comparison
+// nor the Blake2b state lengthens the finish's live ranges (scratch frame).
+constexpr uint32_t kOptPost = kOptEtaClaim | kOptLeaderClaim | kOptEtaNonce;
+OURO_NI void hdr_post(const ouro_tpraos_batch& b, size_t i, uint32_t opts, uint8_t* verdict,
+                      const uint8_t* beta_eta, const uint8_t* beta_leader) {
+  uint32_t v = verdict[i], be[16], bl[16];
+  ld_words(be, beta_eta + 64 * i, 4);
+  ld_words(bl, beta_leader + 64 * i, 4);
+  v |= hdr_claim_bit(b, i, opts, 0, (v & 0x04u) != 0, be);
+  v |= hdr_claim_bit(b, i, opts, 1, (v & 0x08u) != 0, bl);
+  hdr_eta_nonce(b, i, opts, be);
+  verdict[i] = (uint8_t)v;
 }
 
 // latency-mode finish of header i, VRF by VRF (the host form of the lane-pair
@@ -489,13 +516,13 @@ OURO_HD inline void hdr_finish_item(const ouro_tpraos_batch& b, size_t i, uint32
   uint32_t pie[20], pil[20], be[16], bl[16];
   ld_words(pie, b.eta_proof + 80 * i, 5);
   ld_words(pil, b.leader_proof + 80 * i, 5);
-  uint32_t v = hdr_finish(res, tmp, pie, pil, be, bl);
-  v |= hdr_claim_bit(b, i, opts, 0, (v & 0x04u) != 0, be);
-  v |= hdr_claim_bit(b, i, opts, 1, (v & 0x08u) != 0, bl);
-  hdr_eta_nonce(b, i, opts, be);
+  const uint32_t v = hdr_finish(res, tmp, pie, pil, be, bl);
   if (beta_eta) st_words(beta_eta + 64 * i, be, 4);
   if (beta_leader) st_words(beta_leader + 64 * i, bl, 4);
   verdict[i] = (uint8_t)v;
+  // claimed outputs / eta nonce: from the results just stored (both outputs
+  // are required then; the kernels always pass them)
+  if (opts & kOptPost) hdr_post(b, i, opts, verdict, beta_eta, beta_leader);
 }
 
 

@@ -16,15 +16,23 @@ ORACLE_SO = os.path.join(ROOT, "oracle", "build", "liboracle.so")
 SODIUM_SO = "/opt/conda/lib/libsodium.so.23"
 
 _lib = None
+_path = None
 
 
-def lib() -> ctypes.CDLL:
-    global _lib
+def lib(path: str = None) -> ctypes.CDLL:
+    """The oracle library (once per process).  `path` picks a build variant
+    (bench.py: the -O3 -march=native build; the ASan build in the sanitizer
+    test); the default is oracle/build/liboracle.so."""
+    global _lib, _path
+    if _lib is not None and path not in (None, _path):
+        raise RuntimeError(f"oracle already loaded from {_path}")
     if _lib is None:
-        if not os.path.exists(ORACLE_SO):
+        path = path or ORACLE_SO
+        if path == ORACLE_SO and not os.path.exists(ORACLE_SO):
             subprocess.run(["make", "-C", os.path.join(ROOT, "oracle")], check=True,
                            stdout=subprocess.DEVNULL)
-        _lib = ctypes.CDLL(ORACLE_SO)
+        _lib = ctypes.CDLL(path)
+        _path = path
         P, SZ, I = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int
         sig = {
             "orc_sha512": (None, [P, P, SZ]),
@@ -49,6 +57,7 @@ def lib() -> ctypes.CDLL:
             "orc_synth_vrf": (None, [SZ, ctypes.c_uint64, P, P, P, I]),
             "orc_mk_nonce_from_number": (None, [P, ctypes.c_uint64]),
             "orc_mk_seed": (None, [P, P, ctypes.c_uint64, P]),
+            "orc_sodium_ed25519_verify_batch": (I, [ctypes.c_char_p, SZ, P, P, P, P, I]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(_lib, name)

@@ -64,10 +64,19 @@ def main():
                                                    "SQ_ACTIVE_INST_ANY", "SQ_ACTIVE_INST_VALU")
                             if k in sq}
         out["valu_insts_per_header"] = sq.get("SQ_INSTS_VALU", 0) * 64 / args.pmc_headers / 64
+    # the source the PMC passes measured: bench.py stamps it into its JSON line
+    src = None
+    bj = os.path.join(d, "bench_under_rocprof.json")
+    if os.path.exists(bj):
+        with open(bj) as f:
+            lines = [ln for ln in f.read().splitlines() if ln.startswith("{")]
+        if lines:
+            src = json.loads(lines[-1]).get("roofline", {}).get("source_hash")
+    out["source_hash"] = src
     with open(os.path.join(d, "summary.json"), "w") as f:
         json.dump(out, f, indent=1, sort_keys=True)
     with open(os.path.join(ROOT, "profiles", "pmc_traffic.json"), "w") as f:
-        json.dump({"round": args.round,
+        json.dump({"round": args.round, "source_hash": src,
                    "k_tpraos_verify_bytes_per_launch_per_header": hbm / args.pmc_headers}, f, indent=1)
     print(json.dumps(out, indent=1, sort_keys=True))
 
