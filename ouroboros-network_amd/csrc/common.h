@@ -26,4 +26,44 @@ OURO_FI void bytes_to_words8(uint32_t w[8], const uint8_t* p) {
 
 OURO_FI uint32_t byte_of(const uint32_t* w, int i) { return (w[i >> 2] >> (8 * (i & 3))) & 0xffu; }
 
+// ---- global-memory accessors --------------------------------------------------
+// Every buffer the lane routines touch (inputs, outputs, scratch slots, the B
+// tables) is device global memory, but a pointer that crosses an out-of-line
+// call or a struct is generic to LLVM, which then emits FLAT instructions:
+// those count on both vmcnt and lgkmcnt, so any s_waitcnt lgkmcnt(0) for a
+// scalar load also waits for every table prefetch in flight.  These accessors
+// cast to address space 1 (global_load / global_store, vmcnt only).
+#if defined(__HIP_DEVICE_COMPILE__)
+#define OURO_AS1 __attribute__((address_space(1)))
+typedef int ouro_v4i __attribute__((ext_vector_type(4)));
+typedef int ouro_v2i __attribute__((ext_vector_type(2)));
+OURO_FI int4 ldg4(const void* p) {
+  const ouro_v4i v = *(const OURO_AS1 ouro_v4i*)p;
+  return make_int4(v.x, v.y, v.z, v.w);
+}
+OURO_FI int2 ldg2(const void* p) {
+  const ouro_v2i v = *(const OURO_AS1 ouro_v2i*)p;
+  return make_int2(v.x, v.y);
+}
+OURO_FI int32_t ldg1(const void* p) { return *(const OURO_AS1 int32_t*)p; }
+OURO_FI uint64_t ldg8(const void* p) { return *(const OURO_AS1 uint64_t*)p; }
+OURO_FI uint32_t ldg_u8(const void* p) { return *(const OURO_AS1 uint8_t*)p; }
+OURO_FI void stg4(void* p, int4 v) {
+  *(OURO_AS1 ouro_v4i*)p = ouro_v4i{v.x, v.y, v.z, v.w};
+}
+OURO_FI void stg2(void* p, int2 v) { *(OURO_AS1 ouro_v2i*)p = ouro_v2i{v.x, v.y}; }
+OURO_FI void stg1(void* p, int32_t v) { *(OURO_AS1 int32_t*)p = v; }
+OURO_FI void stg8(void* p, uint64_t v) { *(OURO_AS1 uint64_t*)p = v; }
+#else
+OURO_FI int4 ldg4(const void* p) { return *static_cast<const int4*>(p); }
+OURO_FI int2 ldg2(const void* p) { return *static_cast<const int2*>(p); }
+OURO_FI int32_t ldg1(const void* p) { return *static_cast<const int32_t*>(p); }
+OURO_FI uint64_t ldg8(const void* p) { return *static_cast<const uint64_t*>(p); }
+OURO_FI uint32_t ldg_u8(const void* p) { return *static_cast<const uint8_t*>(p); }
+OURO_FI void stg4(void* p, int4 v) { *static_cast<int4*>(p) = v; }
+OURO_FI void stg2(void* p, int2 v) { *static_cast<int2*>(p) = v; }
+OURO_FI void stg1(void* p, int32_t v) { *static_cast<int32_t*>(p) = v; }
+OURO_FI void stg8(void* p, uint64_t v) { *static_cast<uint64_t*>(p) = v; }
+#endif
+
 }  // namespace ouro

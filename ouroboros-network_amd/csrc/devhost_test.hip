@@ -6,6 +6,7 @@
 // container with no GPU.  It is never linked into, or loaded by, the product
 // library (lib/libouro_verify.so) and launches nothing.
 #include <cstdlib>
+#include <algorithm>
 #include <cstring>
 #include <vector>
 
@@ -56,8 +57,16 @@ const int32_t* host_btab() {
   }();
   return tab.data();
 }
-struct Lane {
-  alignas(16) int32_t w[kLaneWords];
+// one slot (column 0) of a kSlotGroup-slot region, laid out as on the device
+struct SlotRegion {
+  std::vector<int32_t> buf;
+  Slot s;
+  explicit SlotRegion(int slot_words) : buf(slot_region_words(1, slot_words) + 4, 0) {
+    s = Slot{reinterpret_cast<int32_t*>((reinterpret_cast<uintptr_t>(buf.data()) + 15) & ~uintptr_t(15))};
+  }
+};
+struct Lane : SlotRegion {
+  Lane() : SlotRegion(kLaneWords) {}
 };
 fe fe_from_bytes(const uint8_t* b) {
   uint32_t w[8];
@@ -189,7 +198,7 @@ int dh_ed25519_verify(const uint8_t* sig, const uint8_t* m, uint32_t mlen, const
   for (int i = 0; i < 16; i++) s[i] = ld_le32(sig + 4 * i);
   bytes_to_words8(p, pk);
   Lane lane;
-  return ed25519_verify_lane(s, p, ShaGlobalTail{m}, mlen, lane.w, host_btab()) ? 0 : -1;
+  return ed25519_verify_lane(s, p, ShaGlobalTail{m}, mlen, lane.s, host_btab()) ? 0 : -1;
 }
 int dh_vrf03_verify(uint8_t* beta, const uint8_t* pk, const uint8_t* proof, const uint8_t* alpha,
                     uint32_t alen) {
@@ -197,7 +206,7 @@ int dh_vrf03_verify(uint8_t* beta, const uint8_t* pk, const uint8_t* proof, cons
   bytes_to_words8(p, pk);
   for (int i = 0; i < 20; i++) pi[i] = ld_le32(proof + 4 * i);
   Lane lane;
-  bool ok = vrf03_verify_lane(b, p, pi, ShaGlobalTail{alpha}, alen, lane.w, host_btab());
+  bool ok = vrf03_verify_lane(b, p, pi, ShaGlobalTail{alpha}, alen, lane.s, host_btab());
   memcpy(beta, b, 64);
   return ok ? 0 : -1;
 }
@@ -208,7 +217,7 @@ int dh_sum6kes_verify(const uint8_t* vk, uint32_t t, const uint8_t* m, uint32_t 
   alignas(16) uint32_t sw[112];
   memcpy(sw, sig, 448);
   Lane lane;
-  return sum6kes_verify_lane(v, t, sw, ShaGlobalTail{m}, mlen, lane.w, host_btab()) ? 0 : -1;
+  return sum6kes_verify_lane(v, t, sw, ShaGlobalTail{m}, mlen, lane.s, host_btab()) ? 0 : -1;
 }
 // mkSeed through the header kernels' own path (tpraos.h hdr_seed: blake2b.h
 // mkseed_hash and the seedEta / seedL constants); eta0 = NULL: NeutralNonce.
@@ -231,21 +240,21 @@ void dh_mk_seed(uint8_t* out, int leader, uint64_t slot, const uint8_t* eta0) {
 int dh_tpraos_verify(const ouro_tpraos_batch* b, int mode, uint8_t* verdict, uint8_t* beta_eta,
                      uint8_t* beta_leader) {
   std::vector<Lane> lanes(kLatCores);
-  std::vector<int32_t> res(kLatResWords + 4);
-  int32_t* r = reinterpret_cast<int32_t*>((reinterpret_cast<uintptr_t>(res.data()) + 15) & ~uintptr_t(15));
+  SlotRegion rr(kLatResWords);
+  const Slot r = rr.s;
   const uint32_t opts = batch_opts(*b);
   for (size_t i = 0; i < b->n; i++) {
-    memset(r, 0, kLatResWords * sizeof(int32_t));
+    std::fill(rr.buf.begin(), rr.buf.end(), 0);
     const int cores = mode ? kLatCores : kHdrCores;
     for (int core = 0; core < cores; core++)
-      hdr_core(*b, i, opts, core, lanes[mode ? core : 0].w, r, host_btab(), mode == 0, mode != 0,
+      hdr_core(*b, i, opts, core, lanes[mode ? core : 0].s, r, host_btab(), mode == 0, mode != 0,
                mode == 2);
     if (mode == 2) {
       hdr_finish_item_split(*b, i, opts, r, verdict, beta_eta, beta_leader);
       continue;
     }
     if (mode) hdr_combine_split(r);
-    hdr_finish_item(*b, i, opts, r, lanes[0].w, verdict, beta_eta, beta_leader);
+    hdr_finish_item(*b, i, opts, r, lanes[0].s, verdict, beta_eta, beta_leader);
   }
   return 0;
 }

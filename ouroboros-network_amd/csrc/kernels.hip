@@ -33,17 +33,16 @@ constexpr int kHdrLaneWords = kLaneWords + kResWords;
 constexpr int kLatBlock = 64;  // default latency-mode workgroup (lat_block(); A/B: tools/ab_latency.py)
 
 __device__ __forceinline__ void load_words(uint32_t* w, const uint8_t* p, int nwords16) {
-  const uint4* q = reinterpret_cast<const uint4*>(p);
 #pragma unroll
   for (int i = 0; i < nwords16; i++) {
-    uint4 v = q[i];
+    const int4 v = ldg4(p + 16 * i);
     w[4 * i] = v.x; w[4 * i + 1] = v.y; w[4 * i + 2] = v.z; w[4 * i + 3] = v.w;
   }
 }
 __device__ __forceinline__ void store_words(uint8_t* p, const uint32_t* w, int nwords16) {
-  uint4* q = reinterpret_cast<uint4*>(p);
 #pragma unroll
-  for (int i = 0; i < nwords16; i++) q[i] = make_uint4(w[4 * i], w[4 * i + 1], w[4 * i + 2], w[4 * i + 3]);
+  for (int i = 0; i < nwords16; i++)
+    stg4(p + 16 * i, make_int4((int)w[4 * i], (int)w[4 * i + 1], (int)w[4 * i + 2], (int)w[4 * i + 3]));
 }
 
 __device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
@@ -60,7 +59,7 @@ __global__ void __launch_bounds__(kBlock, OURO_WAVES) k_ed25519_verify(
     const int32_t* __restrict__ btab, uint32_t byron) {
   const size_t tid = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   const size_t nth = (size_t)gridDim.x * blockDim.x;
-  int32_t* lane = scratch + tid * kLaneWords;
+  const Slot lane = slot_of(scratch, tid, kLaneWords);
   for (size_t i = tid; i < n; i += nth) {
     uint32_t s[16], p[8];
     load_words(s, sig + 64 * i, 4);
@@ -78,7 +77,7 @@ __global__ void __launch_bounds__(kBlock, OURO_WAVES) k_vrf03_verify(
     uint8_t* __restrict__ verdict, int32_t* scratch, const int32_t* __restrict__ btab) {
   const size_t tid = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   const size_t nth = (size_t)gridDim.x * blockDim.x;
-  int32_t* lane = scratch + tid * kLaneWords;
+  const Slot lane = slot_of(scratch, tid, kLaneWords);
   for (size_t i = tid; i < n; i += nth) {
     uint32_t p[8], pi[20], b[16];
     load_words(p, pk + 32 * i, 2);
@@ -96,7 +95,7 @@ __global__ void __launch_bounds__(kBlock, OURO_WAVES) k_sum6kes_verify(
     uint8_t* __restrict__ verdict, int32_t* scratch, const int32_t* __restrict__ btab) {
   const size_t tid = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   const size_t nth = (size_t)gridDim.x * blockDim.x;
-  int32_t* lane = scratch + tid * kLaneWords;
+  const Slot lane = slot_of(scratch, tid, kLaneWords);
   for (size_t i = tid; i < n; i += nth) {
     uint32_t v[8];
     load_words(v, vk + 32 * i, 2);
@@ -115,7 +114,7 @@ __global__ void __launch_bounds__(kBlock, OURO_WAVES) k_sum6kes_verify(
 #if OURO_HDR_FINISH_NI
 // A/B: the finish (inversion, encodings, hashes) with its own register allocation
 __device__ __noinline__ void hdr_finish_item_ni(const ouro_tpraos_batch& b, size_t i,
-                                                uint32_t opts, const int32_t* res, int32_t* tmp,
+                                                uint32_t opts, Slot res, Slot tmp,
                                                 uint8_t* verdict, uint8_t* beta_eta,
                                                 uint8_t* beta_leader) {
   hdr_finish_item(b, i, opts, res, tmp, verdict, beta_eta, beta_leader);
@@ -132,8 +131,8 @@ __global__ void __launch_bounds__(kBlock, OURO_WAVES) k_tpraos_verify(ouro_tprao
                                                              const int32_t* __restrict__ btab) {
   const size_t tid = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   const size_t nth = (size_t)gridDim.x * blockDim.x;
-  int32_t* lane = scratch + tid * kHdrLaneWords;
-  int32_t* res = lane + kLaneWords;
+  const Slot lane = slot_of(scratch, tid, kHdrLaneWords);
+  const Slot res = lane + kLaneWords;
   const uint32_t opts = batch_opts(b);
   for (size_t i = tid; i < b.n; i += nth) {
 #if OURO_HDR_LOOP
@@ -173,11 +172,11 @@ __global__ void __launch_bounds__(kBlock, OURO_WAVES) k_tpraos_cores(ouro_tpraos
   const int sh = quad ? 2 : 0;
   const size_t tid = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) >> sh;
   const size_t nth = ((size_t)gridDim.x * blockDim.x) >> sh;
-  int32_t* lane = scratch + tid * kLaneWords;
+  const Slot lane = slot_of(scratch, tid, kLaneWords);
   for (size_t w = tid; w < (size_t)kLatCores * n; w += nth) {
     const int core = (int)(w / n);
     const size_t i = w - (size_t)core * n;
-    hdr_core(b, i, opts, core, lane, res_buf + i * kLatResWords, btab, /*share_key=*/false,
+    hdr_core(b, i, opts, core, lane, slot_of(res_buf, i, kLatResWords), btab, /*share_key=*/false,
              /*split=*/true, quad != 0);
   }
 }
@@ -198,10 +197,10 @@ __global__ void __launch_bounds__(kBlock, OURO_WAVES) k_tpraos_finish(ouro_tprao
   const int sh = quad ? 2 : 0;
   const size_t tid = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) >> sh;
   const size_t nth = ((size_t)gridDim.x * blockDim.x) >> sh;
-  int32_t* lane = scratch + tid * kLaneWords;
+  const Slot lane = slot_of(scratch, tid, kLaneWords);
   const uint32_t q = threadIdx.x & 3u;
   for (size_t i = tid; i < n; i += nth) {
-    int32_t* res = res_buf + i * kLatResWords;
+    const Slot res = slot_of(res_buf, i, kLatResWords);
     if (!quad) {
       hdr_combine_split(res);
       hdr_finish_item(b, i, opts, res, lane, verdict, beta_eta, beta_leader);
@@ -219,8 +218,8 @@ __global__ void __launch_bounds__(kBlock, OURO_WAVES) k_tpraos_finish(ouro_tprao
     if ((q & 1u) == 0 && dst) store_words(dst + 64 * i, beta, 4);
     if (q == 0) {
       uint32_t v = bit | other;
-      if (res[kResFlags + kCoreOcert] & kFlagOk) v |= 0x01u;
-      if (res[kResFlags + kCoreKes] & kFlagOk) v |= 0x02u;
+      if (ldg1(res.word(kResFlags + kCoreOcert)) & kFlagOk) v |= 0x01u;
+      if (ldg1(res.word(kResFlags + kCoreKes)) & kFlagOk) v |= 0x02u;
       verdict[i] = (uint8_t)v;
     }
   }
@@ -922,7 +921,7 @@ int hdr_batch_once(const ouro_tpraos_batch* b, const HdrOut& o, bool lowlat) {
   if (lowlat) {
     const uint32_t nw[4] = {(uint32_t)n, batch_opts(s.d), 0u, 0u};
     const uint32_t* d_n = sg.up(nw, 4);
-    int32_t* res = sg.out<int32_t>(n * kLatResWords);
+    int32_t* res = sg.out<int32_t>(slot_region_words(n, kLatResWords));
     int32_t* scr = sg.out<int32_t>(lowlat_scratch_words(ds, n));
     if (sg.rc) return sg.rc;
     // (nw is read by the H2D above; this frame outlives the sync below)
@@ -1257,7 +1256,7 @@ int plan_build(ouro_tpraos_plan* p) {
   OURO_HIP(hipHostMalloc(&p->h_out, p->out_bytes, hipHostMallocDefault));
   OURO_HIP(hipMalloc(&p->d_in, p->in_bytes));
   OURO_HIP(hipMalloc(&p->d_out, p->out_bytes));
-  OURO_HIP(hipMalloc(&p->res, sizeof(int32_t) * kLatResWords * p->cap));
+  OURO_HIP(hipMalloc(&p->res, sizeof(int32_t) * slot_region_words(p->cap, kLatResWords)));
   OURO_HIP(hipMalloc(&p->scratch, sizeof(int32_t) * lowlat_scratch_words(ds, p->cap)));
   memset(p->h_in, 0, p->in_bytes);
   uint8_t* d = p->d_in;

@@ -103,7 +103,7 @@ struct ShaNoTail {
 };
 struct ShaGlobalTail {
   const uint8_t* msg;
-  OURO_FI uint32_t tail(uint32_t q) const { return msg[q]; }
+  OURO_FI uint32_t tail(uint32_t q) const { return ldg_u8(msg + q); }
 };
 
 // SHA-512 over prefix (PL bytes, as little-endian packed words) || tail (tl

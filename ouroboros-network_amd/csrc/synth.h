@@ -36,18 +36,18 @@ OURO_FI void sc_muladd(uint32_t out[8], const uint32_t a[8], const uint32_t b[8]
 }
 
 // [k]B for k < L, through the shared multiplication routine (B table only)
-OURO_FI ge_p2 base_mul(const uint32_t k[8], int32_t* lane, const int32_t* btab) {
+OURO_FI ge_p2 base_mul(const uint32_t k[8], Slot lane, const int32_t* btab) {
   st_words8(lane + kSlotB, k);
-  reinterpret_cast<uint64_t*>(lane + kSlotCarry)[2] = sc_recode_b(k);
+  st_carry(lane, 2, sc_recode_b(k));
   dsm(lane, btab, dsm_cfg(0, 0, true));
   return dsm_result(lane);
 }
 
 // [k]P for k < L
-OURO_FI ge_p2 var_mul(const uint32_t k[8], const ge_p3& P, int32_t* lane, const int32_t* btab) {
+OURO_FI ge_p2 var_mul(const uint32_t k[8], const ge_p3& P, Slot lane, const int32_t* btab) {
   build_table(lane + kSlotTab1, P);
   st_words8(lane + kSlotA1, k);
-  reinterpret_cast<uint64_t*>(lane + kSlotCarry)[0] = sc_recode_carries<4, 64>(k);
+  st_carry(lane, 0, sc_recode_carries<4, 64>(k));
   dsm(lane, btab, dsm_cfg(64, 0, false));
   return dsm_result(lane);
 }
@@ -69,7 +69,7 @@ struct ExpandedKey {
   uint32_t pk[8];
 };
 
-OURO_FI void expand_seed(ExpandedKey& k, const uint32_t seed[8], int32_t* lane,
+OURO_FI void expand_seed(ExpandedKey& k, const uint32_t seed[8], Slot lane,
                          const int32_t* btab) {
   uint32_t az[16];
   sha512_32(az, seed);
@@ -88,7 +88,7 @@ OURO_FI void expand_seed(ExpandedKey& k, const uint32_t seed[8], int32_t* lane,
 // Ed25519 signature of a message (register prefix-free tail source)
 template <class Tail>
 OURO_FI void ed25519_sign_lane(uint32_t sig[16], const ExpandedKey& k, const Tail& msg,
-                               uint32_t mlen, int32_t* lane, const int32_t* btab) {
+                               uint32_t mlen, Slot lane, const int32_t* btab) {
   uint64_t H[8];
   uint32_t hw[16], r[8], h[8];
   sha512_prefixed<32>(H, k.prefix, msg, mlen);
@@ -116,7 +116,7 @@ OURO_FI void ed25519_sign_lane(uint32_t sig[16], const ExpandedKey& k, const Tai
 
 // draft-03 prove (SURVEY.md App. B.3'), 32-byte alpha in registers
 OURO_FI void vrf03_prove_lane(uint32_t pi[20], const ExpandedKey& k, const uint32_t alpha[8],
-                              int32_t* lane, const int32_t* btab) {
+                              Slot lane, const int32_t* btab) {
   uint32_t pre[9];
   pre[0] = 0x04u | (0x01u << 8) | (k.pk[0] << 16);
 #pragma unroll

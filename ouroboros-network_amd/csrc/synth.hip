@@ -82,7 +82,7 @@ __global__ void __launch_bounds__(kBlock) k_synth_ed25519(size_t n, uint64_t fir
                                                           const int32_t* btab) {
   const size_t tid = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   const size_t nth = (size_t)gridDim.x * blockDim.x;
-  int32_t* lane = scratch + tid * kLaneWords;
+  const Slot lane = slot_of(scratch, tid, kLaneWords);
   for (size_t i = tid; i < n; i += nth) {
     uint32_t seed[8];
     RegTail32 m;
@@ -104,7 +104,7 @@ __global__ void __launch_bounds__(kBlock) k_synth_vrf(size_t n, uint64_t first, 
                                                       const int32_t* btab) {
   const size_t tid = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   const size_t nth = (size_t)gridDim.x * blockDim.x;
-  int32_t* lane = scratch + tid * kLaneWords;
+  const Slot lane = slot_of(scratch, tid, kLaneWords);
   for (size_t i = tid; i < n; i += nth) {
     uint32_t seed[8], a[8], pi[20];
     seed_of(seed, tseed, first + i);
@@ -128,7 +128,7 @@ __global__ void __launch_bounds__(kBlock) k_synth_kes_leaves(int npools, Tag tke
                                                              int32_t* scratch, const int32_t* btab) {
   const size_t tid = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   const size_t nth = (size_t)gridDim.x * blockDim.x;
-  int32_t* lane = scratch + tid * kLaneWords;
+  const Slot lane = slot_of(scratch, tid, kLaneWords);
   for (size_t g = tid; g < (size_t)npools * 64; g += nth) {
     const int j = (int)(g >> 6), l = (int)(g & 63);
     uint32_t ts[8], ls[8];
@@ -164,7 +164,7 @@ __global__ void __launch_bounds__(kBlock) k_synth_pools(int npools, Tag tcold, T
   // pool record (words): cold_pk 8 | vrf a 8 | vrf prefix 8 | vrf pk 8 | hot_vk 8 | sigma 16
   const size_t tid = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   const size_t nth = (size_t)gridDim.x * blockDim.x;
-  int32_t* lane = scratch + tid * kLaneWords;
+  const Slot lane = slot_of(scratch, tid, kLaneWords);
   for (size_t j = tid; j < (size_t)npools; j += nth) {
     uint32_t cs[8], vs[8];
     seed_of(cs, tcold, j);
@@ -206,7 +206,7 @@ __global__ void __launch_bounds__(kBlock) k_synth_headers(
     int32_t* scratch, const int32_t* btab) {
   const size_t tid = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   const size_t nth = (size_t)gridDim.x * blockDim.x;
-  int32_t* lane = scratch + tid * kLaneWords;
+  const Slot lane = slot_of(scratch, tid, kLaneWords);
   for (size_t i = tid; i < n; i += nth) {
     const uint64_t g = first + i;  // global header index
     const int j = (int)(g % (uint64_t)npools);

@@ -55,18 +55,18 @@ OURO_HD inline uint32_t batch_opts(const ouro_tpraos_batch& b) {
          (b.eta_nonce ? kOptEtaNonce : 0u);
 }
 
-OURO_FI void st_point_at(int32_t* p, const fe& X, const fe& Y, const fe& Z) {
+OURO_FI void st_point_at(Slot p, const fe& X, const fe& Y, const fe& Z) {
   st_fe(p, X);
   st_fe(p + 12, Y);
   st_fe(p + 24, Z);
 }
-OURO_FI void st_point(int32_t* res, int which, const fe& X, const fe& Y, const fe& Z) {
+OURO_FI void st_point(Slot res, int which, const fe& X, const fe& Y, const fe& Z) {
   st_point_at(res + which * kPtWords, X, Y, Z);
 }
-OURO_FI ge_p2 ld_point_at(const int32_t* p) {
+OURO_FI ge_p2 ld_point_at(Slot p) {
   return ge_p2{ld_fe(p), ld_fe(p + 12), ld_fe(p + 24)};
 }
-OURO_FI void st_point_from_dsm(int32_t* res, int which, const int32_t* lane) {
+OURO_FI void st_point_from_dsm(Slot res, int which, Slot lane) {
   const ge_p2 r = dsm_result(lane);
   st_point(res, which, r.X, r.Y, r.Z);
 }
@@ -107,7 +107,7 @@ OURO_HD inline void ocert_msg(OcertMsg& m, const uint32_t hot_vk[8], uint64_t ct
 // table written to table slot `yslot`; otherwise a previous call's table is
 // reused (throughput mode: both VRFs of a header share the key).
 OURO_HD inline bool vrf_u_core(const uint32_t pk[8], const uint32_t pi[20], bool build_y,
-                               int yslot, int32_t* lane, const int32_t* btab,
+                               int yslot, Slot lane, const int32_t* btab,
                                bool quad = false) {
   bool ok = true;
   if (build_y) {
@@ -125,9 +125,8 @@ OURO_HD inline bool vrf_u_core(const uint32_t pk[8], const uint32_t pi[20], bool
   sc_reduce256(s, s_raw);
   st_words8(lane + kSlotA1, c);
   st_words8(lane + kSlotB, s);
-  uint64_t* carr = reinterpret_cast<uint64_t*>(lane + kSlotCarry);
-  carr[0] = sc_recode_carries<4, 33>(c);
-  carr[2] = sc_recode_b(s);
+  st_carry(lane, 0, sc_recode_carries<4, 33>(c));
+  st_carry(lane, 2, sc_recode_b(s));
   dsm(lane, btab, dsm_cfg(33, 0, true, yslot, 1), quad);
   return ok;
 }
@@ -139,9 +138,9 @@ OURO_HD inline bool vrf_u_core(const uint32_t pk[8], const uint32_t pi[20], bool
 // the two halves run on two lanes and hdr_combine_split adds them).
 template <class Tail>
 OURO_HD inline int32_t vrf_v_core(const uint32_t pk[8], const uint32_t pi[20], const Tail& alpha,
-                                  uint32_t alen, int32_t* lane, const int32_t* btab,
-                                  int32_t* res, int ptH, int ptV, int ptG8, int part = 0,
-                                  int32_t* partial = nullptr, bool quad = false) {
+                                  uint32_t alen, Slot lane, const int32_t* btab,
+                                  Slot res, int ptH, int ptV, int ptG8, int part,
+                                  Slot partial, bool quad = false) {
   uint32_t G[8], c[8], s_raw[8], s[8];
 #pragma unroll
   for (int i = 0; i < 8; i++) {
@@ -149,7 +148,6 @@ OURO_HD inline int32_t vrf_v_core(const uint32_t pk[8], const uint32_t pi[20], c
     s_raw[i] = pi[12 + i];
     c[i] = i < 4 ? pi[8 + i] : 0u;
   }
-  uint64_t* carr = reinterpret_cast<uint64_t*>(lane + kSlotCarry);
   ge_p3 Gamma;
   bool ok = true;
   if (part != 1) {
@@ -159,7 +157,7 @@ OURO_HD inline int32_t vrf_v_core(const uint32_t pk[8], const uint32_t pi[20], c
   if (part == 2) {
     build_table(lane + kSlotTab1, ge_p3_neg(Gamma), quad);
     st_words8(lane + kSlotA1, c);
-    carr[0] = sc_recode_carries<4, 33>(c);
+    st_carry(lane, 0, sc_recode_carries<4, 33>(c));
     dsm(lane, btab, dsm_cfg(33, 0, false, 0, 1), quad);
     const ge_p2 r = dsm_result(lane);
     st_point_at(partial, r.X, r.Y, r.Z);
@@ -179,11 +177,11 @@ OURO_HD inline int32_t vrf_v_core(const uint32_t pk[8], const uint32_t pi[20], c
     st_point(res, ptH, Hp.X, Hp.Y, Hp.Z);
     build_table(lane + kSlotTab1, Hp, quad);
     st_words8(lane + kSlotA1, s);
-    carr[0] = sc_recode_carries<4, 64>(s);
+    st_carry(lane, 0, sc_recode_carries<4, 64>(s));
     if (part == 0) {
       build_table(lane + kSlotTab2, ge_p3_neg(Gamma), quad);
       st_words8(lane + kSlotA2, c);
-      carr[1] = sc_recode_carries<4, 33>(c);
+      st_carry(lane, 1, sc_recode_carries<4, 33>(c));
       dsm(lane, btab, dsm_cfg(64, 33, false, 0, 1), quad);
     } else {
       dsm(lane, btab, dsm_cfg(64, 0, false, 0, 1), quad);
@@ -235,22 +233,22 @@ OURO_HD inline bool vrf_finish(uint32_t beta[16], const uint32_t Henc[8], const 
 // Latency mode: V = [s]H + (-[c]Gamma) from the two half cores, and the V
 // flag word from both (acceptance of both halves; Gamma's x = 0 bit from the
 // Gamma half).  Complete projective addition, so no case is special.
-OURO_HD inline void hdr_combine_split(int32_t* res) {
+OURO_HD inline void hdr_combine_split(Slot res) {
 #pragma unroll 1
   for (int which = 0; which < 2; which++) {
     const int ptV = which ? kPtVl : kPtVe;
     const ge_p2 V = ge_p2_add(ld_point_at(res + ptV * kPtWords),
                               ld_point_at(res + kLatPart + which * kPtWords));
     st_point(res, ptV, V.X, V.Y, V.Z);
-    int32_t* fv = res + kResFlags + (which ? kCoreVl : kCoreVe);
-    const int32_t fg = res[kResFlags + (which ? kCoreGl : kCoreGe)];
-    *fv = (*fv & fg & kFlagOk) | (fg & kFlagGammaX0);
+    int32_t* fv = res.word(kResFlags + (which ? kCoreVl : kCoreVe));
+    const int32_t fg = ldg1(res.word(kResFlags + (which ? kCoreGl : kCoreGe)));
+    stg1(fv, (ldg1(fv) & fg & kFlagOk) | (fg & kFlagGammaX0));
   }
 }
 
 // One inversion for all eight Z; tmp = 8 x 12 scratch words.  Then every
 // comparison and hash.  Returns the OURO_HDR_* verdict bits.
-OURO_HD inline uint32_t hdr_finish(const int32_t* res, int32_t* tmp, const uint32_t pie[20],
+OURO_HD inline uint32_t hdr_finish(Slot res, Slot tmp, const uint32_t pie[20],
                                    const uint32_t pil[20], uint32_t beta_e[16],
                                    uint32_t beta_l[16]) {
   // prefix products P_k = Z_0 ... Z_k
@@ -275,15 +273,15 @@ OURO_HD inline uint32_t hdr_finish(const int32_t* res, int32_t* tmp, const uint3
   for (int k = 0; k < kHdrPoints; k++)
     ge_encode_with_inv(enc[k], ld_fe(res + k * kPtWords), ld_fe(res + k * kPtWords + 12),
                        ld_fe(tmp + 12 * k));
-  const int32_t* fl = res + kResFlags;
+  auto fl = [&](int core) { return ldg1(res.word(kResFlags + core)); };
   uint32_t v = 0;
-  if (fl[kCoreOcert] & kFlagOk) v |= 0x01u;
-  if (fl[kCoreKes] & kFlagOk) v |= 0x02u;
+  if (fl(kCoreOcert) & kFlagOk) v |= 0x01u;
+  if (fl(kCoreKes) & kFlagOk) v |= 0x02u;
 #pragma unroll 1
   for (int which = 0; which < 2; which++) {
     const uint32_t* pi = which ? pil : pie;
     const int base = which ? kPtHl : kPtHe;
-    const int32_t fu = fl[which ? kCoreUl : kCoreUe], fv = fl[which ? kCoreVl : kCoreVe];
+    const int32_t fu = fl(which ? kCoreUl : kCoreUe), fv = fl(which ? kCoreVl : kCoreVe);
     uint32_t Genc[8], c[4], b[16];
 #pragma unroll
     for (int i = 0; i < 8; i++) Genc[i] = pi[i];
@@ -306,15 +304,15 @@ OURO_HD inline uint32_t hdr_finish(const int32_t* res, int32_t* tmp, const uint3
 // verdict bit (OURO_HDR 0x04 / 0x08); beta is zeroed unless it is set.  The
 // two VRFs of a header run on two lane pairs of a quad (k_tpraos_finish), so
 // a header's finish takes one VRF's time.  Reads res only.
-OURO_HD inline uint32_t vrf_finish_split(const int32_t* res, int which, const uint32_t pi[20],
+OURO_HD inline uint32_t vrf_finish_split(Slot res, int which, const uint32_t pi[20],
                                          uint32_t beta[16]) {
   const int base = which ? kPtHl : kPtHe;
   const ge_p2 V = ge_p2_add(ld_point_at(res + (base + 2) * kPtWords),
                             ld_point_at(res + kLatPart + which * kPtWords));
-  const int32_t* fl = res + kResFlags;
-  const int32_t fu = fl[which ? kCoreUl : kCoreUe];
-  const int32_t fg = fl[which ? kCoreGl : kCoreGe];
-  const int32_t fv = (fl[which ? kCoreVl : kCoreVe] & fg & kFlagOk) | (fg & kFlagGammaX0);
+  auto fl = [&](int core) { return ldg1(res.word(kResFlags + core)); };
+  const int32_t fu = fl(which ? kCoreUl : kCoreUe);
+  const int32_t fg = fl(which ? kCoreGl : kCoreGe);
+  const int32_t fv = (fl(which ? kCoreVl : kCoreVe) & fg & kFlagOk) | (fg & kFlagGammaX0);
   // Z^-1 of H, U, V, [8]Gamma by one inversion (prefix products)
   const fe z0 = ld_fe(res + base * kPtWords + 24), z1 = ld_fe(res + (base + 1) * kPtWords + 24);
   const fe z3 = ld_fe(res + (base + 3) * kPtWords + 24);
@@ -347,17 +345,16 @@ OURO_HD inline uint32_t vrf_finish_split(const int32_t* res, int which, const ui
 
 // ---- per-header drivers (the kernels' bodies; host-testable) -------------
 OURO_FI void ld_words(uint32_t* w, const uint8_t* p, int n16) {
-  const uint4* q = reinterpret_cast<const uint4*>(p);
 #pragma unroll
   for (int i = 0; i < n16; i++) {
-    uint4 v = q[i];
+    const int4 v = ldg4(p + 16 * i);
     w[4 * i] = v.x; w[4 * i + 1] = v.y; w[4 * i + 2] = v.z; w[4 * i + 3] = v.w;
   }
 }
 OURO_FI void st_words(uint8_t* p, const uint32_t* w, int n16) {
-  uint4* q = reinterpret_cast<uint4*>(p);
 #pragma unroll
-  for (int i = 0; i < n16; i++) q[i] = make_uint4(w[4 * i], w[4 * i + 1], w[4 * i + 2], w[4 * i + 3]);
+  for (int i = 0; i < n16; i++)
+    stg4(p + 16 * i, make_int4((int)w[4 * i], (int)w[4 * i + 1], (int)w[4 * i + 2], (int)w[4 * i + 3]));
 }
 
 // The VRF input of header i: mkSeed seedEta / seedL slot eta0 on the device
@@ -385,7 +382,7 @@ OURO_HD inline void hdr_seed(SeedMsg& a, const ouro_tpraos_batch& b, size_t i, b
 // built by the eta U core (table slot 2) for the leader U core.
 // opts: the batch's optional members (batch_opts / the latency launches' word).
 OURO_HD inline void hdr_core(const ouro_tpraos_batch& b, size_t i, uint32_t opts, int core,
-                             int32_t* lane, int32_t* res, const int32_t* btab,
+                             Slot lane, Slot res, const int32_t* btab,
                              bool share_key = true, bool split = false, bool quad = false) {
   int32_t flag = 0;
   switch (core) {
@@ -415,7 +412,7 @@ OURO_HD inline void hdr_core(const ouro_tpraos_batch& b, size_t i, uint32_t opts
       ld_words(pi, (leader ? b.leader_proof : b.eta_proof) + 80 * i, 5);
       const bool build = !(share_key && leader);
       const bool ok = vrf_u_core(p, pi, build, 2, lane, btab, quad);
-      flag = build ? (ok ? kFlagOk : 0) : (res[kResFlags + kCoreUe] & kFlagOk);
+      flag = build ? (ok ? kFlagOk : 0) : (ldg1(res.word(kResFlags + kCoreUe)) & kFlagOk);
       st_point_from_dsm(res, leader ? kPtUl : kPtUe, lane);
       break;
     }
@@ -425,23 +422,22 @@ OURO_HD inline void hdr_core(const ouro_tpraos_batch& b, size_t i, uint32_t opts
       uint32_t p[8], pi[20];
       ld_words(p, b.vrf_vk + 32 * i, 2);
       ld_words(pi, (leader ? b.leader_proof : b.eta_proof) + 80 * i, 5);
-      // the 32-byte VRF input: the caller's alpha, or mkSeed's output staged
+      // the 32-byte VRF input (the caller's alpha, or mkSeed's output) staged
       // in the lane slot's (still free) result area
-      const uint8_t* a = (leader ? b.leader_alpha : b.eta_alpha) + 32 * i;
-      if ((opts & kOptSeeds) && !gamma) {
+      if (!gamma) {
         uint32_t w[8];
-        hdr_mkseed(w, b, i, leader, opts);
+        if (opts & kOptSeeds) hdr_mkseed(w, b, i, leader, opts);
+        else ld_words(w, (leader ? b.leader_alpha : b.eta_alpha) + 32 * i, 2);
         st_words8(lane + kSlotOut, w);
-        a = reinterpret_cast<const uint8_t*>(lane + kSlotOut);
       }
-      flag = vrf_v_core(p, pi, ShaGlobalTail{a}, 32, lane, btab, res,
+      flag = vrf_v_core(p, pi, SlotTail{lane + kSlotOut}, 32, lane, btab, res,
                         leader ? kPtHl : kPtHe, leader ? kPtVl : kPtVe,
                         leader ? kPtG8l : kPtG8e, gamma ? 2 : (split ? 1 : 0),
                         res + kLatPart + (leader ? kPtWords : 0), quad);
       break;
     }
   }
-  res[kResFlags + core] = flag;
+  stg1(res.word(kResFlags + core), flag);
 }
 
 // The claimed-output bit of one VRF (OURO_HDR_ETA_CLAIM_OK / _LEADER_CLAIM_OK):
@@ -493,11 +489,11 @@ OURO_NI void hdr_post(const ouro_tpraos_batch& b, size_t i, uint32_t opts, uint8
 // latency-mode finish of header i, VRF by VRF (the host form of the lane-pair
 // finish in k_tpraos_finish)
 OURO_HD inline void hdr_finish_item_split(const ouro_tpraos_batch& b, size_t i, uint32_t opts,
-                                          const int32_t* res, uint8_t* verdict,
+                                          Slot res, uint8_t* verdict,
                                           uint8_t* beta_eta, uint8_t* beta_leader) {
   uint32_t v = 0;
-  if (res[kResFlags + kCoreOcert] & kFlagOk) v |= 0x01u;
-  if (res[kResFlags + kCoreKes] & kFlagOk) v |= 0x02u;
+  if (ldg1(res.word(kResFlags + kCoreOcert)) & kFlagOk) v |= 0x01u;
+  if (ldg1(res.word(kResFlags + kCoreKes)) & kFlagOk) v |= 0x02u;
   for (int which = 0; which < 2; which++) {
     uint32_t pi[20], beta[16];
     ld_words(pi, (which ? b.leader_proof : b.eta_proof) + 80 * i, 5);
@@ -511,7 +507,7 @@ OURO_HD inline void hdr_finish_item_split(const ouro_tpraos_batch& b, size_t i, 
 }
 
 OURO_HD inline void hdr_finish_item(const ouro_tpraos_batch& b, size_t i, uint32_t opts,
-                                     const int32_t* res, int32_t* tmp, uint8_t* verdict,
+                                     Slot res, Slot tmp, uint8_t* verdict,
                                      uint8_t* beta_eta, uint8_t* beta_leader) {
   uint32_t pie[20], pil[20], be[16], bl[16];
   ld_words(pie, b.eta_proof + 80 * i, 5);

@@ -42,6 +42,47 @@ constexpr int kSlotCarry = kSlotB + 8;            // 6 words (3 x u64)
 constexpr int kSlotOut = kSlotCarry + 8;          // p2 result: 3 fe at 12-word stride
 constexpr int kLaneWords = kSlotOut + 36;         // 1028 words = 4112 B (16-B multiple)
 
+// ---- scratch slots -----------------------------------------------------------
+// The slots of kSlotGroup consecutive lanes are interleaved in 16-byte chunks:
+// chunk k of slot (g * kSlotGroup + j) sits at words
+//   g * kSlotGroup * slot_words + k * kChunkStride + 4 j.
+// Every slot offset used is a multiple of 4 words; words inside a chunk are
+// contiguous (int2 / uint64 accesses at even words stay inside one chunk).
+// kSlotGroup = 1 is the plain lane-major layout (a slot is contiguous), the
+// default: the table reads are per-lane GATHERS (each lane's digit picks its
+// own entry), so a lane wants its 160-B entry in as few lines as possible.
+// Interleaving the 64 slots of a wave (OURO_SLOT_GROUP=64) coalesces the
+// uniform accesses (scalars, table stores) but spreads every gathered entry
+// over ten 1-KiB-apart lines: measured 2.0x the HBM traffic (411 vs 207
+// KB/header), +51 % VMEM instructions and +6.4 % kernel time
+// (profiles/r02b).  The host build uses the same layout as the device.
+#ifndef OURO_SLOT_GROUP
+#define OURO_SLOT_GROUP 1
+#endif
+constexpr int kSlotGroup = OURO_SLOT_GROUP;
+constexpr int kChunkStride = 4 * kSlotGroup;       // words between a slot's chunks
+struct Slot {
+  int32_t* p;  // chunk 0 of this slot
+  // the slot region starting at word w (w a multiple of 4)
+  OURO_FI Slot operator+(int w) const {
+    OURO_TRK(if (w & 3) ouro_trk_violation();)
+    return Slot{p + (w >> 2) * kChunkStride};
+  }
+  // k chunks further (run-time table entry offsets)
+  OURO_FI Slot chunks(int k) const { return Slot{p + k * kChunkStride}; }
+  OURO_FI int32_t* word(int w) const { return p + (w >> 2) * kChunkStride + (w & 3); }
+  OURO_FI int4* chunk(int k) const { return reinterpret_cast<int4*>(p + k * kChunkStride); }
+};
+// slot s of a region of slots of slot_words words each (slot_words % 4 == 0;
+// the region holds a multiple of kSlotGroup slots)
+OURO_FI Slot slot_of(int32_t* base, size_t s, int slot_words) {
+  return Slot{base + (s / kSlotGroup) * (size_t)kSlotGroup * slot_words + (s % kSlotGroup) * 4};
+}
+// words a region of n slots takes (rounded up to whole groups)
+constexpr size_t slot_region_words(size_t n, int slot_words) {
+  return (n + kSlotGroup - 1) / kSlotGroup * kSlotGroup * (size_t)slot_words;
+}
+
 // Fixed base B: the scalar is split at bit 128 (halves with B and 2^128 B, so
 // the doubling chain spans 128 bits) and each half is cut into signed digits
 // of kBW bits, one every kBW / 4 windows of the chain.  kBW = 16: 8 additions
@@ -61,31 +102,34 @@ constexpr size_t kBTabWords = 2 * (size_t)kBTabEntries * kNielsWords;
 
 // ---- vector load/store helpers ---------------------------------------------
 // (the host bound tracker of fe25519.h follows elements through memory)
-OURO_FI void st_fe(int32_t* p, const fe& f) {
-  int4* q = reinterpret_cast<int4*>(p);
-  // 10 words: store as 2 x int4 + int2
-  q[0] = make_int4(f.v[0], f.v[1], f.v[2], f.v[3]);
-  q[1] = make_int4(f.v[4], f.v[5], f.v[6], f.v[7]);
-  reinterpret_cast<int2*>(p + 8)[0] = make_int2(f.v[8], f.v[9]);
-  OURO_TRK(ouro_trk_store(p, f.b));
+// one field element at slot word 0: chunks 0, 1 and half of chunk 2
+OURO_FI void st_fe(Slot p, const fe& f) {
+  stg4(p.chunk(0), make_int4(f.v[0], f.v[1], f.v[2], f.v[3]));
+  stg4(p.chunk(1), make_int4(f.v[4], f.v[5], f.v[6], f.v[7]));
+  stg2(p.chunk(2), make_int2(f.v[8], f.v[9]));
+  OURO_TRK(ouro_trk_store(p.p, f.b));
 }
-OURO_FI fe ld_fe(const int32_t* p) {
-  const int4* q = reinterpret_cast<const int4*>(p);
-  int4 a = q[0], b = q[1];
-  int2 c = reinterpret_cast<const int2*>(p + 8)[0];
+OURO_FI fe ld_fe(Slot p) {
+  const int4 a = ldg4(p.chunk(0)), b = ldg4(p.chunk(1));
+  const int2 c = ldg2(p.chunk(2));
   fe f = fe_make(a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w, c.x, c.y);
-  OURO_TRK(ouro_trk_load(p, f.b));
+  OURO_TRK(ouro_trk_load(p.p, f.b));
   return f;
 }
-// one element at an 8-byte-aligned address (fe k of a table entry)
-OURO_FI fe ld_fe_w2(const int32_t* p) {
-  const int2* q = reinterpret_cast<const int2*>(p);
-  const int2 a = q[0], b = q[1], c = q[2], d = q[3], e = q[4];
-  return fe_make(a.x, a.y, b.x, b.y, c.x, c.y, d.x, d.y, e.x, e.y);
+// one element as five int2 at words w0, w0 + 2, ... (w0 even, run-time) of a
+// region whose chunks are `stride` words apart: a slot (kChunkStride) or
+// plain memory (4)
+OURO_FI fe ld_fe_w2(const int32_t* base, int w0, int stride) {
+  int2 q[5];
+#pragma unroll
+  for (int j = 0; j < 5; j++) {
+    const int w = w0 + 2 * j;
+    q[j] = ldg2(base + (w >> 2) * stride + (w & 3));
+  }
+  return fe_make(q[0].x, q[0].y, q[1].x, q[1].y, q[2].x, q[2].y, q[3].x, q[3].y, q[4].x, q[4].y);
 }
-// cached point: 40 words = 10 x int4, fe k at words [10k, 10k+10)
-OURO_FI void st_cached(int32_t* p, const ge_cached& c) {
-  int4* q = reinterpret_cast<int4*>(p);
+// cached point: 40 words = 10 chunks, fe k at words [10k, 10k+10)
+OURO_FI void st_cached(Slot p, const ge_cached& c) {
   const uint32_t* s[4] = {c.YplusX.v, c.YminusX.v, c.Z2.v, c.T2d.v};
   int32_t w[40];
 #pragma unroll
@@ -93,16 +137,16 @@ OURO_FI void st_cached(int32_t* p, const ge_cached& c) {
 #pragma unroll
     for (int i = 0; i < 10; i++) w[10 * k + i] = s[k][i];
 #pragma unroll
-  for (int i = 0; i < 10; i++) q[i] = make_int4(w[4 * i], w[4 * i + 1], w[4 * i + 2], w[4 * i + 3]);
-  OURO_TRK(ouro_trk_store(p, c.YplusX.b); ouro_trk_store(p + 10, c.YminusX.b);
-           ouro_trk_store(p + 20, c.Z2.b); ouro_trk_store(p + 30, c.T2d.b);)
+  for (int i = 0; i < 10; i++)
+    stg4(p.chunk(i), make_int4(w[4 * i], w[4 * i + 1], w[4 * i + 2], w[4 * i + 3]));
+  OURO_TRK(ouro_trk_store(p.word(0), c.YplusX.b); ouro_trk_store(p.word(10), c.YminusX.b);
+           ouro_trk_store(p.word(20), c.Z2.b); ouro_trk_store(p.word(30), c.T2d.b);)
 }
-OURO_FI ge_cached ld_cached(const int32_t* p) {
-  const int4* q = reinterpret_cast<const int4*>(p);
+OURO_FI ge_cached ld_cached(Slot p) {
   int32_t w[40];
 #pragma unroll
   for (int i = 0; i < 10; i++) {
-    int4 v = q[i];
+    int4 v = ldg4(p.chunk(i));
     w[4 * i] = v.x; w[4 * i + 1] = v.y; w[4 * i + 2] = v.z; w[4 * i + 3] = v.w;
   }
   ge_cached c;
@@ -113,16 +157,15 @@ OURO_FI ge_cached ld_cached(const int32_t* p) {
     c.Z2.v[i] = w[20 + i];
     c.T2d.v[i] = w[30 + i];
   }
-  OURO_TRK(ouro_trk_load(p, c.YplusX.b); ouro_trk_load(p + 10, c.YminusX.b);
-           ouro_trk_load(p + 20, c.Z2.b); ouro_trk_load(p + 30, c.T2d.b);)
+  OURO_TRK(ouro_trk_load(p.word(0), c.YplusX.b); ouro_trk_load(p.word(10), c.YminusX.b);
+           ouro_trk_load(p.word(20), c.Z2.b); ouro_trk_load(p.word(30), c.T2d.b);)
   return c;
 }
 OURO_FI ge_niels ld_niels(const int32_t* p) {
-  const int4* q = reinterpret_cast<const int4*>(p);
   int32_t w[32];
 #pragma unroll
   for (int i = 0; i < 8; i++) {
-    int4 v = q[i];
+    int4 v = ldg4(p + 4 * i);
     w[4 * i] = v.x; w[4 * i + 1] = v.y; w[4 * i + 2] = v.z; w[4 * i + 3] = v.w;
   }
   ge_niels n;
@@ -136,21 +179,29 @@ OURO_FI ge_niels ld_niels(const int32_t* p) {
            ouro_trk_load(p + 20, n.xy2d.b);)
   return n;
 }
-OURO_FI void st_words8(int32_t* p, const uint32_t w[8]) {
-  int4* q = reinterpret_cast<int4*>(p);
-  q[0] = make_int4((int)w[0], (int)w[1], (int)w[2], (int)w[3]);
-  q[1] = make_int4((int)w[4], (int)w[5], (int)w[6], (int)w[7]);
+OURO_FI void st_words8(Slot p, const uint32_t w[8]) {
+  stg4(p.chunk(0), make_int4((int)w[0], (int)w[1], (int)w[2], (int)w[3]));
+  stg4(p.chunk(1), make_int4((int)w[4], (int)w[5], (int)w[6], (int)w[7]));
 }
-OURO_FI void ld_words8(uint32_t w[8], const int32_t* p) {
-  const int4* q = reinterpret_cast<const int4*>(p);
-  int4 a = q[0], b = q[1];
+OURO_FI void ld_words8(uint32_t w[8], Slot p) {
+  const int4 a = ldg4(p.chunk(0)), b = ldg4(p.chunk(1));
   w[0] = a.x; w[1] = a.y; w[2] = a.z; w[3] = a.w;
   w[4] = b.x; w[5] = b.y; w[6] = b.z; w[7] = b.w;
 }
+// the recoding carries of scalars a1, a2, b (k = 0, 1, 2)
+OURO_FI uint64_t ld_carry(Slot lane, int k) { return ldg8(lane.word(kSlotCarry + 2 * k)); }
+OURO_FI void st_carry(Slot lane, int k, uint64_t c) { stg8(lane.word(kSlotCarry + 2 * k), c); }
+// a 32-byte message held in a slot (the VRF input staged by the header cores)
+struct SlotTail {
+  Slot s;
+  OURO_FI uint32_t tail(uint32_t q) const {
+    return ((uint32_t)ldg1(s.word((int)(q >> 2))) >> (8 * (q & 3))) & 0xffu;
+  }
+};
 
 // [1..8]P in cached form into a per-lane table
 // (quad: the lane-quad formulas of ge25519.h, latency mode)
-OURO_HD inline void build_table(int32_t* tab, const ge_p3& P, bool quad = false) {
+OURO_HD inline void build_table(Slot tab, const ge_p3& P, bool quad = false) {
   ge_cached c1 = ge_p3_to_cached(P);
   st_cached(tab, c1);
   ge_p3 Pk = quad ? ge_p1p1_to_p3_quad(ge_p2_dbl_quad(ge_p3_to_p2(P)))
@@ -160,7 +211,7 @@ OURO_HD inline void build_table(int32_t* tab, const ge_p3& P, bool quad = false)
   for (int k = 2; k < kTabEntries; k++) {
     Pk = quad ? ge_p1p1_to_p3_quad(ge_add_cached_quad(Pk, c1, false))
               : ge_p1p1_to_p3(ge_add_cached(Pk, c1, false));
-    st_cached(tab + k * kCachedWords, ge_p3_to_cached(Pk));
+    st_cached(tab.chunks(k * (kCachedWords / 4)), ge_p3_to_cached(Pk));
   }
 }
 
@@ -229,17 +280,16 @@ constexpr uint32_t dsm_cfg(int nw1, int nw2, bool useB, int tab1 = 0, int tab2 =
 #define OURO_ADD_UNROLL_QUAD 4
 #endif
 template <bool kQuad>
-OURO_FI void dsm_body(int32_t* lane, const int32_t* btab, uint32_t cfg) {
+OURO_FI void dsm_body(Slot lane, const int32_t* btab, uint32_t cfg) {
   const int nw1 = (int)(cfg & 0x7f), nw2 = (int)((cfg >> 8) & 0x7f);
   const bool useB = (cfg >> 16) & 1;
-  const int32_t* tab1 = lane + (int)((cfg >> 20) & 3) * kTabWords;
-  const int32_t* tab2 = lane + (int)((cfg >> 22) & 3) * kTabWords;
+  const Slot tab1 = lane.chunks((int)((cfg >> 20) & 3) * (kTabWords / 4));
+  const Slot tab2 = lane.chunks((int)((cfg >> 22) & 3) * (kTabWords / 4));
   uint32_t a1[8], a2[8], b[8];
   ld_words8(a1, lane + kSlotA1);
   ld_words8(a2, lane + kSlotA2);
   ld_words8(b, lane + kSlotB);
-  const uint64_t* carr = reinterpret_cast<const uint64_t*>(lane + kSlotCarry);
-  const uint64_t c1 = carr[0], c2 = carr[1], cb = carr[2];
+  const uint64_t c1 = ld_carry(lane, 0), c2 = ld_carry(lane, 1), cb = ld_carry(lane, 2);
   int top = nw1 > nw2 ? nw1 : nw2;
   if (useB && top < kBStride * kBDigitsHalf) top = kBStride * kBDigitsHalf;
   // digit streams: window top-1 of a1/a2 at the top of the array
@@ -283,16 +333,16 @@ OURO_FI void dsm_body(int32_t* lane, const int32_t* btab, uint32_t cfg) {
     // touch this window's per-lane table entries now, so that the loads
     // after the four doublings hit L2 instead of waiting on HBM
     const int i1 = (d1 < 0 ? -d1 : d1) - 1, i2 = (d2 < 0 ? -d2 : d2) - 1;
-    const int32_t* e1 = tab1 + (i1 > 0 ? i1 : 0) * kCachedWords;
-    const int32_t* e2 = tab2 + (i2 > 0 ? i2 : 0) * kCachedWords;
+    const Slot e1 = tab1.chunks((i1 > 0 ? i1 : 0) * (kCachedWords / 4));
+    const Slot e2 = tab2.chunks((i2 > 0 ? i2 : 0) * (kCachedWords / 4));
     uint32_t pf1 = 0, pf2 = 0, pf3 = 0, pf4 = 0, pf5 = 0, pf6 = 0;
-    if (act1) { pf1 = (uint32_t)e1[0]; pf2 = (uint32_t)e1[kCachedWords - 1]; }
-    if (act2) { pf3 = (uint32_t)e2[0]; pf4 = (uint32_t)e2[kCachedWords - 1]; }
+    if (act1) { pf1 = (uint32_t)ldg1(e1.word(0)); pf2 = (uint32_t)ldg1(e1.word(kCachedWords - 1)); }
+    if (act2) { pf3 = (uint32_t)ldg1(e2.word(0)); pf4 = (uint32_t)ldg1(e2.word(kCachedWords - 1)); }
     if (actB) {
       // the B entries (one 128-B line each) come from the 8 MiB tables
       const int i3 = (d3 < 0 ? -d3 : d3) - 1, i4 = (d4 < 0 ? -d4 : d4) - 1;
-      pf5 = (uint32_t)btab[(size_t)(i3 > 0 ? i3 : 0) * kNielsWords];
-      pf6 = (uint32_t)btab[((size_t)kBTabEntries + (i4 > 0 ? i4 : 0)) * kNielsWords];
+      pf5 = (uint32_t)ldg1(btab + (size_t)(i3 > 0 ? i3 : 0) * kNielsWords);
+      pf6 = (uint32_t)ldg1(btab + ((size_t)kBTabEntries + (i4 > 0 ? i4 : 0)) * kNielsWords);
     }
     // (the top window starts from the identity: its doublings are skipped)
     if (!OURO_DSM_SKIP_ID || j != top - 1) {
@@ -321,10 +371,11 @@ OURO_FI void dsm_body(int32_t* lane, const int32_t* btab, uint32_t cfg) {
         const uint32_t qp = threadIdx.x & 3u;
         const bool niels = src >= 2;
         const int k = qp < 2 ? (int)(qp ^ (neg ? 1u : 0u)) : (qp == 2 ? (niels ? 2 : 3) : (niels ? 0 : 2));
+        // a B entry is plain memory, a per-lane entry an interleaved slot region
         const int32_t* ent =
             niels ? btab + ((src == 3 ? (size_t)kBTabEntries : 0) + idx) * kNielsWords
-                  : (src == 0 ? tab1 : tab2) + idx * kCachedWords;
-        fe b = ld_fe_w2(ent + 10 * k);
+                  : (src == 0 ? tab1 : tab2).chunks(idx * (kCachedWords / 4)).p;
+        fe b = ld_fe_w2(ent, 10 * k, niels ? 4 : kChunkStride);
         // constants: the identity's operands (1, 1, 0, 2); a niels entry's 2Z = 2
         if (mag == 0 || (niels && qp == 3)) {
           b = fe_zero();
@@ -336,7 +387,7 @@ OURO_FI void dsm_body(int32_t* lane, const int32_t* btab, uint32_t cfg) {
 #endif
       ge_cached q;
       if (src < 2) {
-        q = ld_cached((src == 0 ? tab1 : tab2) + idx * kCachedWords);
+        q = ld_cached((src == 0 ? tab1 : tab2).chunks(idx * (kCachedWords / 4)));
       } else {
         const size_t base = src == 3 ? kBTabEntries : 0;
         ge_niels nq = ld_niels(btab + (base + idx) * kNielsWords);
@@ -360,24 +411,24 @@ OURO_FI void dsm_body(int32_t* lane, const int32_t* btab, uint32_t cfg) {
   st_fe(lane + kSlotOut + 12, r.Y);
   st_fe(lane + kSlotOut + 24, r.Z);
   // keeps the prefetch loads alive; limbs are < 2^27, so this never stores
-  if (prefetch == 0xffffffffu) lane[kSlotOut + 35] = (int32_t)prefetch;
+  if (prefetch == 0xffffffffu) stg1(lane.word(kSlotOut + 35), (int32_t)prefetch);
 }
-OURO_NI void dsm_lane(int32_t* lane, const int32_t* btab, uint32_t cfg) {
+OURO_NI void dsm_lane(Slot lane, const int32_t* btab, uint32_t cfg) {
   dsm_body<false>(lane, btab, cfg);
 }
 // latency mode: the four lanes of a quad run one chain (same inputs, same
 // slot), splitting each group operation's products
-OURO_NI void dsm_quad(int32_t* lane, const int32_t* btab, uint32_t cfg) {
+OURO_NI void dsm_quad(Slot lane, const int32_t* btab, uint32_t cfg) {
   dsm_body<true>(lane, btab, cfg);
 }
-OURO_FI void dsm(int32_t* lane, const int32_t* btab, uint32_t cfg, bool quad = false) {
+OURO_FI void dsm(Slot lane, const int32_t* btab, uint32_t cfg, bool quad = false) {
   if (quad)
     dsm_quad(lane, btab, cfg);
   else
     dsm_lane(lane, btab, cfg);
 }
 
-OURO_FI ge_p2 dsm_result(const int32_t* lane) {
+OURO_FI ge_p2 dsm_result(Slot lane) {
   return ge_p2{ld_fe(lane + kSlotOut), ld_fe(lane + kSlotOut + 12), ld_fe(lane + kSlotOut + 24)};
 }
 
@@ -409,7 +460,7 @@ OURO_FI int wave_max_small(int x) {
 // identity projectively.
 template <class Tail>
 OURO_HD inline bool ed25519_verify_lane(const uint32_t sig[16], const uint32_t pk[8],
-                                        const Tail& msg, uint32_t mlen, int32_t* lane,
+                                        const Tail& msg, uint32_t mlen, Slot lane,
                                         const int32_t* btab, bool byron = false,
                                         bool quad = false) {
   uint32_t R[8], S[8];
@@ -474,10 +525,9 @@ OURO_HD inline bool ed25519_verify_lane(const uint32_t sig[16], const uint32_t p
   st_words8(lane + kSlotA1, hs.c0);
   st_words8(lane + kSlotA2, hs.c1);
   st_words8(lane + kSlotB, b);
-  uint64_t* carr = reinterpret_cast<uint64_t*>(lane + kSlotCarry);
-  carr[0] = sc_recode_carries<4, 64>(hs.c0);
-  carr[1] = sc_recode_carries<4, 64>(hs.c1);
-  carr[2] = sc_recode_b(b);
+  st_carry(lane, 0, sc_recode_carries<4, 64>(hs.c0));
+  st_carry(lane, 1, sc_recode_carries<4, 64>(hs.c1));
+  st_carry(lane, 2, sc_recode_b(b));
   // windows so that every scalar is < 2^(4 nw - 1) (top carry zero), <= 64
   int nw = wave_max_small((hs.bits + 4) >> 2);
   nw = nw < 1 ? 1 : (nw > 64 ? 64 : nw);
@@ -587,7 +637,7 @@ OURO_FI void fe_invert4(fe out[4], const fe z[4]) {
 template <class Tail>
 OURO_HD inline bool vrf03_verify_lane(uint32_t beta[16], const uint32_t pk[8],
                                       const uint32_t pi[20], const Tail& alpha, uint32_t alen,
-                                      int32_t* lane, const int32_t* btab) {
+                                      Slot lane, const int32_t* btab) {
   uint32_t G[8], c[8], s_raw[8], s[8];
 #pragma unroll
   for (int i = 0; i < 8; i++) {
@@ -618,9 +668,8 @@ OURO_HD inline bool vrf03_verify_lane(uint32_t beta[16], const uint32_t pk[8],
   build_table(lane + kSlotTab1, ge_p3_neg(Y));
   st_words8(lane + kSlotA1, c);
   st_words8(lane + kSlotB, s);
-  uint64_t* carr = reinterpret_cast<uint64_t*>(lane + kSlotCarry);
-  carr[0] = sc_recode_carries<4, 33>(c);
-  carr[2] = sc_recode_b(s);
+  st_carry(lane, 0, sc_recode_carries<4, 33>(c));
+  st_carry(lane, 2, sc_recode_b(s));
   dsm(lane, btab, dsm_cfg(33, 0, true));
   ge_p2 U = dsm_result(lane);
   // V = [s]H - [c]Gamma
@@ -628,8 +677,8 @@ OURO_HD inline bool vrf03_verify_lane(uint32_t beta[16], const uint32_t pk[8],
   build_table(lane + kSlotTab2, ge_p3_neg(Gamma));
   st_words8(lane + kSlotA1, s);
   st_words8(lane + kSlotA2, c);
-  carr[0] = sc_recode_carries<4, 64>(s);
-  carr[1] = sc_recode_carries<4, 33>(c);
+  st_carry(lane, 0, sc_recode_carries<4, 64>(s));
+  st_carry(lane, 1, sc_recode_carries<4, 33>(c));
   dsm(lane, btab, dsm_cfg(64, 33, false));
   ge_p2 V = dsm_result(lane);
   ge_p3 G8 = ge_mul8(Gamma);
@@ -688,7 +737,7 @@ OURO_HD inline bool vrf03_verify_lane(uint32_t beta[16], const uint32_t pk[8],
 // levels 1..6 bottom-up; verification walks top-down from the root vk.
 template <class Tail>
 OURO_HD inline bool sum6kes_verify_lane(const uint32_t vk[8], uint32_t t, const uint32_t* sigw,
-                                        const Tail& msg, uint32_t mlen, int32_t* lane,
+                                        const Tail& msg, uint32_t mlen, Slot lane,
                                         const int32_t* btab, bool quad = false) {
   uint32_t cur[8];
 #pragma unroll
@@ -698,10 +747,9 @@ OURO_HD inline bool sum6kes_verify_lane(const uint32_t vk[8], uint32_t t, const 
   for (int k = 6; k >= 1; k--) {
     const uint32_t* pair = sigw + 16 + 16 * (k - 1);
     uint32_t pw[16], h[8];
-    const uint4* p4 = reinterpret_cast<const uint4*>(pair);
 #pragma unroll
     for (int i = 0; i < 4; i++) {
-      uint4 v = p4[i];
+      const int4 v = ldg4(pair + 4 * i);
       pw[4 * i] = v.x; pw[4 * i + 1] = v.y; pw[4 * i + 2] = v.z; pw[4 * i + 3] = v.w;
     }
     blake2b256_64(h, pw);
@@ -714,10 +762,9 @@ OURO_HD inline bool sum6kes_verify_lane(const uint32_t vk[8], uint32_t t, const 
     for (int i = 0; i < 8; i++) cur[i] = right ? pw[8 + i] : pw[i];
   }
   uint32_t sig[16];
-  const uint4* s4 = reinterpret_cast<const uint4*>(sigw);
 #pragma unroll
   for (int i = 0; i < 4; i++) {
-    uint4 v = s4[i];
+    const int4 v = ldg4(sigw + 4 * i);
     sig[4 * i] = v.x; sig[4 * i + 1] = v.y; sig[4 * i + 2] = v.z; sig[4 * i + 3] = v.w;
   }
   const bool leaf = ed25519_verify_lane(sig, cur, msg, mlen, lane, btab, false, quad);
