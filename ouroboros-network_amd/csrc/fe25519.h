@@ -22,7 +22,8 @@
 // routine covers all of its inputs.
 //
 // "Reduced" = what fe_mul/fe_sq/fe_carry64 return: limb i <= mask_i (2^26 - 1
-// even, 2^25 - 1 odd), except limb 1 <= 2^25 + 2^18.
+// even, 2^25 - 1 odd), except limb 1 <= 2^25 + 2^18 and (two-chain scanned
+// multiply) limb 6 <= 2^26 + 2^12; the host tracker carries the exact bounds.
 #pragma once
 #include "common.h"
 
@@ -226,11 +227,116 @@ OURO_FI fe fe_carry(const fe& f) {
   return h;
 }
 
+// ---- column-scan products ---------------------------------------------------
+// The carry out of column k is the FIRST addend of column k + 1's chain of
+// multiply-adds (v_mad_u64_u32 adds a 64-bit value for free), so a product
+// needs one shift and one mask per column instead of the separate 64-bit
+// carry additions of fe_carry64.  The accumulator is made opaque after each
+// multiply-add: LLVM would otherwise reassociate the column sum and add the
+// carry last.  Squarings scan the ten columns in one chain; multiplies in two
+// independent chains (columns 0..4 and 5..9, whose dependent multiply-adds the
+// scheduler interleaves), joined by carrying column 4 into limb 5.  Either way
+// column 9's carry wraps into limb 0 (x 19) and limb 0 carries into limb 1.
+// tools/microbench/fe_cs.hip (profiles/r02c/fe_cs.json): squaring 344 -> 368 G/s,
+// multiply 239 -> 245 G/s on MI355X, canonical outputs identical.
+#ifndef OURO_FE_SCAN
+#define OURO_FE_SCAN 1
+#endif
+OURO_FI uint64_t mad_acc(uint32_t a, uint32_t b, uint64_t c) {
+  uint64_t r = (uint64_t)a * b + c;
+#if defined(__HIP_DEVICE_COMPILE__)
+  asm("" : "+v"(r));
+#endif
+  return r;
+}
+// limbs of a scanned product, carry c9 out of column 9 still to wrap
+OURO_FI fe scan_finish(uint32_t h[10], uint64_t c9) {
+  const uint64_t t = (uint64_t)h[0] + 19ull * c9;
+  h[0] = (uint32_t)t & limb_mask(0);
+  h[1] += (uint32_t)(t >> 26);
+  fe r;
+#pragma unroll
+  for (int i = 0; i < 10; i++) {
+    r.v[i] = h[i];
+#if defined(__HIP_DEVICE_COMPILE__)
+    asm("" : "+v"(r.v[i]));  // hide the limb ranges (see fe_carry64)
+#endif
+  }
+  return r;
+}
+#if defined(OURO_TRACK_BOUNDS)
+// bounds of a scanned product from its column bounds T: chains [lo, hi)
+// scanned with the carry as first addend, then the joins and the wrap
+inline void trk_scan(fe& h, const unsigned __int128 T[10], bool two_chains) {
+  const unsigned __int128 lim = (unsigned __int128)1 << 64;
+  unsigned __int128 b[10], cA = 0, cB = 0;
+  for (int k = 0; k < 10; k++) {
+    const bool second = two_chains && k >= 5;
+    unsigned __int128 t = T[k] + (second ? cB : cA);
+    trk_check(t < lim);
+    b[k] = t > limb_mask(k) ? limb_mask(k) : t;
+    (second ? cB : cA) = t >> limb_bits(k);
+  }
+  unsigned __int128 c9 = cA;
+  if (two_chains) {
+    const unsigned __int128 t5 = b[5] + cA;  // column 4's carry into limb 5
+    trk_check(t5 < lim);
+    b[5] = t5 > limb_mask(5) ? limb_mask(5) : t5;
+    b[6] += t5 >> 25;
+    c9 = cB;
+  }
+  const unsigned __int128 t0 = b[0] + 19 * c9;
+  trk_check(t0 < lim);
+  b[0] = t0 > limb_mask(0) ? limb_mask(0) : t0;
+  b[1] += t0 >> 26;
+  for (int i = 0; i < 10; i++) {
+    trk_check(b[i] < ((unsigned __int128)1 << 32));
+    h.b[i] = (uint64_t)b[i];
+  }
+}
+#endif
+
 // h = f * g.  Column k collects f_i g_j with i + j = k (mod 10); odd*odd
 // terms carry a factor 2 (2^ceil(25.5 i) 2^ceil(25.5 j) = 2 * 2^ceil(25.5 (i+j)))
 // and wrapped terms a factor 19 (2^255 = 19), applied to g.  Needs
 // 19 g_j < 2^32: g is the operand with the smaller bound.
-OURO_FI fe fe_mul(const fe& f, const fe& g) {
+OURO_FI fe fe_mul_scan(const fe& f, const fe& g) {
+  uint32_t g19[10], f2[10];
+#pragma unroll
+  for (int i = 0; i < 10; i++) {
+    g19[i] = 19u * g.v[i];
+    f2[i] = (i & 1) ? 2u * f.v[i] : f.v[i];
+  }
+  uint32_t h[10];
+  uint64_t cA = 0, cB = 0;
+#pragma unroll
+  for (int s = 0; s < 5; s++) {
+    uint64_t tA = cA, tB = cB;
+#pragma unroll
+    for (int i = 0; i < 10; i++) {
+#pragma unroll
+      for (int half = 0; half < 2; half++) {
+        const int k = s + 5 * half;
+        const int j = (k - i + 10) % 10;
+        const uint32_t a = ((i & 1) && (j & 1)) ? f2[i] : f.v[i];
+        const uint32_t b = (i + j >= 10) ? g19[j] : g.v[j];
+        if (half) tB = mad_acc(a, b, tB);
+        else tA = mad_acc(a, b, tA);
+      }
+    }
+    h[s] = (uint32_t)tA & limb_mask(s);
+    cA = tA >> limb_bits(s);
+    h[s + 5] = (uint32_t)tB & limb_mask(s + 5);
+    cB = tB >> limb_bits(s + 5);
+  }
+  const uint64_t t5 = (uint64_t)h[5] + cA;
+  h[5] = (uint32_t)t5 & limb_mask(5);
+  h[6] += (uint32_t)(t5 >> 25);
+  return scan_finish(h, cB);
+}
+
+// the row-order form (A/B: OURO_FE_SCAN=0)
+OURO_FI fe fe_mul_rows(const fe& f, const fe& g) {
   OURO_COUNT_MUL();
   uint32_t g19[10], f2[10];
 #pragma unroll
@@ -268,6 +374,31 @@ OURO_FI fe fe_mul(const fe& f, const fe& g) {
     trk_carry(h, T, (unsigned __int128)1 << 64);
   })
   return h;
+}
+
+OURO_FI fe fe_mul(const fe& f, const fe& g) {
+#if OURO_FE_SCAN
+  OURO_COUNT_MUL();
+  fe h = fe_mul_scan(f, g);
+  OURO_TRK({
+    unsigned __int128 T[10] = {0};
+    for (int i = 0; i < 10; i++) {
+      if (i & 1) trk_check(2 * f.b[i] < (1ull << 32));
+      if (i >= 1) trk_check(19 * g.b[i] < (1ull << 32));
+      for (int j = 0; j < 10; j++) {
+        const int k = i + j;
+        unsigned __int128 x = (unsigned __int128)f.b[i] * g.b[j];
+        if ((i & 1) && (j & 1)) x *= 2;
+        if (k >= 10) x *= 19;
+        T[k % 10] += x;
+      }
+    }
+    trk_scan(h, T, true);
+  })
+  return h;
+#else
+  return fe_mul_rows(f, g);
+#endif
 }
 
 // f * g with the factor 19 applied per column after accumulation: no bound on
@@ -361,16 +492,86 @@ inline void trk_sq(fe& h, const fe& f, unsigned scale) {
 }
 #endif
 
+// f^2 (scale 1) or 2 f^2 (scale 2) scanned in one chain: column k's terms
+// are the diagonal f_i^2 (x2 if i odd) and the cross terms 2 f_i f_j (x2 if
+// both odd), x19 when wrapped; scale 2 doubles the left operands
+template <int kScale>
+OURO_FI fe fe_sq_scan(const fe& f) {
+  uint32_t fs[10], f2s[10], f4s[10], f19[10];
+#pragma unroll
+  for (int i = 0; i < 10; i++) {
+    fs[i] = kScale * f.v[i];
+    f2s[i] = 2u * kScale * f.v[i];
+    f4s[i] = 4u * kScale * f.v[i];
+    f19[i] = 19u * f.v[i];
+  }
+  uint32_t h[10];
+  uint64_t c = 0;
+#pragma unroll
+  for (int k = 0; k < 10; k++) {
+    uint64_t t = c;
+#pragma unroll
+    for (int i = 0; i < 10; i++) {
+#pragma unroll
+      for (int j = i; j < 10; j++) {
+        if ((i + j) % 10 != k) continue;
+        uint32_t a, b;
+        if (i == j) {
+          a = (i & 1) ? f2s[i] : fs[i];
+          b = (2 * i >= 10) ? f19[i] : f.v[i];
+        } else {
+          a = ((i & 1) && (j & 1)) ? f4s[i] : f2s[i];
+          b = (i + j >= 10) ? f19[j] : f.v[j];
+        }
+        t = mad_acc(a, b, t);
+      }
+    }
+    h[k] = (uint32_t)t & limb_mask(k);
+    c = t >> limb_bits(k);
+  }
+  return scan_finish(h, c);
+}
+#if defined(OURO_TRACK_BOUNDS)
+inline void trk_sq_scan(fe& h, const fe& f, unsigned scale) {
+  unsigned __int128 T[10] = {0};
+  for (int i = 0; i < 10; i++) {
+    trk_check(((i & 1) ? 4 : 2) * scale * f.b[i] < (1ull << 32));
+    if (i >= 5) trk_check(19 * f.b[i] < (1ull << 32));
+    for (int j = 0; j < 10; j++) {
+      const int k = i + j;
+      unsigned __int128 x = (unsigned __int128)f.b[i] * f.b[j];
+      if ((i & 1) && (j & 1)) x *= 2;
+      if (k >= 10) x *= 19;
+      T[k % 10] += x * scale;
+    }
+  }
+  trk_scan(h, T, false);
+}
+#endif
+
 OURO_FI fe fe_sq(const fe& f) {
+#if OURO_FE_SCAN
+  OURO_COUNT_SQ();
+  fe h = fe_sq_scan<1>(f);
+  OURO_TRK(trk_sq_scan(h, f, 1));
+  return h;
+#else
   uint64_t t[10];
   fe_sq_cols(t, f);
   fe h = fe_carry64(t);
   OURO_TRK(trk_sq(h, f, 1));
   return h;
+#endif
 }
 
 // 2 f^2
 OURO_FI fe fe_sq2(const fe& f) {
+#if OURO_FE_SCAN
+  OURO_COUNT_SQ();
+  fe h = fe_sq_scan<2>(f);
+  OURO_TRK(trk_sq_scan(h, f, 2));
+  return h;
+#else
   uint64_t t[10];
   fe_sq_cols(t, f);
 #pragma unroll
@@ -378,6 +579,7 @@ OURO_FI fe fe_sq2(const fe& f) {
   fe h = fe_carry64(t);
   OURO_TRK(trk_sq(h, f, 2));
   return h;
+#endif
 }
 
 // ---- encoding -------------------------------------------------------------
