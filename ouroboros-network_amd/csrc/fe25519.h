@@ -265,27 +265,34 @@ OURO_FI fe scan_finish(uint32_t h[10], uint64_t c9) {
   return r;
 }
 #if defined(OURO_TRACK_BOUNDS)
-// bounds of a scanned product from its column bounds T: chains [lo, hi)
-// scanned with the carry as first addend, then the joins and the wrap
-inline void trk_scan(fe& h, const unsigned __int128 T[10], bool two_chains) {
+// bounds of a scanned product from its column bounds T: chains starting at
+// columns starts[0] = 0 < starts[1] < ... scanned with the carry as first
+// addend, each chain's carry-out joined into the next chain's first limb,
+// then the wrap of column 9's carry
+inline void trk_scan(fe& h, const unsigned __int128 T[10], int nchains) {
+  const int starts3[3] = {0, 4, 7}, starts2[2] = {0, 5}, starts1[1] = {0};
+  const int* st = nchains == 3 ? starts3 : (nchains == 2 ? starts2 : starts1);
   const unsigned __int128 lim = (unsigned __int128)1 << 64;
-  unsigned __int128 b[10], cA = 0, cB = 0;
-  for (int k = 0; k < 10; k++) {
-    const bool second = two_chains && k >= 5;
-    unsigned __int128 t = T[k] + (second ? cB : cA);
+  unsigned __int128 b[10], cout[3] = {0, 0, 0};
+  for (int c = 0; c < nchains; c++) {
+    const int end = c + 1 < nchains ? st[c + 1] : 10;
+    unsigned __int128 carry = 0;
+    for (int k = st[c]; k < end; k++) {
+      const unsigned __int128 t = T[k] + carry;
+      trk_check(t < lim);
+      b[k] = t > limb_mask(k) ? limb_mask(k) : t;
+      carry = t >> limb_bits(k);
+    }
+    cout[c] = carry;
+  }
+  for (int c = 0; c + 1 < nchains; c++) {  // join into the next chain's first limb
+    const int k = st[c + 1];
+    const unsigned __int128 t = b[k] + cout[c];
     trk_check(t < lim);
     b[k] = t > limb_mask(k) ? limb_mask(k) : t;
-    (second ? cB : cA) = t >> limb_bits(k);
+    b[k + 1] += t >> limb_bits(k);
   }
-  unsigned __int128 c9 = cA;
-  if (two_chains) {
-    const unsigned __int128 t5 = b[5] + cA;  // column 4's carry into limb 5
-    trk_check(t5 < lim);
-    b[5] = t5 > limb_mask(5) ? limb_mask(5) : t5;
-    b[6] += t5 >> 25;
-    c9 = cB;
-  }
-  const unsigned __int128 t0 = b[0] + 19 * c9;
+  const unsigned __int128 t0 = b[0] + 19 * cout[nchains - 1];
   trk_check(t0 < lim);
   b[0] = t0 > limb_mask(0) ? limb_mask(0) : t0;
   b[1] += t0 >> 26;
@@ -376,10 +383,62 @@ OURO_FI fe fe_mul_rows(const fe& f, const fe& g) {
   return h;
 }
 
+// three chains (columns 0..3, 4..6, 7..9): a chain's dependent multiply-adds
+// are two instructions apart, which the MI355X issues without the s_nop the
+// two-chain form needs between each pair
+OURO_FI fe fe_mul_scan3(const fe& f, const fe& g) {
+  uint32_t g19[10], f2[10];
+#pragma unroll
+  for (int i = 0; i < 10; i++) {
+    g19[i] = 19u * g.v[i];
+    f2[i] = (i & 1) ? 2u * f.v[i] : f.v[i];
+  }
+  constexpr int kStart[3] = {0, 4, 7}, kLen[3] = {4, 3, 3};
+  uint32_t h[10];
+  uint64_t c[3] = {0, 0, 0};
+#pragma unroll
+  for (int s = 0; s < 4; s++) {
+    uint64_t t[3] = {c[0], c[1], c[2]};
+#pragma unroll
+    for (int i = 0; i < 10; i++) {
+#pragma unroll
+      for (int ch = 0; ch < 3; ch++) {
+        if (s >= kLen[ch]) continue;
+        const int k = kStart[ch] + s;
+        const int j = (k - i + 10) % 10;
+        const uint32_t a = ((i & 1) && (j & 1)) ? f2[i] : f.v[i];
+        const uint32_t b = (i + j >= 10) ? g19[j] : g.v[j];
+        t[ch] = mad_acc(a, b, t[ch]);
+      }
+    }
+#pragma unroll
+    for (int ch = 0; ch < 3; ch++) {
+      if (s >= kLen[ch]) continue;
+      const int k = kStart[ch] + s;
+      h[k] = (uint32_t)t[ch] & limb_mask(k);
+      c[ch] = t[ch] >> limb_bits(k);
+    }
+  }
+  // joins: column 3's carry into limb 4, column 6's into limb 7
+  const uint64_t t4 = (uint64_t)h[4] + c[0];
+  h[4] = (uint32_t)t4 & limb_mask(4);
+  h[5] += (uint32_t)(t4 >> 26);
+  const uint64_t t7 = (uint64_t)h[7] + c[1];
+  h[7] = (uint32_t)t7 & limb_mask(7);
+  h[8] += (uint32_t)(t7 >> 25);
+  return scan_finish(h, c[2]);
+}
+#ifndef OURO_MUL_X2
+#define OURO_MUL_X2 0  // 1: paired products, fewer s_nop but spills: no gain (profiles/r02c/ab_mul_x2.json)
+#endif
+#ifndef OURO_MUL_CHAINS
+#define OURO_MUL_CHAINS 2  // 3: profiles/r02c/ab_mul_chains.json, 2.0 % slower
+#endif
+
 OURO_FI fe fe_mul(const fe& f, const fe& g) {
 #if OURO_FE_SCAN
   OURO_COUNT_MUL();
-  fe h = fe_mul_scan(f, g);
+  fe h = OURO_MUL_CHAINS == 3 ? fe_mul_scan3(f, g) : fe_mul_scan(f, g);
   OURO_TRK({
     unsigned __int128 T[10] = {0};
     for (int i = 0; i < 10; i++) {
@@ -393,11 +452,77 @@ OURO_FI fe fe_mul(const fe& f, const fe& g) {
         T[k % 10] += x;
       }
     }
-    trk_scan(h, T, true);
+    trk_scan(h, T, OURO_MUL_CHAINS);
   })
   return h;
 #else
   return fe_mul_rows(f, g);
+#endif
+}
+
+// Two independent products with their four scan chains interleaved (a
+// chain's dependent multiply-adds then sit four instructions apart, the
+// distance the MI355X needs between a 64-bit multiply-add result and its use
+// without s_nop); the group formulas pair their independent products.
+OURO_FI void fe_mul_x2(fe& h1, fe& h2, const fe& f1, const fe& g1, const fe& f2, const fe& g2) {
+#if OURO_FE_SCAN && OURO_MUL_X2
+  const fe* F[2] = {&f1, &f2};
+  const fe* G[2] = {&g1, &g2};
+  uint32_t g19[2][10], fd[2][10];
+#pragma unroll
+  for (int p = 0; p < 2; p++)
+#pragma unroll
+    for (int i = 0; i < 10; i++) {
+      g19[p][i] = 19u * G[p]->v[i];
+      fd[p][i] = (i & 1) ? 2u * F[p]->v[i] : F[p]->v[i];
+    }
+  uint32_t h[2][10];
+  uint64_t c[2][2] = {{0, 0}, {0, 0}};
+#pragma unroll
+  for (int s = 0; s < 5; s++) {
+    uint64_t t[2][2] = {{c[0][0], c[0][1]}, {c[1][0], c[1][1]}};
+#pragma unroll
+    for (int i = 0; i < 10; i++) {
+#pragma unroll
+      for (int half = 0; half < 2; half++) {
+#pragma unroll
+        for (int p = 0; p < 2; p++) {
+          const int k = s + 5 * half;
+          const int j = (k - i + 10) % 10;
+          const uint32_t a = ((i & 1) && (j & 1)) ? fd[p][i] : F[p]->v[i];
+          const uint32_t b = (i + j >= 10) ? g19[p][j] : G[p]->v[j];
+          t[p][half] = mad_acc(a, b, t[p][half]);
+        }
+      }
+    }
+#pragma unroll
+    for (int p = 0; p < 2; p++) {
+      h[p][s] = (uint32_t)t[p][0] & limb_mask(s);
+      c[p][0] = t[p][0] >> limb_bits(s);
+      h[p][s + 5] = (uint32_t)t[p][1] & limb_mask(s + 5);
+      c[p][1] = t[p][1] >> limb_bits(s + 5);
+    }
+  }
+  fe r[2];
+#pragma unroll
+  for (int p = 0; p < 2; p++) {
+    const uint64_t t5 = (uint64_t)h[p][5] + c[p][0];
+    h[p][5] = (uint32_t)t5 & limb_mask(5);
+    h[p][6] += (uint32_t)(t5 >> 25);
+    r[p] = scan_finish(h[p], c[p][1]);
+  }
+  h1 = r[0];
+  h2 = r[1];
+  OURO_TRK({
+    fe t1 = fe_mul(f1, g1), t2 = fe_mul(f2, g2);  // bounds (and counts) of the pair
+    for (int i = 0; i < 10; i++) {
+      h1.b[i] = t1.b[i];
+      h2.b[i] = t2.b[i];
+    }
+  })
+#else
+  h1 = fe_mul(f1, g1);
+  h2 = fe_mul(f2, g2);
 #endif
 }
 
@@ -545,7 +670,7 @@ inline void trk_sq_scan(fe& h, const fe& f, unsigned scale) {
       T[k % 10] += x * scale;
     }
   }
-  trk_scan(h, T, false);
+  trk_scan(h, T, 1);
 }
 #endif
 

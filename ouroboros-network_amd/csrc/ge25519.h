@@ -38,10 +38,16 @@ OURO_FI ge_cached ge_cached_identity() {
 OURO_FI ge_niels ge_niels_identity() { return ge_niels{fe_one(), fe_one(), fe_zero()}; }
 
 OURO_FI ge_p2 ge_p1p1_to_p2(const ge_p1p1& p) {
-  return ge_p2{fe_mul(p.T, p.X), fe_mul(p.Z, p.Y), fe_mul(p.T, p.Z)};
+  ge_p2 r;
+  fe_mul_x2(r.X, r.Y, p.T, p.X, p.Z, p.Y);
+  r.Z = fe_mul(p.T, p.Z);
+  return r;
 }
 OURO_FI ge_p3 ge_p1p1_to_p3(const ge_p1p1& p) {
-  return ge_p3{fe_mul(p.T, p.X), fe_mul(p.Z, p.Y), fe_mul(p.T, p.Z), fe_mul(p.X, p.Y)};
+  ge_p3 r;
+  fe_mul_x2(r.X, r.Y, p.T, p.X, p.Z, p.Y);
+  fe_mul_x2(r.Z, r.T, p.T, p.Z, p.X, p.Y);
+  return r;
 }
 OURO_FI ge_p2 ge_p3_to_p2(const ge_p3& p) { return ge_p2{p.X, p.Y, p.Z}; }
 OURO_FI ge_cached ge_p3_to_cached(const ge_p3& p) {
@@ -71,10 +77,14 @@ OURO_FI ge_p1p1 ge_add_cached(const ge_p3& p, const ge_cached& q, bool neg,
                               bool affine_q = false) {
   fe qa = fe_select(q.YminusX, q.YplusX, neg);
   fe qb = fe_select(q.YplusX, q.YminusX, neg);
-  fe A = fe_mul(fe_add(p.Y, p.X), qa);
-  fe B = fe_mul(fe_sub(p.Y, p.X), qb);
-  fe C = fe_mul(p.T, q.T2d);
-  fe D = affine_q ? fe_carry(fe_add(p.Z, p.Z)) : fe_mul(p.Z, q.Z2);
+  fe A, B, C, D;
+  fe_mul_x2(A, B, fe_add(p.Y, p.X), qa, fe_sub(p.Y, p.X), qb);
+  if (affine_q) {
+    C = fe_mul(p.T, q.T2d);
+    D = fe_carry(fe_add(p.Z, p.Z));
+  } else {
+    fe_mul_x2(C, D, p.T, q.T2d, p.Z, q.Z2);
+  }
   fe Dp = fe_add(D, C), Dm = fe_sub(D, C);
   ge_p1p1 r;
   r.X = fe_sub(A, B);
