@@ -48,7 +48,7 @@ def body_template() -> bytes:
     return H.parse_header(bytes.fromhex(kats["headers"][0]["raw"])).body
 
 
-def synth_headers(n: int, npools: int, device, first: int = 0):
+def synth_headers(n: int, npools: int, device, first: int = 0, keep_nodes: bool = False):
     """Device-resident SoA header batch (torch uint8 tensors)."""
     import torch
 
@@ -81,7 +81,85 @@ def synth_headers(n: int, npools: int, device, first: int = 0):
     if rc != 0:
         raise RuntimeError(f"ouro_synth_headers failed: {rc}")
     torch.cuda.synchronize()
+    if keep_nodes:
+        return t, blen, nodes
     return t, blen
+
+
+RAW_OFFSET_NAMES = ["body", "body_len", "slot", "prev", "issuer", "vrf", "eta_out", "eta_proof",
+                    "lead_out", "lead_proof", "hot", "sigma", "sig"]
+
+
+def raw_template():
+    """Wire-header template for synthesised raw headers:
+    #6.24(bytes .cbor [header_body, kes_sig]) with the golden Shelley body
+    re-encoded -- slot as a 4-byte uint, counter = kesPeriod = 0 (the synthetic
+    opcerts sign counter 0, period 0), the other fields at fixed offsets that
+    the device fills (ouro_synth_raw_headers).  Returns (bytes, offsets)."""
+    from ouroboros_network_amd import header as H
+
+    golden = body_template()
+    f = H.array_items(golden, 0)
+    raw = lambda k: golden[f[k][0]:f[k][1]]  # noqa: E731
+    body = bytearray(b"\x8f")
+    offs = {}
+
+    def put(name, head, size):
+        body.extend(head)
+        offs[name] = len(body)
+        body.extend(b"\0" * size)
+
+    body += raw(0)                                   # blockNo
+    put("slot", b"\x1a", 4)                          # slot (4-byte uint)
+    put("prev", b"\x58\x20", 32)                     # prevHash
+    put("issuer", b"\x58\x20", 32)
+    put("vrf", b"\x58\x20", 32)
+    body += b"\x82"
+    put("eta_out", b"\x58\x40", 64)
+    put("eta_proof", b"\x58\x50", 80)
+    body += b"\x82"
+    put("lead_out", b"\x58\x40", 64)
+    put("lead_proof", b"\x58\x50", 80)
+    body += raw(7) + raw(8)                          # bodySize, bodyHash
+    put("hot", b"\x58\x20", 32)
+    body += b"\x00\x00"                              # counter 0, kesPeriod 0
+    put("sigma", b"\x58\x40", 64)
+    body += raw(13) + raw(14)                        # protocol version
+    inner = b"\x82" + bytes(body) + b"\x59\x01\xc0" + b"\0" * 448
+    prefix = b"\xd8\x18\x59" + len(inner).to_bytes(2, "big")
+    base = len(prefix) + 1                           # header_body starts after 0x82
+    out = {k: base + v for k, v in offs.items()}
+    out["body"] = base
+    out["body_len"] = len(body)
+    out["sig"] = len(prefix) + len(inner) - 448
+    return prefix + inner, [out[k] for k in RAW_OFFSET_NAMES]
+
+
+def synth_raw_headers(n: int, npools: int, device, first: int = 0,
+                      slots_per_kes_period: int = 129600):
+    """Synthetic SoA batch plus the same headers as raw wire CBOR on the device
+    (n x raw_len bytes, uint8 tensor): (t, raw, raw_len)."""
+    import torch
+
+    t, _blen, nodes = synth_headers(n, npools, device, first, keep_nodes=True)
+    tmpl, offs = raw_template()
+    lib = ctypes.CDLL(SYNTH_SO)
+    raw = torch.empty(n * len(tmpl), dtype=torch.uint8, device=device)
+    dt = torch.frombuffer(bytearray(tmpl), dtype=torch.uint8).to(device)
+    o = (ctypes.c_uint32 * 13)(*offs)
+    P = ctypes.c_void_p
+    fn = lib.ouro_synth_raw_headers
+    fn.restype = ctypes.c_int
+    fn.argtypes = [ctypes.c_size_t, ctypes.c_uint64, ctypes.c_int, P, P, ctypes.c_uint32, P,
+                   ctypes.c_uint64] + [P] * 8
+    rc = fn(n, first, npools, nodes.data_ptr(), dt.data_ptr(), len(tmpl), o,
+            slots_per_kes_period, *[t[k].data_ptr() for k in (
+                "issuer_vk", "vrf_vk", "eta_proof", "leader_proof", "hot_vk", "ocert_sigma",
+                "kes_t")], raw.data_ptr())
+    if rc != 0:
+        raise RuntimeError(f"ouro_synth_raw_headers failed: {rc}")
+    torch.cuda.synchronize()
+    return t, raw, len(tmpl)
 
 
 class DeviceHeaders:
@@ -490,6 +568,87 @@ def e2e_leg(hdr, n: int, reps: int = 3):
     return res
 
 
+def raw_leg(n: int, npools: int, device, threads: int, chunk: int = 1 << 18, reps: int = 3):
+    """Raw wire CBOR -> verdicts: n synthetic headers as
+    the bytes ChainSync hands over (#6.24-wrapped [header_body, kes_sig],
+    bench.raw_template), in pageable host memory.  Per chunk the C slicer
+    (ouro_tpraos_pack_cbor, `threads` host threads) builds the SoA, then
+    ouro_tpraos_verify_batch runs H2D + header kernel + D2H; the slicing of
+    chunk k+1 overlaps the verification of chunk k.  The slicer alone is timed
+    too.  Never `value` (host buffers, PCIe-inclusive)."""
+    import threading
+
+    from ouroboros_network_amd import _native
+
+    t, raw, rl = synth_raw_headers(n, npools, device)
+    rawh = raw.cpu().numpy()
+    del raw
+    ea = t["eta_alpha"].cpu().numpy()
+    la = t["leader_alpha"].cpu().numpy()
+    del t
+    lib = _native.load()
+    P = lambda a: a.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
+    off = np.arange(n, dtype=np.uint64) * rl
+    ln = np.full(n, rl, np.uint32)
+    nch = (n + chunk - 1) // chunk
+    arenas = [np.zeros(lib.ouro_tpraos_pack_bytes(chunk), np.uint8) for _ in range(2)]
+    status = np.zeros(n, np.uint8)
+    verdict = np.zeros(n, np.uint8)
+    be = np.zeros((n, 64), np.uint8)
+    bl = np.zeros((n, 64), np.uint8)
+    structs = [_native.TPraosBatch() for _ in range(nch)]
+
+    def pack(k):
+        lo = k * chunk
+        m = min(chunk, n - lo)
+        a = arenas[k % 2]
+        rc = lib.ouro_tpraos_pack_cbor(P(rawh), rawh.size, P(off[lo:]), P(ln[lo:]), m, 129600,
+                                       P(a), a.size, ctypes.byref(structs[k]), None, None,
+                                       P(status[lo:]), threads)
+        assert rc == 0, rc
+        structs[k].eta_alpha = ea.ctypes.data + 32 * lo
+        structs[k].leader_alpha = la.ctypes.data + 32 * lo
+
+    def verify(k):
+        lo = k * chunk
+        rc = lib.ouro_tpraos_verify_batch(ctypes.byref(structs[k]), P(verdict[lo:]), P(be[lo:]),
+                                          P(bl[lo:]))
+        _native.check(rc, "ouro_tpraos_verify_batch")
+
+    def run_pipelined():
+        pack(0)
+        for k in range(nch):
+            th = None
+            if k + 1 < nch:
+                # arena (k+1) % 2 is free: chunk k-1's verify has returned
+                th = threading.Thread(target=pack, args=(k + 1,))
+                th.start()
+            verify(k)
+            if th:
+                th.join()
+
+    run_pipelined()  # warm: device buffers, pinned staging, arena pages
+    best = min(_timed(run_pipelined) for _ in range(reps))
+    ok = bool((status == 0).all() and (verdict == 0x3F).all())
+    pk_t = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        for k in range(nch):
+            pack(k)
+        pk_t.append(time.perf_counter() - t0)
+    return {"workload": f"{n} raw wire headers ({rl} B each, pageable host memory) -> C slicer "
+                        f"({threads} threads, chunks of {chunk}) -> ouro_tpraos_verify_batch",
+            "headers_per_s": round(n / best, 1), "ms": round(best * 1e3, 2),
+            "slicer_headers_per_s": round(n / min(pk_t), 1), "slicer_threads": threads,
+            "all_valid": ok}
+
+
+def _timed(fn) -> float:
+    t0 = time.perf_counter()
+    fn()
+    return time.perf_counter() - t0
+
+
 def load_pmc_traffic():
     """HBM bytes per header of one header-kernel launch from the committed PMC
     run (profiles/pmc_traffic.json, tools/summarize_profile.py), with whether
@@ -769,6 +928,11 @@ def main():
                 out["e2e"] = e2e_leg(hdr, n)
             except Exception as e:  # noqa: BLE001
                 out["e2e"] = {"error": str(e)}
+        if not args.no_e2e and world == 1:
+            try:
+                out["raw_cbor"] = raw_leg(n, args.pools, device, cpu["usable"])
+            except Exception as e:  # noqa: BLE001
+                out["raw_cbor"] = {"error": str(e)}
         if not args.no_latency and world == 1:
             try:
                 out["latency"] = latency_leg(hdr, 64, args.lat_iters, cpu["usable"],

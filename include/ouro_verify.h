@@ -200,6 +200,42 @@ typedef struct ouro_tpraos_batch {
 int ouro_tpraos_verify_batch(const ouro_tpraos_batch *b, uint8_t *verdict,
                              uint8_t *beta_eta, uint8_t *beta_leader);
 
+/* Raw header CBOR -> the SoA above.  Replaces the
+ * per-header decode the reference runs on every header ChainSync receives
+ * (ouroboros-consensus-shelley/src/Ouroboros/Consensus/Shelley/Ledger/Block.hs:216-217,
+ * the Annotator keeping the raw header_body bytes; N2N wrapping at
+ * .../Shelley/Node/Serialisation.hs:88-90) with one host call per batch.
+ * Header i is raw[off[i] .. off[i] + len[i]) as it came off the wire:
+ *   #6.24(bytes .cbor [header_body, kes_sig])             (N2N v1), or
+ *   [era, #6.24(bytes .cbor [header_body, kes_sig])]      (Cardano HFC, era >= 1)
+ * header_body = [blockNo, slot, prevHash, issuerVk, vrfVk, [etaOut, etaProof],
+ * [leaderOut, leaderProof], bodySize, bodyHash, hotVk, counter, kesPeriod,
+ * sigma, protMajor, protMinor] (ouroboros-network/test/messages.cddl:27-34).
+ * The fixed-size fields are copied into `arena` (ouro_tpraos_pack_bytes(n)
+ * bytes, any alignment) and *out's required members and eta_output /
+ * leader_output (the claimed outputs) are pointed at them; body = raw and
+ * body_off / body_len are the header_body spans inside raw (the KES message,
+ * not copied); kes_t = kesPeriod(slot) - kesPeriod, clamped at 0 and saturated
+ * at 2^32 - 1 (Integrity.hs:38-44).  eta_alpha / leader_alpha / slot /
+ * epoch_nonce / eta_nonce are left to the caller (set out->slot = slot and
+ * epoch_nonce to have the device derive the VRF inputs).  slot / era (n
+ * each, may be NULL) receive bheaderSlotNo and the HFC era (1 if unwrapped).
+ * status[i] = OURO_PACK_*; a rejected header's rows are zero (every verdict
+ * bit then fails).  nthreads <= 0: one per hardware thread (at least 4096
+ * headers each).  Host-only.  Returns OURO_OK, or OURO_EINVAL for bad
+ * arguments (a span outside raw_bytes, a short arena, NULLs). */
+#define OURO_PACK_OK 0u
+#define OURO_PACK_ECBOR 1u  /* malformed or truncated CBOR                    */
+#define OURO_PACK_ESHAPE 2u /* not the header shape (tag 24, [body, sig], 15
+                               fields, [output, proof] certs, uint/bytes types) */
+#define OURO_PACK_ESIZE 3u  /* a fixed-size crypto field has the wrong length  */
+#define OURO_PACK_EBYRON 4u /* HFC era 0: a Byron header, not TPraos          */
+size_t ouro_tpraos_pack_bytes(size_t n);
+int ouro_tpraos_pack_cbor(const uint8_t *raw, size_t raw_bytes, const uint64_t *off,
+                          const uint32_t *len, size_t n, uint64_t slots_per_kes_period,
+                          void *arena, size_t arena_bytes, ouro_tpraos_batch *out,
+                          uint64_t *slot, uint8_t *era, uint8_t *status, int nthreads);
+
 /* The host-side UPDN fold (ledger-specs; the per-header step of
  * SL.updateChainDepState after the crypto): for i = 0..n-1
  *   eta_v <- eta_v (*) eta_nonce[i]

@@ -106,6 +106,9 @@ SIGNATURES = {
     "ouro_leader_check_batch_device": (_I, [_P, _SZ, _P, _P, _P, ctypes.c_int64, ctypes.c_uint64,
                                             _I, _P]),
     "ouro_nonce_fold": (_I, [_SZ, _P, _P, ctypes.c_uint64, ctypes.c_uint64, _P, _P, _P]),
+    "ouro_tpraos_pack_bytes": (_SZ, [_SZ]),
+    "ouro_tpraos_pack_cbor": (_I, [_P, _SZ, _P, _P, _SZ, ctypes.c_uint64, _P, _SZ,
+                                   ctypes.POINTER(TPraosBatch), _P, _P, _P, _I]),
 }
 
 # the cardano-crypto-praos names the library also exports (include/ouro_verify.h)

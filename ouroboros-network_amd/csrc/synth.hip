@@ -13,6 +13,7 @@
 // (tests/test_synth.py).
 #include <hip/hip_runtime.h>
 
+#include <cstring>
 #include <vector>
 
 #include "synth.h"
@@ -262,6 +263,88 @@ __global__ void __launch_bounds__(kBlock) k_synth_headers(
   }
 }
 
+
+// Raw wire headers (#6.24(bytes .cbor [header_body, kes_sig])) consistent with
+// a synthesised SoA batch, for the raw-CBOR -> verdict bench leg and tests:
+// the host-built template (bench.raw_template: the golden body re-encoded with
+// a 4-byte slot and counter = kesPeriod = 0) gets this header's prevHash seed,
+// keys, VRF certificates (outputs = proof_to_hash of the proofs), sigma and a
+// slot in KES period t; then the header_body bytes are KES-signed in place.
+struct RawOffsets {
+  uint32_t body, body_len, slot, prev, issuer, vrf, eta_out, eta_proof, lead_out, lead_proof,
+      hot, sigma, sig;
+};
+__device__ void proof_output(uint8_t* dst, const uint8_t* proof) {
+  uint32_t G[8];
+  for (int k = 0; k < 8; k++)
+    G[k] = proof[4 * k] | (proof[4 * k + 1] << 8) | (proof[4 * k + 2] << 16) |
+           ((uint32_t)proof[4 * k + 3] << 24);
+  ge_p3 Gamma;
+  ge_decode(&Gamma, G, false);
+  ge_p3 G8 = ge_mul8(Gamma);
+  uint32_t enc[8];
+  ge_encode_with_inv(enc, G8.X, G8.Y, fe_invert(G8.Z));
+  uint32_t bp[9];
+  bp[0] = 0x04u | (0x03u << 8) | (enc[0] << 16);
+  for (int k = 1; k < 8; k++) bp[k] = (enc[k - 1] >> 16) | (enc[k] << 16);
+  bp[8] = enc[7] >> 16;
+  uint64_t H[8];
+  sha512_prefixed<34>(H, bp, ShaNoTail{}, 0);
+  uint32_t w[16];
+  sha512_digest_words(w, H);
+  for (int k = 0; k < 64; k++) dst[k] = (uint8_t)byte_of(w, k);
+}
+__global__ void __launch_bounds__(kBlock) k_synth_raw(
+    size_t n, uint64_t first, int npools, Tag tbody, Tag tkes, const uint32_t* nodes,
+    const uint8_t* tmpl, uint32_t raw_len, RawOffsets o, uint64_t spkp, const uint8_t* issuer_vk,
+    const uint8_t* vrf_vk, const uint8_t* eta_proof, const uint8_t* leader_proof,
+    const uint8_t* hot_vk, const uint8_t* sigma, const uint32_t* kes_t, uint8_t* raw,
+    int32_t* scratch, const int32_t* btab) {
+  const size_t tid = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const size_t nth = (size_t)gridDim.x * blockDim.x;
+  const Slot lane = slot_of(scratch, tid, kLaneWords);
+  for (size_t i = tid; i < n; i += nth) {
+    const uint64_t g = first + i;
+    const int j = (int)(g % (uint64_t)npools);
+    const uint32_t t = kes_t[i];
+    uint8_t* r = raw + i * (size_t)raw_len;
+    for (uint32_t b = 0; b < raw_len; b++) r[b] = tmpl[b];
+    const uint32_t slot = (uint32_t)(t * spkp + g % 1000);
+    for (int b = 0; b < 4; b++) r[o.slot + b] = (uint8_t)(slot >> (24 - 8 * b));
+    uint32_t ph[8];
+    seed_of(ph, tbody, g);
+    for (int b = 0; b < 32; b++) r[o.prev + b] = (uint8_t)byte_of(ph, b);
+    for (int b = 0; b < 32; b++) {
+      r[o.issuer + b] = issuer_vk[32 * i + b];
+      r[o.vrf + b] = vrf_vk[32 * i + b];
+      r[o.hot + b] = hot_vk[32 * i + b];
+    }
+    for (int b = 0; b < 80; b++) {
+      r[o.eta_proof + b] = eta_proof[80 * i + b];
+      r[o.lead_proof + b] = leader_proof[80 * i + b];
+    }
+    for (int b = 0; b < 64; b++) r[o.sigma + b] = sigma[64 * i + b];
+    proof_output(r + o.eta_out, eta_proof + 80 * i);
+    proof_output(r + o.lead_out, leader_proof + 80 * i);
+    // KES: leaf t of pool j signs the header_body bytes; Merkle pairs bottom-up
+    uint32_t ts[8], ls[8];
+    seed_of(ts, tkes, (uint64_t)j);
+    kes_leaf_seed(ls, ts, t);
+    ExpandedKey leaf;
+    expand_seed(leaf, ls, lane, btab);
+    uint32_t lsig[16];
+    ed25519_sign_lane(lsig, leaf, ShaGlobalTail{r + o.body}, o.body_len, lane, btab);
+    uint8_t* ks = r + o.sig;
+    for (int b = 0; b < 64; b++) ks[b] = (uint8_t)byte_of(lsig, b);
+    const uint32_t* nb = nodes + (size_t)j * 127 * 8;
+    for (int k = 1; k <= 6; k++) {
+      const int idx = (int)(t >> (k - 1)) & ~1;
+      const uint32_t* pair = nb + node_index(k - 1, idx) * 8;  // vk0 || vk1
+      for (int b = 0; b < 64; b++) ks[64 + 64 * (k - 1) + b] = (uint8_t)byte_of(pair, b);
+    }
+  }
+}
+
 // ---- host launchers (device pointers; synchronous) ---------------------------
 namespace {
 Tag make_tag(const char* s) {
@@ -381,6 +464,26 @@ int ouro_synth_headers(size_t n, uint64_t first, int npools, const uint8_t* body
                      nodes, body_tmpl, body_len, issuer_vk, vrf_vk, eta_proof, leader_proof,
                      eta_alpha, leader_alpha, hot_vk, counter, c0, sigma, kes_t, kes_sig, body,
                      body_off, body_lens, g_ctx.scratch, g_ctx.btab);
+  return done();
+}
+
+// raw wire headers for a batch made by ouro_synth_headers (same n, first,
+// npools, nodes); offs = 13 uint32 (RawOffsets order), tmpl on the device
+int ouro_synth_raw_headers(size_t n, uint64_t first, int npools, const uint32_t* nodes,
+                           const uint8_t* tmpl, uint32_t raw_len, const uint32_t* offs,
+                           uint64_t slots_per_kes_period, const uint8_t* issuer_vk,
+                           const uint8_t* vrf_vk, const uint8_t* eta_proof,
+                           const uint8_t* leader_proof, const uint8_t* hot_vk,
+                           const uint8_t* sigma, const uint32_t* kes_t, uint8_t* raw) {
+  if (npools <= 0 || slots_per_kes_period == 0) return -3;
+  RawOffsets o;
+  memcpy(&o, offs, sizeof(o));
+  if (o.body + o.body_len > raw_len || o.sig + 448 > raw_len) return -3;
+  if (prepare(n)) return -2;
+  hipLaunchKernelGGL(k_synth_raw, dim3(grid_for(n)), dim3(kBlock), 0, 0, n, first, npools,
+                     make_tag("body"), make_tag("kes"), nodes, tmpl, raw_len, o,
+                     slots_per_kes_period, issuer_vk, vrf_vk, eta_proof, leader_proof, hot_vk,
+                     sigma, kes_t, raw, g_ctx.scratch, g_ctx.btab);
   return done();
 }
 }

@@ -60,6 +60,8 @@ def skip(buf: bytes, i: int) -> int:
             while buf[j] != 0xFF:
                 j = skip(buf, j)
             return j + 1
+        if j + arg > len(buf):
+            raise CBORError("truncated")  # (a short final string is not a shorter one)
         return j + arg
     if mt in (4, 5):
         count = arg * (2 if mt == 5 else 1)
@@ -99,6 +101,8 @@ def bytes_at(buf: bytes, i: int) -> bytes:
     mt, arg, j = _head(buf, i)
     if mt != 2 or arg < 0:
         raise CBORError(f"expected definite bytes at {i}")
+    if j + arg > len(buf):
+        raise CBORError("truncated")
     return bytes(buf[j:j + arg])
 
 
@@ -234,6 +238,97 @@ def pack(headers: Sequence[ShelleyHeader], eta_alpha: Optional[Sequence[bytes]] 
         slot=np.array([h.slot for h in headers], np.uint64) if seeds else None,
         epoch_nonce=np.frombuffer(epoch_nonce, np.uint8) if (seeds and epoch_nonce) else None,
     )
+
+
+PACK_OK, PACK_ECBOR, PACK_ESHAPE, PACK_ESIZE, PACK_EBYRON = 0, 1, 2, 3, 4
+
+
+@dataclass
+class PackedHeaders:
+    """Result of :func:`pack_cbor`: the batch (arrays view the C arena and the
+    raw buffer, which this object keeps alive), per-header status
+    (PACK_*), slots and HFC eras."""
+    batch: HeaderBatch
+    status: np.ndarray
+    slot: np.ndarray
+    era: np.ndarray
+    _keep: tuple = ()
+
+
+def pack_cbor(raw_headers, *, slots_per_kes_period: int = 129600,
+              eta_alpha: Optional[np.ndarray] = None, leader_alpha: Optional[np.ndarray] = None,
+              seeds: bool = False, epoch_nonce: Optional[bytes] = None, claimed: bool = True,
+              nthreads: int = 0) -> PackedHeaders:
+    """Raw header CBOR -> SoA batch through the C slicer of the product library
+    (include/ouro_verify.h ouro_tpraos_pack_cbor; csrc/pack.cpp).  Same
+    acceptance and arrays as parse_header + pack, without per-header Python.
+
+    raw_headers: a sequence of bytes (one header each), or (buf, off, len)
+    with the headers at buf[off[i]:off[i]+len[i]].  VRF inputs as for pack:
+    the caller's alphas, or seeds=True (+ epoch_nonce) for mkSeed on device.
+    Rejected headers (status != PACK_OK) get zero rows: they fail every check."""
+    import ctypes
+
+    from . import _native
+    lib = _native.load()
+    if isinstance(raw_headers, tuple) and len(raw_headers) == 3:
+        buf, off, ln = raw_headers
+        buf = np.frombuffer(buf, np.uint8) if isinstance(buf, (bytes, bytearray)) else \
+            np.ascontiguousarray(buf, np.uint8).reshape(-1)
+        off = np.ascontiguousarray(off, np.uint64)
+        ln = np.ascontiguousarray(ln, np.uint32)
+    else:
+        items = [bytes(r) for r in raw_headers]
+        ln = np.array([len(r) for r in items], np.uint32)
+        off = np.zeros(len(items), np.uint64)
+        if len(items) > 1:
+            off[1:] = np.cumsum(ln[:-1], dtype=np.uint64)
+        buf = np.frombuffer(b"".join(items) or b"\0", np.uint8)
+    n = int(off.size)
+    if ln.size != n:
+        raise ValueError("off / len: one entry per header")
+    if epoch_nonce is not None and len(epoch_nonce) != 32:
+        raise ValueError("epoch_nonce: 32 bytes")
+    if not seeds and (eta_alpha is None or leader_alpha is None):
+        raise ValueError("one eta/leader alpha per header (or seeds=True)")
+    nbytes = int(lib.ouro_tpraos_pack_bytes(n))
+    arena = np.empty(nbytes, np.uint8)
+    status = np.zeros(max(n, 1), np.uint8)
+    slot = np.zeros(max(n, 1), np.uint64)
+    era = np.zeros(max(n, 1), np.uint8)
+    out = _native.TPraosBatch()
+    ptr = lambda a: a.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
+    rc = lib.ouro_tpraos_pack_cbor(ptr(buf), buf.size, ptr(off), ptr(ln), n,
+                                   slots_per_kes_period, ptr(arena), nbytes, ctypes.byref(out),
+                                   ptr(slot), ptr(era), ptr(status), nthreads)
+    if rc != _native.OURO_OK:
+        raise ValueError(f"ouro_tpraos_pack_cbor: {rc} (spans outside the buffer?)")
+    base = arena.ctypes.data
+
+    def view(addr, dt, w):
+        if n == 0:
+            return np.zeros((0, w) if w else 0, dt)
+        cnt = n * (w or 1)
+        a = arena[addr - base: addr - base + cnt * np.dtype(dt).itemsize].view(dt)
+        return a.reshape(n, w) if w else a
+
+    batch = HeaderBatch(
+        issuer_vk=view(out.issuer_vk, np.uint8, 32), vrf_vk=view(out.vrf_vk, np.uint8, 32),
+        eta_proof=view(out.eta_proof, np.uint8, 80),
+        leader_proof=view(out.leader_proof, np.uint8, 80),
+        eta_alpha=None if seeds else eta_alpha, leader_alpha=None if seeds else leader_alpha,
+        hot_vk=view(out.hot_vk, np.uint8, 32),
+        ocert_counter=view(out.ocert_counter, np.uint64, None),
+        ocert_kes_period=view(out.ocert_kes_period, np.uint64, None),
+        ocert_sigma=view(out.ocert_sigma, np.uint8, 64), kes_t=view(out.kes_t, np.uint32, None),
+        kes_sig=view(out.kes_sig, np.uint8, 448), body=buf,
+        body_off=view(out.body_off, np.uint64, None), body_len=view(out.body_len, np.uint32, None),
+        eta_output=view(out.eta_output, np.uint8, 64) if claimed else None,
+        leader_output=view(out.leader_output, np.uint8, 64) if claimed else None,
+        slot=slot[:n] if seeds else None,
+        epoch_nonce=np.frombuffer(epoch_nonce, np.uint8) if (seeds and epoch_nonce) else None,
+    )
+    return PackedHeaders(batch, status[:n], slot[:n], era[:n], (arena, buf))
 
 
 def _blake2b_256(m: bytes) -> bytes:

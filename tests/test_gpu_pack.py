@@ -1,0 +1,112 @@
+"""Raw wire CBOR -> verdicts on the GPU: headers sliced
+by the C slicer (ouro_tpraos_pack_cbor) give the verdicts and outputs of the
+Python-sliced batch and of the oracle; synthesised raw headers (keys, VRF
+certificates with their real outputs, opcerts, KES over the encoded body) are
+all valid end to end, and corruptions of their wire bytes are judged like the
+oracle judges the same sliced batch."""
+import os
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+import oracle_ffi as O  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+
+def test_golden_raw_headers_through_the_c_slicer(gpu_lib, kats):
+    from ouroboros_network_amd import header as H
+    from ouroboros_network_amd import verify_headers
+
+    hs = kats["headers"]
+    raws = [bytes.fromhex(h["raw"]) for h in hs]
+    ea = np.array([list(bytes.fromhex(h["eta_alpha"])) for h in hs], np.uint8)
+    la = np.array([list(bytes.fromhex(h["leader_alpha"])) for h in hs], np.uint8)
+    pk = H.pack_cbor(raws, slots_per_kes_period=100, eta_alpha=ea, leader_alpha=la)
+    assert (pk.status == H.PACK_OK).all()
+    verdict, be, bl = verify_headers(pk.batch)
+    ref = H.pack([H.parse_header(r) for r in raws], [bytes(a) for a in ea], [bytes(a) for a in la],
+                 slots_per_kes_period=100)
+    rv, rbe, rbl = verify_headers(ref)
+    np.testing.assert_array_equal(verdict, rv)
+    np.testing.assert_array_equal(be, rbe)
+    np.testing.assert_array_equal(bl, rbl)
+    for h, v in zip(hs, verdict):
+        assert int(v) & 0x0F == h["expect_verdict"], h["name"]
+
+
+def test_synthesised_raw_headers_end_to_end(gpu_lib):
+    import torch
+
+    import bench
+    from ouroboros_network_amd import header as H
+    from ouroboros_network_amd import verify_headers
+
+    n = 2048
+    dev = torch.device("cuda", 0)
+    t, raw, rl = bench.synth_raw_headers(n, 64, dev)
+    rawh = raw.cpu().numpy()
+    off = np.arange(n, dtype=np.uint64) * rl
+    ln = np.full(n, rl, np.uint32)
+    host = {k: v.cpu().numpy() for k, v in t.items()}
+    ea = host["eta_alpha"].reshape(n, 32)
+    la = host["leader_alpha"].reshape(n, 32)
+    pk = H.pack_cbor((rawh, off, ln), eta_alpha=ea, leader_alpha=la, nthreads=2)
+    assert (pk.status == H.PACK_OK).all()
+    b = pk.batch
+    for k, w in (("issuer_vk", 32), ("vrf_vk", 32), ("eta_proof", 80), ("leader_proof", 80),
+                 ("hot_vk", 32), ("ocert_sigma", 64)):
+        np.testing.assert_array_equal(getattr(b, k), host[k].reshape(n, w), k)
+    np.testing.assert_array_equal(b.kes_t, host["kes_t"].view(np.uint32))
+    assert not b.ocert_counter.any() and not b.ocert_kes_period.any()
+    verdict, be, bl = verify_headers(b)
+    assert (verdict == 0x3F).all()  # every check, claimed outputs = computed
+    np.testing.assert_array_equal(be, b.eta_output)
+    np.testing.assert_array_equal(bl, b.leader_output)
+
+    # wire corruptions: a byte in each of the body, the KES signature and a
+    # claimed output; verdicts equal the oracle's on the sliced batch
+    rng = np.random.default_rng(11)
+    tmpl, offs = bench.raw_template()
+    o = dict(zip(bench.RAW_OFFSET_NAMES, offs))
+    bad = rawh.copy().reshape(n, rl)
+    rows = rng.choice(n, 96, replace=False)
+    for k, r in enumerate(rows):
+        lo, hi = [(o["body"], o["body"] + o["body_len"]), (o["sig"], o["sig"] + 448),
+                  (o["eta_out"], o["eta_out"] + 64)][k % 3]
+        bad[r, int(rng.integers(lo, hi))] ^= 1 << int(rng.integers(0, 8))
+    pk2 = H.pack_cbor((bad.reshape(-1), off, ln), eta_alpha=ea, leader_alpha=la)
+    sel = np.sort(rows)
+    v2, be2, bl2 = verify_headers(pk2.batch)
+    wv, wbe, wbl = O.tpraos_verify_batch(_rows(pk2.batch, sel))
+    np.testing.assert_array_equal(v2[sel], wv)
+    np.testing.assert_array_equal(be2[sel], wbe)
+    np.testing.assert_array_equal(bl2[sel], wbl)
+    assert (v2[np.setdiff1d(np.arange(n), sel)] == 0x3F).all()
+    assert (v2[sel] != 0x3F).all()  # every corruption is caught by some check
+
+
+def _rows(batch, sel):
+    """The headers `sel` of a batch as a new HeaderBatch (for the oracle)."""
+    from ouroboros_network_amd.tpraos import HeaderBatch
+
+    def pick(a):
+        return None if a is None else a[sel]
+
+    bodies = [bytes(batch.body[int(batch.body_off[i]):int(batch.body_off[i]) + int(batch.body_len[i])])
+              for i in sel]
+    lens = np.array([len(x) for x in bodies], np.uint32)
+    offs = np.zeros(len(sel), np.uint64)
+    offs[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
+    return HeaderBatch(
+        issuer_vk=pick(batch.issuer_vk), vrf_vk=pick(batch.vrf_vk), eta_proof=pick(batch.eta_proof),
+        leader_proof=pick(batch.leader_proof), eta_alpha=pick(batch.eta_alpha),
+        leader_alpha=pick(batch.leader_alpha), hot_vk=pick(batch.hot_vk),
+        ocert_counter=pick(batch.ocert_counter), ocert_kes_period=pick(batch.ocert_kes_period),
+        ocert_sigma=pick(batch.ocert_sigma), kes_t=pick(batch.kes_t), kes_sig=pick(batch.kes_sig),
+        body=np.frombuffer(b"".join(bodies), np.uint8), body_off=offs, body_len=lens,
+        eta_output=pick(batch.eta_output), leader_output=pick(batch.leader_output))
