@@ -5,6 +5,9 @@
 // fly from a byte source: a wave-uniform register prefix followed by bytes
 // fetched from global memory, so nothing is staged per lane.
 #pragma once
+#include <type_traits>
+#include <utility>
+
 #include "common.h"
 
 namespace ouro {
@@ -97,14 +100,62 @@ OURO_NI void sha512_compress(uint64_t H[8], uint64_t W[16]) {
 }
 
 // Byte sources.  `prefix(p)` is only ever asked for a compile-time p < PL in
-// the first block; `tail(q)` reads message byte q from global memory.
+// the first block; `tail(q)` reads message byte q.  A source may also offer
+// word_be(q, tl): bytes q..q+7 as one big-endian word (bytes at or beyond tl
+// arbitrary); the others are assembled byte by byte (sha_tail_word).
 struct ShaNoTail {
   OURO_FI uint32_t tail(uint32_t) const { return 0; }
 };
+// bytes in global memory at any alignment: the dwords covering q..q+7 (only
+// those that start before the message end: never a load past the buffer),
+// funnel-shifted into place (v_alignbit) and byte-swapped -- three dword loads
+// per eight bytes instead of eight byte loads with their shifts and ORs
 struct ShaGlobalTail {
   const uint8_t* msg;
   OURO_FI uint32_t tail(uint32_t q) const { return ldg_u8(msg + q); }
+#if defined(__HIP_DEVICE_COMPILE__)
+  OURO_FI uint64_t word_be(uint32_t q, uint32_t tl) const {
+    const uintptr_t a = reinterpret_cast<uintptr_t>(msg) + q;
+    const uintptr_t end = reinterpret_cast<uintptr_t>(msg) + tl;
+    const uintptr_t w = a & ~uintptr_t(3);
+    const uint32_t sh = (uint32_t)(a & 3) * 8;
+    const uint32_t d0 = w < end ? (uint32_t)ldg1(reinterpret_cast<const void*>(w)) : 0u;
+    const uint32_t d1 = w + 4 < end ? (uint32_t)ldg1(reinterpret_cast<const void*>(w + 4)) : 0u;
+    const uint32_t d2 = w + 8 < end ? (uint32_t)ldg1(reinterpret_cast<const void*>(w + 8)) : 0u;
+    const uint32_t lo = __builtin_amdgcn_alignbit(d1, d0, sh);  // bytes q..q+3, little-endian
+    const uint32_t hi = __builtin_amdgcn_alignbit(d2, d1, sh);  // bytes q+4..q+7
+    return ((uint64_t)__builtin_bswap32(lo) << 32) | __builtin_bswap32(hi);
+  }
+#endif
 };
+
+template <class T, class = void>
+struct has_word_be : std::false_type {};
+template <class T>
+struct has_word_be<T, decltype((void)std::declval<const T&>().word_be(0u, 0u))> : std::true_type {};
+
+// bytes q..q+7 of a tail as a big-endian word (bytes at or beyond tl arbitrary)
+template <class Tail>
+OURO_FI uint64_t sha_tail_word(const Tail& t, uint32_t q, uint32_t tl) {
+  if constexpr (has_word_be<Tail>::value) {
+    return t.word_be(q, tl);
+  } else {
+    uint64_t r = 0;
+#pragma unroll
+    for (int k = 0; k < 8; k++) r = (r << 8) | (q + k < tl ? t.tail(q + k) : 0u);
+    return r;
+  }
+}
+
+// the padded message word at byte position p (>= PL) from its raw tail bytes:
+// data before `total`, the 0x80 terminator at `total`, zeros after
+OURO_FI uint64_t sha_pad_word(uint64_t raw, uint32_t p, uint32_t total) {
+  if (p + 8 <= total) return raw;
+  if (p >= total) return p == total ? (0x80ull << 56) : 0ull;
+  const uint32_t v = total - p;  // 1..7 message bytes in this word
+  const uint64_t keep = ~0ull << (64 - 8 * v);
+  return (raw & keep) | (0x80ull << (56 - 8 * v));
+}
 
 // SHA-512 over prefix (PL bytes, as little-endian packed words) || tail (tl
 // bytes).  PL <= 128 - 17 is not required: the prefix may spill into block 1
@@ -124,14 +175,19 @@ OURO_FI void sha512_prefixed(uint64_t out[8], const uint32_t* prefix, const Tail
     uint64_t W[16];
 #pragma unroll
     for (int w = 0; w < 16; w++) {
+      const uint32_t p0 = (uint32_t)(b * 128 + w * 8);
       uint64_t r = 0;
+      if (p0 >= (uint32_t)PL) {
+        r = sha_pad_word(sha_tail_word(tail, p0 - PL, tl), p0, total);
+      } else {
 #pragma unroll
-      for (int k = 0; k < 8; k++) {
-        const uint32_t p = (uint32_t)(b * 128 + w * 8 + k);
-        uint32_t byte;
-        if (p < (uint32_t)PL) byte = byte_of(prefix, (int)p);
-        else byte = (p < total) ? tail.tail(p - PL) : (p == total ? 0x80u : 0u);
-        r = (r << 8) | byte;
+        for (int k = 0; k < 8; k++) {
+          const uint32_t p = p0 + k;
+          uint32_t byte;
+          if (p < (uint32_t)PL) byte = byte_of(prefix, (int)p);
+          else byte = (p < total) ? tail.tail(p - PL) : (p == total ? 0x80u : 0u);
+          r = (r << 8) | byte;
+        }
       }
       const uint32_t widx = (uint32_t)(b * 16 + w);
       if (widx == nb * 16 - 1) r = (uint64_t)total << 3;
@@ -146,13 +202,8 @@ OURO_FI void sha512_prefixed(uint64_t out[8], const uint32_t* prefix, const Tail
     uint64_t W[16];
 #pragma unroll
     for (int w = 0; w < 16; w++) {
-      uint64_t r = 0;
-#pragma unroll
-      for (int k = 0; k < 8; k++) {
-        const uint32_t p = b * 128 + w * 8 + k;
-        const uint32_t byte = (p < total) ? tail.tail(p - PL) : (p == total ? 0x80u : 0u);
-        r = (r << 8) | byte;
-      }
+      const uint32_t p0 = b * 128 + w * 8;
+      uint64_t r = sha_pad_word(sha_tail_word(tail, p0 - PL, tl), p0, total);
       const uint32_t widx = b * 16 + w;
       if (widx == nb * 16 - 1) r = (uint64_t)total << 3;
       else if (widx == nb * 16 - 2) r = 0;

@@ -23,6 +23,7 @@ def main():
     ap.add_argument("libs", nargs="+")
     ap.add_argument("--headers", type=int, default=1 << 20)
     ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--kes", action="store_true", help="also time the Sum6KES batch kernel")
     args = ap.parse_args()
     import torch
 
@@ -62,6 +63,28 @@ def main():
             assert rc == 0, (p, rc)
             if r > 0:
                 times[p].append(e0.elapsed_time(e1))
+    kes_times = {p: [] for p, _ in libs}
+    if args.kes:
+        kv = {p: torch.zeros(n, dtype=torch.uint8, device=dev) for p, _ in libs}
+        kfns = []
+        for path, _ in libs:
+            lib = ctypes.CDLL(os.path.abspath(path))
+            f = lib.ouro_sum6kes_verify_batch_device
+            f.restype = ctypes.c_int
+            kfns.append((path, f))
+        for r in range(args.rounds + 1):
+            for p, f in kfns:
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(st)
+                rc = f(ctypes.c_void_p(st.cuda_stream), ctypes.c_size_t(n),
+                       *[ctypes.c_void_p(t[k].data_ptr()) for k in
+                         ("hot_vk", "kes_t", "body", "body_off", "body_len", "kes_sig")],
+                       ctypes.c_void_p(kv[p].data_ptr()))
+                e1.record(st)
+                torch.cuda.synchronize()
+                assert rc == 0, (p, rc)
+                if r > 0:
+                    kes_times[p].append(e0.elapsed_time(e1))
     ref = outs[libs[0][0]]
     res = {}
     for p, _ in libs:
@@ -70,6 +93,9 @@ def main():
         res[os.path.basename(p)] = {"median_ms": float(np.median(times[p])), "min_ms": float(np.min(times[p])),
                                     "headers_per_s": n / (np.median(times[p]) * 1e-3),
                                     "all_valid": bool((v == 15).all().item()), "same_as_first": same}
+        if args.kes:
+            res[os.path.basename(p)]["kes_median_ms"] = float(np.median(kes_times[p]))
+            res[os.path.basename(p)]["kes_all_valid"] = bool((kv[p] == 1).all().item())
     print(json.dumps(res, indent=1))
 
 
