@@ -18,6 +18,7 @@ spans instead of re-encoding anything.
 from __future__ import annotations
 
 import hashlib
+import os
 from dataclasses import dataclass
 from typing import List, Optional, Sequence, Tuple
 
@@ -255,6 +256,29 @@ class PackedHeaders:
     _keep: tuple = ()
 
 
+_PACK_LIB = None
+
+
+def _pack_lib():
+    """TEST-ONLY: OURO_PACK_LIB names a library exporting just the slicer (the
+    ASan/UBSan build of csrc/pack.cpp, tests/test_sanitizers.py)."""
+    global _PACK_LIB
+    path = os.environ.get("OURO_PACK_LIB")
+    if not path:
+        return None
+    if _PACK_LIB is None:
+        import ctypes
+
+        from . import _native
+        lib = ctypes.CDLL(path)
+        for name in ("ouro_tpraos_pack_bytes", "ouro_tpraos_pack_cbor"):
+            res, args = _native.SIGNATURES[name]
+            getattr(lib, name).restype = res
+            getattr(lib, name).argtypes = args
+        _PACK_LIB = lib
+    return _PACK_LIB
+
+
 def pack_cbor(raw_headers, *, slots_per_kes_period: int = 129600,
               eta_alpha: Optional[np.ndarray] = None, leader_alpha: Optional[np.ndarray] = None,
               seeds: bool = False, epoch_nonce: Optional[bytes] = None, claimed: bool = True,
@@ -270,7 +294,7 @@ def pack_cbor(raw_headers, *, slots_per_kes_period: int = 129600,
     import ctypes
 
     from . import _native
-    lib = _native.load()
+    lib = _pack_lib() or _native.load()
     if isinstance(raw_headers, tuple) and len(raw_headers) == 3:
         buf, off, ln = raw_headers
         buf = np.frombuffer(buf, np.uint8) if isinstance(buf, (bytes, bytearray)) else \

@@ -13,6 +13,8 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 ORACLE_SO = os.path.join(ROOT, "oracle", "build", "liboracle.so")
+# OURO_ORACLE_LIB: a build variant for the whole process (tests/test_sanitizers.py)
+ORACLE_ENV = os.environ.get("OURO_ORACLE_LIB")
 SODIUM_SO = "/opt/conda/lib/libsodium.so.23"
 
 _lib = None
@@ -27,7 +29,7 @@ def lib(path: str = None) -> ctypes.CDLL:
     if _lib is not None and path not in (None, _path):
         raise RuntimeError(f"oracle already loaded from {_path}")
     if _lib is None:
-        path = path or ORACLE_SO
+        path = path or ORACLE_ENV or ORACLE_SO
         if path == ORACLE_SO and not os.path.exists(ORACLE_SO):
             subprocess.run(["make", "-C", os.path.join(ROOT, "oracle")], check=True,
                            stdout=subprocess.DEVNULL)

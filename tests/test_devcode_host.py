@@ -17,7 +17,9 @@ import oracle_ffi as O
 from edge_cases import ed25519_edge_cases, vrf_edge_cases
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-SO = os.path.join(ROOT, "ouroboros-network_amd", "lib", "libouro_devhost_test.so")
+# OURO_DEVHOST_LIB: the ASan/UBSan build (tests/test_sanitizers.py)
+SO = os.environ.get("OURO_DEVHOST_LIB") or os.path.join(
+    ROOT, "ouroboros-network_amd", "lib", "libouro_devhost_test.so")
 P = 2**255 - 19
 L = 2**252 + 27742317777372353535851937790883648493
 
