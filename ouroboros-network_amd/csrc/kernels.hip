@@ -29,7 +29,14 @@ constexpr int kBlock = 256;
 #define OURO_WAVES 2
 #endif
 // throughput header kernel: scratch slot + the per-header result record
-constexpr int kHdrLaneWords = kLaneWords + kResWords;
+// rounded up to whole 128-B lines (OURO_SLOT_ALIGN): every table entry then
+// starts 32-B aligned and a gathered 160-B entry touches exactly two lines
+#ifndef OURO_SLOT_ALIGN
+#define OURO_SLOT_ALIGN 32
+#endif
+constexpr int round_slot(int w) { return (w + OURO_SLOT_ALIGN - 1) / OURO_SLOT_ALIGN * OURO_SLOT_ALIGN; }
+constexpr int kHdrLaneWords = round_slot(kLaneWords + kResWords);
+constexpr int kSlotWords = round_slot(kLaneWords);  // the other kernels' slots
 constexpr int kLatBlock = 64;  // default latency-mode workgroup (lat_block(); A/B: tools/ab_latency.py)
 
 __device__ __forceinline__ void load_words(uint32_t* w, const uint8_t* p, int nwords16) {
@@ -59,7 +66,7 @@ __global__ void __launch_bounds__(kBlock, OURO_WAVES) k_ed25519_verify(
     const int32_t* __restrict__ btab, uint32_t byron) {
   const size_t tid = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   const size_t nth = (size_t)gridDim.x * blockDim.x;
-  const Slot lane = slot_of(scratch, tid, kLaneWords);
+  const Slot lane = slot_of(scratch, tid, kSlotWords);
   for (size_t i = tid; i < n; i += nth) {
     uint32_t s[16], p[8];
     load_words(s, sig + 64 * i, 4);
@@ -77,7 +84,7 @@ __global__ void __launch_bounds__(kBlock, OURO_WAVES) k_vrf03_verify(
     uint8_t* __restrict__ verdict, int32_t* scratch, const int32_t* __restrict__ btab) {
   const size_t tid = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   const size_t nth = (size_t)gridDim.x * blockDim.x;
-  const Slot lane = slot_of(scratch, tid, kLaneWords);
+  const Slot lane = slot_of(scratch, tid, kSlotWords);
   for (size_t i = tid; i < n; i += nth) {
     uint32_t p[8], pi[20], b[16];
     load_words(p, pk + 32 * i, 2);
@@ -95,7 +102,7 @@ __global__ void __launch_bounds__(kBlock, OURO_WAVES) k_sum6kes_verify(
     uint8_t* __restrict__ verdict, int32_t* scratch, const int32_t* __restrict__ btab) {
   const size_t tid = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   const size_t nth = (size_t)gridDim.x * blockDim.x;
-  const Slot lane = slot_of(scratch, tid, kLaneWords);
+  const Slot lane = slot_of(scratch, tid, kSlotWords);
   for (size_t i = tid; i < n; i += nth) {
     uint32_t v[8];
     load_words(v, vk + 32 * i, 2);
@@ -172,7 +179,7 @@ __global__ void __launch_bounds__(kBlock, OURO_WAVES) k_tpraos_cores(ouro_tpraos
   const int sh = quad ? 2 : 0;
   const size_t tid = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) >> sh;
   const size_t nth = ((size_t)gridDim.x * blockDim.x) >> sh;
-  const Slot lane = slot_of(scratch, tid, kLaneWords);
+  const Slot lane = slot_of(scratch, tid, kSlotWords);
   for (size_t w = tid; w < (size_t)kLatCores * n; w += nth) {
     const int core = (int)(w / n);
     const size_t i = w - (size_t)core * n;
@@ -197,7 +204,7 @@ __global__ void __launch_bounds__(kBlock, OURO_WAVES) k_tpraos_finish(ouro_tprao
   const int sh = quad ? 2 : 0;
   const size_t tid = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) >> sh;
   const size_t nth = ((size_t)gridDim.x * blockDim.x) >> sh;
-  const Slot lane = slot_of(scratch, tid, kLaneWords);
+  const Slot lane = slot_of(scratch, tid, kSlotWords);
   const uint32_t q = threadIdx.x & 3u;
   for (size_t i = tid; i < n; i += nth) {
     const Slot res = slot_of(res_buf, i, kLatResWords);
@@ -406,7 +413,7 @@ int thread_stream(hipStream_t* s) {
 
 // grid for n items of kernel `id`; returns the scratch slot count
 int plan(DeviceState* ds, int id, size_t n, hipStream_t stream, int* grid, int32_t** scratch,
-         int lane_words = kLaneWords) {
+         int lane_words = kSlotWords) {
   size_t blocks = (n + kBlock - 1) / kBlock;
   blocks = std::max<size_t>(1, std::min<size_t>(blocks, (size_t)ds->max_blocks[id]));
   *grid = (int)blocks;
@@ -541,7 +548,7 @@ size_t lowlat_scratch_words(DeviceState* ds, size_t n_cap) {
   size_t b1 = std::min<size_t>(((size_t)kLatCores * n_cap + kBlock - 1) / kBlock,
                                (size_t)ds->max_blocks[kCores]);
   size_t b2 = std::min<size_t>((n_cap + kBlock - 1) / kBlock, (size_t)ds->max_blocks[kFinish]);
-  return std::max<size_t>(1, std::max(b1, b2)) * kBlock * kLaneWords;
+  return std::max<size_t>(1, std::max(b1, b2)) * kBlock * kSlotWords;
 }
 
 // ---- host-buffer staging ----
