@@ -16,46 +16,12 @@
 #include <vector>
 
 #include "../../include/ouro_verify.h"
+#include "launch.h"
 #include "leader.h"
 #include "tpraos.h"
 
 using namespace ouro;
 
-namespace {
-
-constexpr int kBlock = 256;
-// resident waves per SIMD the kernels are compiled for (VGPR budget 512 / W)
-#ifndef OURO_WAVES
-#define OURO_WAVES 2
-#endif
-// throughput header kernel: scratch slot + the per-header result record
-// rounded up to whole 128-B lines (OURO_SLOT_ALIGN): every table entry then
-// starts 32-B aligned and a gathered 160-B entry touches exactly two lines
-#ifndef OURO_SLOT_ALIGN
-#define OURO_SLOT_ALIGN 32
-#endif
-constexpr int round_slot(int w) { return (w + OURO_SLOT_ALIGN - 1) / OURO_SLOT_ALIGN * OURO_SLOT_ALIGN; }
-constexpr int kHdrLaneWords = round_slot(kLaneWords + kResWords);
-constexpr int kSlotWords = round_slot(kLaneWords);  // the other kernels' slots
-constexpr int kLatBlock = 64;  // default latency-mode workgroup (lat_block(); A/B: tools/ab_latency.py)
-
-__device__ __forceinline__ void load_words(uint32_t* w, const uint8_t* p, int nwords16) {
-#pragma unroll
-  for (int i = 0; i < nwords16; i++) {
-    const int4 v = ldg4(p + 16 * i);
-    w[4 * i] = v.x; w[4 * i + 1] = v.y; w[4 * i + 2] = v.z; w[4 * i + 3] = v.w;
-  }
-}
-__device__ __forceinline__ void store_words(uint8_t* p, const uint32_t* w, int nwords16) {
-#pragma unroll
-  for (int i = 0; i < nwords16; i++)
-    stg4(p + 16 * i, make_int4((int)w[4 * i], (int)w[4 * i + 1], (int)w[4 * i + 2], (int)w[4 * i + 3]));
-}
-
-__device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
-
-
-}  // namespace
 
 // ---------------------------------------------------------------- kernels ----
 
@@ -162,75 +128,17 @@ __global__ void __launch_bounds__(kBlock, OURO_WAVES) k_tpraos_verify(ouro_tprao
   }
 }
 
-// Latency mode, launch 1: eight cores per header (work item w = core * n + i,
-// so each wave runs one core type), results to a per-header record.
-// quad = 1: each work item runs on the four lanes of a DPP quad, which share
-// its scratch slot and split every group operation's products (ge25519.h);
-// quad = 0: one lane per item.  n (d_n[0]) and the batch's optional members
-// (d_n[1], tpraos.h kOpt*) are read from device memory so a captured graph
-// serves any batch of n <= capacity.
-__global__ void __launch_bounds__(kBlock, OURO_WAVES) k_tpraos_cores(ouro_tpraos_batch b,
-                                                            const uint32_t* __restrict__ d_n,
-                                                            int32_t* res_buf, int32_t* scratch,
-                                                            const int32_t* __restrict__ btab,
-                                                            int quad) {
-  const size_t n = d_n[0];
-  const uint32_t opts = d_n[1];
-  const int sh = quad ? 2 : 0;
-  const size_t tid = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) >> sh;
-  const size_t nth = ((size_t)gridDim.x * blockDim.x) >> sh;
-  const Slot lane = slot_of(scratch, tid, kSlotWords);
-  for (size_t w = tid; w < (size_t)kLatCores * n; w += nth) {
-    const int core = (int)(w / n);
-    const size_t i = w - (size_t)core * n;
-    hdr_core(b, i, opts, core, lane, slot_of(res_buf, i, kLatResWords), btab, /*share_key=*/false,
-             /*split=*/true, quad != 0);
-  }
-}
-
-// Latency mode, launch 2: the finish.  quad = 1: a lane quad per header, its
-// lane pairs finishing one VRF each (vrf_finish_split: one inversion of four
-// Z per VRF), quad position 0 assembling the verdict; quad = 0: one lane per
-// header with one inversion of all eight Z.
-__global__ void __launch_bounds__(kBlock, OURO_WAVES) k_tpraos_finish(ouro_tpraos_batch b,
-                                                             const uint32_t* __restrict__ d_n,
-                                                             int32_t* res_buf,
-                                                             uint8_t* __restrict__ verdict,
-                                                             uint8_t* __restrict__ beta_eta,
-                                                             uint8_t* __restrict__ beta_leader,
-                                                             int32_t* scratch, int quad) {
-  const size_t n = d_n[0];
-  const uint32_t opts = d_n[1];
-  const int sh = quad ? 2 : 0;
-  const size_t tid = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) >> sh;
-  const size_t nth = ((size_t)gridDim.x * blockDim.x) >> sh;
-  const Slot lane = slot_of(scratch, tid, kSlotWords);
-  const uint32_t q = threadIdx.x & 3u;
-  for (size_t i = tid; i < n; i += nth) {
-    const Slot res = slot_of(res_buf, i, kLatResWords);
-    if (!quad) {
-      hdr_combine_split(res);
-      hdr_finish_item(b, i, opts, res, lane, verdict, beta_eta, beta_leader);
-      continue;
-    }
-    const int which = (int)(q >> 1);
-    uint32_t pi[20], beta[16];
-    load_words(pi, (which ? b.leader_proof : b.eta_proof) + 80 * i, 5);
-    uint32_t bit = vrf_finish_split(res, which, pi, beta);
-    bit |= hdr_claim_bit(b, i, opts, which, bit != 0, beta);
-    if (q == 0) hdr_eta_nonce(b, i, opts, beta);
-    // quad position 0 takes position 2's (the leader VRF's) bits
-    const uint32_t other = (uint32_t)__builtin_amdgcn_mov_dpp((int)bit, 0x0a, 0xf, 0xf, true);
-    uint8_t* dst = which ? beta_leader : beta_eta;
-    if ((q & 1u) == 0 && dst) store_words(dst + 64 * i, beta, 4);
-    if (q == 0) {
-      uint32_t v = bit | other;
-      if (ldg1(res.word(kResFlags + kCoreOcert)) & kFlagOk) v |= 0x01u;
-      if (ldg1(res.word(kResFlags + kCoreKes)) & kFlagOk) v |= 0x02u;
-      verdict[i] = (uint8_t)v;
-    }
-  }
-}
+// Latency mode (k_tpraos_cores, k_tpraos_finish): kernels_lat.hip, its own
+// translation unit built with the row-order field products (lane quads issue
+// one product per lane, whose dependent column-scan chains would stall: A/B
+// p50 0.5875 -> 0.5712 ms, profiles/r02d/ablat_rows_scan.json).
+__global__ void k_tpraos_cores(ouro_tpraos_batch b, const uint32_t* __restrict__ d_n,
+                               int32_t* res_buf, int32_t* scratch,
+                               const int32_t* __restrict__ btab, int quad);
+__global__ void k_tpraos_finish(ouro_tpraos_batch b, const uint32_t* __restrict__ d_n,
+                                int32_t* res_buf, uint8_t* __restrict__ verdict,
+                                uint8_t* __restrict__ beta_eta, uint8_t* __restrict__ beta_leader,
+                                int32_t* scratch, int quad);
 
 // leader threshold (leader.h), one item per lane; verdict 1 / 0 / 0xff
 __global__ void __launch_bounds__(kBlock) k_leader_check(size_t n, const uint8_t* __restrict__ beta,

@@ -26,6 +26,8 @@ def main():
     ap.add_argument("--batch", type=int, default=64)
     ap.add_argument("--var", default="OURO_LAT_BLOCK")
     ap.add_argument("--values", default="256,128,64")
+    ap.add_argument("--libs", nargs="*", default=None,
+                    help="A/B build variants of libouro_verify.so instead of an env variable")
     args = ap.parse_args()
     import torch
 
@@ -39,6 +41,8 @@ def main():
     hb = hdr.host_sample(args.batch)
     body = int(hb.body_len.astype(np.int64).sum())
     plans, ref = {}, None
+    if args.libs:
+        return lib_variants(args, hb, body)
     values = args.values.split(",")
     for v in values:
         os.environ[args.var] = v
@@ -64,6 +68,49 @@ def main():
                             "all_valid": bool((outs[k][0] == 15).all()), "same_as_first": same}
     for p in plans.values():
         p.close()
+    print(json.dumps(res, indent=1))
+
+
+def lib_variants(args, hb, body):
+    """One 64-header plan per library build (same batch), interleaved rounds."""
+    import ctypes
+
+    from ouroboros_network_amd import _native
+
+    P = ctypes.c_void_p
+    plans = {}
+    for path in args.libs:
+        lib = ctypes.CDLL(os.path.abspath(path))
+        lib.ouro_tpraos_plan_create.restype = P
+        lib.ouro_tpraos_plan_create.argtypes = [ctypes.c_size_t, ctypes.c_size_t]
+        lib.ouro_tpraos_plan_run.restype = ctypes.c_int
+        lib.ouro_tpraos_plan_run.argtypes = [P, ctypes.POINTER(_native.TPraosBatch), P, P, P]
+        plan = lib.ouro_tpraos_plan_create(args.batch, body)
+        assert plan, path
+        plans[os.path.basename(path)] = (lib, plan)
+    n = len(hb)
+    s = hb.c_struct()
+    outs = {k: (np.zeros(n, np.uint8), np.zeros((n, 64), np.uint8), np.zeros((n, 64), np.uint8))
+            for k in plans}
+    ptr = lambda a: a.ctypes.data_as(P)  # noqa: E731
+    lat = {k: [] for k in plans}
+    for r in range(args.rounds + 1):
+        for k, (lib, plan) in plans.items():
+            o = outs[k]
+            for _ in range(args.iters):
+                t0 = time.perf_counter()
+                rc = lib.ouro_tpraos_plan_run(plan, ctypes.byref(s), ptr(o[0]), ptr(o[1]), ptr(o[2]))
+                if r:
+                    lat[k].append(time.perf_counter() - t0)
+                assert rc == 0, (k, rc)
+    first = outs[next(iter(plans))]
+    res = {}
+    for k, v in lat.items():
+        a = np.array(v) * 1e3
+        same = all((outs[k][i] == first[i]).all() for i in range(3))
+        res[k] = {"p50_ms": round(float(np.percentile(a, 50)), 4),
+                  "p99_ms": round(float(np.percentile(a, 99)), 4),
+                  "all_valid": bool((outs[k][0] == 15).all()), "same_as_first": same}
     print(json.dumps(res, indent=1))
 
 
