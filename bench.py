@@ -579,30 +579,124 @@ def e2e_leg(hdr, n: int, reps: int = 3):
 def raw_leg(n: int, npools: int, device, threads: int, chunk: int = 0, reps: int = 3):
     """Raw wire CBOR -> verdicts: n synthetic headers as
     the bytes ChainSync hands over (#6.24-wrapped [header_body, kes_sig],
-    bench.raw_template), in pageable host memory.  Per chunk the C slicer
-    (ouro_tpraos_pack_cbor, `threads` host threads) builds the SoA, then
-    ouro_tpraos_verify_batch runs H2D + header kernel + D2H; the slicing of
-    chunk k+1 overlaps the verification of chunk k.  The slicer alone is timed
-    too.  Never `value` (host buffers, PCIe-inclusive)."""
+    bench.raw_template).  Three forms, never `value`:
+      device    raw headers resident in HBM -> the device slicer
+                (ouro_tpraos_pack_cbor_device) -> the header kernel, one stream;
+      pcie      raw headers in pinned host memory, uploaded in chunks on a
+                copy stream overlapping the slicer + kernel of the previous
+                chunk, results copied back;
+      host      pageable host memory -> the C slicer on `threads` host threads
+                -> ouro_tpraos_verify_batch (H2D + kernel + D2H), slicing chunk
+                k+1 behind the verification of chunk k."""
     import threading
+
+    import torch
 
     from ouroboros_network_amd import _native
 
-    # two chunks: each verify call pipelines its own H2D / kernel / D2H
-    # sub-chunks, and slicing chunk 1 overlaps verifying chunk 0
-    chunk = chunk or max(1, (n + 1) // 2)
     t, raw, rl = synth_raw_headers(n, npools, device)
+    lib = _native.load()
+    P = lambda a: a.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
+    V = ctypes.c_void_p
+    res = {"raw_bytes_per_header": rl}
+
+    # ---- device: raw in HBM -> device slicer -> kernel ---------------------
+    doff = torch.arange(n, dtype=torch.int64, device=device) * rl
+    dlen = torch.full((n,), rl, dtype=torch.int32, device=device)
+    nbd = int(lib.ouro_tpraos_pack_bytes(n))
+    darena = torch.empty(nbd, dtype=torch.uint8, device=device)
+    dstatus = torch.empty(n, dtype=torch.uint8, device=device)
+    dv = torch.empty(n, dtype=torch.uint8, device=device)
+    dbe = torch.empty(n * 64, dtype=torch.uint8, device=device)
+    dbl = torch.empty(n * 64, dtype=torch.uint8, device=device)
+    st = torch.cuda.current_stream()
+    S = V(st.cuda_stream)
+
+    def dev_batch(lo, m, arena_t, out):
+        rc = lib.ouro_tpraos_pack_cbor_device(
+            S, V(raw.data_ptr()), raw.numel(), V(doff.data_ptr() + 8 * lo), V(dlen.data_ptr() + 4 * lo),
+            m, 129600, V(arena_t.data_ptr()), arena_t.numel(), ctypes.byref(out), None, None,
+            V(dstatus.data_ptr() + lo))
+        _native.check(rc, "ouro_tpraos_pack_cbor_device")
+        out.eta_alpha = t["eta_alpha"].data_ptr() + 32 * lo
+        out.leader_alpha = t["leader_alpha"].data_ptr() + 32 * lo
+        rc = lib.ouro_tpraos_verify_batch_device(S, ctypes.byref(out), V(dv.data_ptr() + lo),
+                                                 V(dbe.data_ptr() + 64 * lo),
+                                                 V(dbl.data_ptr() + 64 * lo))
+        _native.check(rc, "ouro_tpraos_verify_batch_device")
+
+    out = _native.TPraosBatch()
+    dev_batch(0, n, darena, out)  # warm
+    ts = []
+    for _ in range(reps):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(st)
+        dev_batch(0, n, darena, out)
+        e1.record(st)
+        torch.cuda.synchronize()
+        ts.append(e0.elapsed_time(e1))
+    pk = []
+    for _ in range(reps):  # the device slicer alone
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(st)
+        _native.check(lib.ouro_tpraos_pack_cbor_device(
+            S, V(raw.data_ptr()), raw.numel(), V(doff.data_ptr()), V(dlen.data_ptr()), n, 129600,
+            V(darena.data_ptr()), nbd, ctypes.byref(_native.TPraosBatch()), None, None,
+            V(dstatus.data_ptr())), "pack")
+        e1.record(st)
+        torch.cuda.synchronize()
+        pk.append(e0.elapsed_time(e1))
+    dev_ok = bool((dstatus == 0).all().item() and (dv == 0x3F).all().item())
+    res["device"] = {"headers_per_s": round(n / (min(ts) * 1e-3), 1), "ms": round(min(ts), 3),
+                     "slicer_ms": round(min(pk), 3), "all_valid": dev_ok}
+
+    # ---- pcie: pinned host raw, chunked upload overlapping slice + kernel ---
+    rawh = raw.cpu().pin_memory()
+    pch = 1 << 17
+    nchp = (n + pch - 1) // pch
+    arenas = [torch.empty(int(lib.ouro_tpraos_pack_bytes(pch)), dtype=torch.uint8, device=device)
+              for _ in range(2)]
+    copy_st = torch.cuda.Stream()
+    vh = torch.empty(n, dtype=torch.uint8).pin_memory()
+    beh = torch.empty(n * 64, dtype=torch.uint8).pin_memory()
+    blh = torch.empty(n * 64, dtype=torch.uint8).pin_memory()
+
+    def run_pcie():
+        evs = []
+        for k in range(nchp):
+            lo, m = k * pch, min(pch, n - k * pch)
+            with torch.cuda.stream(copy_st):
+                raw[lo * rl:(lo + m) * rl].copy_(rawh[lo * rl:(lo + m) * rl], non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record(copy_st)
+            evs.append(ev)
+        for k in range(nchp):
+            lo, m = k * pch, min(pch, n - k * pch)
+            st.wait_event(evs[k])
+            dev_batch(lo, m, arenas[k % 2], _native.TPraosBatch())
+        vh.copy_(dv, non_blocking=True)
+        beh.copy_(dbe, non_blocking=True)
+        blh.copy_(dbl, non_blocking=True)
+        torch.cuda.synchronize()
+
+    run_pcie()
+    best = min(_timed(run_pcie) for _ in range(reps))
+    res["pcie"] = {"headers_per_s": round(n / best, 1), "ms": round(best * 1e3, 2),
+                   "h2d_bytes": int(n * rl), "chunk": pch,
+                   "all_valid": bool((vh == 0x3F).all().item())}
+    del rawh, arenas, darena
+
+    # ---- host: pageable raw -> C slicer -> host-buffer verify ---------------
     rawh = raw.cpu().numpy()
     del raw
     ea = t["eta_alpha"].cpu().numpy()
     la = t["leader_alpha"].cpu().numpy()
     del t
-    lib = _native.load()
-    P = lambda a: a.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
+    chunk = chunk or max(1, (n + 1) // 2)
     off = np.arange(n, dtype=np.uint64) * rl
     ln = np.full(n, rl, np.uint32)
     nch = (n + chunk - 1) // chunk
-    arenas = [np.zeros(lib.ouro_tpraos_pack_bytes(chunk), np.uint8) for _ in range(2)]
+    harenas = [np.zeros(lib.ouro_tpraos_pack_bytes(chunk), np.uint8) for _ in range(2)]
     status = np.zeros(n, np.uint8)
     verdict = np.zeros(n, np.uint8)
     be = np.zeros((n, 64), np.uint8)
@@ -612,7 +706,7 @@ def raw_leg(n: int, npools: int, device, threads: int, chunk: int = 0, reps: int
     def pack(k):
         lo = k * chunk
         m = min(chunk, n - lo)
-        a = arenas[k % 2]
+        a = harenas[k % 2]
         rc = lib.ouro_tpraos_pack_cbor(P(rawh), rawh.size, P(off[lo:]), P(ln[lo:]), m, 129600,
                                        P(a), a.size, ctypes.byref(structs[k]), None, None,
                                        P(status[lo:]), threads)
@@ -626,7 +720,7 @@ def raw_leg(n: int, npools: int, device, threads: int, chunk: int = 0, reps: int
                                           P(bl[lo:]))
         _native.check(rc, "ouro_tpraos_verify_batch")
 
-    def run_pipelined():
+    def run_host():
         pack(0)
         for k in range(nch):
             th = None
@@ -638,8 +732,8 @@ def raw_leg(n: int, npools: int, device, threads: int, chunk: int = 0, reps: int
             if th:
                 th.join()
 
-    run_pipelined()  # warm: device buffers, pinned staging, arena pages
-    best = min(_timed(run_pipelined) for _ in range(reps))
+    run_host()  # warm: device buffers, pinned staging, arena pages
+    best = min(_timed(run_host) for _ in range(reps))
     ok = bool((status == 0).all() and (verdict == 0x3F).all())
     pk_t = []
     for _ in range(reps):
@@ -647,11 +741,14 @@ def raw_leg(n: int, npools: int, device, threads: int, chunk: int = 0, reps: int
         for k in range(nch):
             pack(k)
         pk_t.append(time.perf_counter() - t0)
-    return {"workload": f"{n} raw wire headers ({rl} B each, pageable host memory) -> C slicer "
-                        f"({threads} threads, chunks of {chunk}) -> ouro_tpraos_verify_batch",
-            "headers_per_s": round(n / best, 1), "ms": round(best * 1e3, 2),
-            "slicer_headers_per_s": round(n / min(pk_t), 1), "slicer_threads": threads,
-            "all_valid": ok}
+    res["host"] = {"headers_per_s": round(n / best, 1), "ms": round(best * 1e3, 2),
+                   "slicer_headers_per_s": round(n / min(pk_t), 1), "slicer_threads": threads,
+                   "chunk": chunk, "all_valid": ok}
+    res["workload"] = (f"{n} raw wire headers ({rl} B each): device = HBM-resident raw -> device "
+                       "slicer -> header kernel; pcie = pinned host raw uploaded in 128K-header "
+                       "chunks overlapping slice + kernel, results back; host = pageable raw -> "
+                       "C slicer -> ouro_tpraos_verify_batch")
+    return res
 
 
 def _timed(fn) -> float:

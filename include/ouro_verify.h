@@ -230,11 +230,24 @@ int ouro_tpraos_verify_batch(const ouro_tpraos_batch *b, uint8_t *verdict,
                                fields, [output, proof] certs, uint/bytes types) */
 #define OURO_PACK_ESIZE 3u  /* a fixed-size crypto field has the wrong length  */
 #define OURO_PACK_EBYRON 4u /* HFC era 0: a Byron header, not TPraos          */
+#define OURO_PACK_ESPAN 5u  /* (device slicer) span outside raw_bytes          */
 size_t ouro_tpraos_pack_bytes(size_t n);
 int ouro_tpraos_pack_cbor(const uint8_t *raw, size_t raw_bytes, const uint64_t *off,
                           const uint32_t *len, size_t n, uint64_t slots_per_kes_period,
                           void *arena, size_t arena_bytes, ouro_tpraos_batch *out,
                           uint64_t *slot, uint8_t *era, uint8_t *status, int nthreads);
+/* The same slicer on the GPU, one lane per header, for raw headers already in
+ * device memory (raw, off, len, arena, slot, era, status: device pointers;
+ * slot / era may be NULL): enqueued on `stream` and returns at once; *out
+ * receives device pointers into the arena, ready for
+ * ouro_tpraos_verify_batch_device on the same stream.  A span outside
+ * raw_bytes is per-header status OURO_PACK_ESPAN.  Same parse code as the
+ * host slicer (csrc/cbor.h); tests/test_gpu_pack.py checks the two agree. */
+int ouro_tpraos_pack_cbor_device(void *stream, const uint8_t *raw, size_t raw_bytes,
+                                 const uint64_t *off, const uint32_t *len, size_t n,
+                                 uint64_t slots_per_kes_period, void *arena, size_t arena_bytes,
+                                 ouro_tpraos_batch *out, uint64_t *slot, uint8_t *era,
+                                 uint8_t *status);
 
 /* The host-side UPDN fold (ledger-specs; the per-header step of
  * SL.updateChainDepState after the crypto): for i = 0..n-1

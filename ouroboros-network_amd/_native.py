@@ -109,6 +109,8 @@ SIGNATURES = {
     "ouro_tpraos_pack_bytes": (_SZ, [_SZ]),
     "ouro_tpraos_pack_cbor": (_I, [_P, _SZ, _P, _P, _SZ, ctypes.c_uint64, _P, _SZ,
                                    ctypes.POINTER(TPraosBatch), _P, _P, _P, _I]),
+    "ouro_tpraos_pack_cbor_device": (_I, [_P, _P, _SZ, _P, _P, _SZ, ctypes.c_uint64, _P, _SZ,
+                                          ctypes.POINTER(TPraosBatch), _P, _P, _P]),
 }
 
 # the cardano-crypto-praos names the library also exports (include/ouro_verify.h)

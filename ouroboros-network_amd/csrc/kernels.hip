@@ -16,6 +16,7 @@
 #include <vector>
 
 #include "../../include/ouro_verify.h"
+#include "cbor.h"
 #include "launch.h"
 #include "leader.h"
 #include "tpraos.h"
@@ -139,6 +140,29 @@ __global__ void k_tpraos_finish(ouro_tpraos_batch b, const uint32_t* __restrict_
                                 int32_t* res_buf, uint8_t* __restrict__ verdict,
                                 uint8_t* __restrict__ beta_eta, uint8_t* __restrict__ beta_leader,
                                 int32_t* scratch, int quad);
+
+// Raw wire headers -> the SoA on the device, one lane
+// per header: the host slicer's parse (cbor.h, pinned to header.py by
+// tests/test_pack.py), spans checked against raw_bytes here (status
+// OURO_PACK_ESPAN) since a device call cannot return OURO_EINVAL per header.
+__global__ void __launch_bounds__(kBlock) k_tpraos_pack(const uint8_t* __restrict__ raw,
+                                                        size_t raw_bytes,
+                                                        const uint64_t* __restrict__ off,
+                                                        const uint32_t* __restrict__ len, size_t n,
+                                                        uint64_t spkp, cbor::Out o,
+                                                        uint8_t* __restrict__ status) {
+  const size_t tid = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const size_t nth = (size_t)gridDim.x * blockDim.x;
+  for (size_t i = tid; i < n; i += nth) {
+    const uint64_t o0 = off[i];
+    const uint32_t l0 = len[i];
+    uint8_t st = (o0 > raw_bytes || raw_bytes - o0 < l0)
+                     ? (uint8_t)OURO_PACK_ESPAN
+                     : cbor::pack_one(raw, o0, l0, spkp, o, i);
+    if (st != OURO_PACK_OK) cbor::zero_row(o, i);
+    status[i] = st;
+  }
+}
 
 // leader threshold (leader.h), one item per lane; verdict 1 / 0 / 0xff
 __global__ void __launch_bounds__(kBlock) k_leader_check(size_t n, const uint8_t* __restrict__ beta,
@@ -1089,6 +1113,27 @@ int ouro_tpraos_verify_batch_device(void* stream, const ouro_tpraos_batch* b, ui
   if (rc) return rc;
   hipStream_t st = static_cast<hipStream_t>(stream);  // NULL = HIP's default stream
   return launch_hdr(st, *b, verdict, beta_eta, beta_leader);
+}
+
+int ouro_tpraos_pack_cbor_device(void* stream, const uint8_t* raw, size_t raw_bytes,
+                                 const uint64_t* off, const uint32_t* len, size_t n,
+                                 uint64_t slots_per_kes_period, void* arena, size_t arena_bytes,
+                                 ouro_tpraos_batch* out, uint64_t* slot, uint8_t* era,
+                                 uint8_t* status) {
+  if (!out || slots_per_kes_period == 0) return fail(OURO_EINVAL, "null batch / zero period");
+  if (n > 0 && (!raw || !off || !len || !arena || !status)) return fail(OURO_EINVAL, "null buffer");
+  if (arena_bytes < ouro_tpraos_pack_bytes(n)) return fail(OURO_EINVAL, "arena too small");
+  const cbor::Out o = cbor::arena_out(cbor::arena_base(arena), n, slot, era);
+  cbor::batch_from(out, o, raw, n);
+  if (n == 0) return OURO_OK;
+  DeviceState* ds;
+  int rc = device_state(&ds);
+  if (rc) return rc;
+  hipStream_t st = static_cast<hipStream_t>(stream);  // NULL = HIP's default stream
+  const size_t blocks = std::min<size_t>((n + kBlock - 1) / kBlock, 4096);
+  hipLaunchKernelGGL(k_tpraos_pack, dim3((unsigned)blocks), dim3(kBlock), 0, st, raw, raw_bytes,
+                     off, len, n, slots_per_kes_period, o, status);
+  return launch_check();
 }
 
 int ouro_leader_check_batch_device(void* stream, size_t n, const uint8_t* beta,

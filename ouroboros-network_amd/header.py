@@ -241,7 +241,7 @@ def pack(headers: Sequence[ShelleyHeader], eta_alpha: Optional[Sequence[bytes]] 
     )
 
 
-PACK_OK, PACK_ECBOR, PACK_ESHAPE, PACK_ESIZE, PACK_EBYRON = 0, 1, 2, 3, 4
+PACK_OK, PACK_ECBOR, PACK_ESHAPE, PACK_ESIZE, PACK_EBYRON, PACK_ESPAN = 0, 1, 2, 3, 4, 5
 
 
 @dataclass

@@ -25,7 +25,13 @@ def kats():
 @pytest.fixture(scope="session")
 def gpu_lib():
     """The product library on a real device; fails loudly (no skip) when the
-    HIP library is missing on a GPU run."""
+    HIP library is missing on a GPU run.  torch is initialised first: its
+    wheel bundles its own libamdhip64, and whichever HIP runtime a process
+    loads first is the one both then share (same soname) -- torch's must win
+    for torch.cuda to see the GPU."""
+    import torch
+
+    torch.cuda.init()
     import ouroboros_network_amd as ona
 
     lib = ona._native.load()

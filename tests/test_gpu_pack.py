@@ -110,3 +110,127 @@ def _rows(batch, sel):
         ocert_sigma=pick(batch.ocert_sigma), kes_t=pick(batch.kes_t), kes_sig=pick(batch.kes_sig),
         body=np.frombuffer(b"".join(bodies), np.uint8), body_off=offs, body_len=lens,
         eta_output=pick(batch.eta_output), leader_output=pick(batch.leader_output))
+
+
+def _device_pack(raw_bytes: bytes, off, ln, spkp=129600):
+    """ouro_tpraos_pack_cbor_device on a device copy of the buffers; returns
+    (host views of the arena arrays as a dict, status, slot, era)."""
+    import ctypes
+
+    import torch
+
+    from ouroboros_network_amd import _native
+
+    lib = _native.load()
+    dev = torch.device("cuda", 0)
+    n = len(off)
+    raw = torch.frombuffer(bytearray(raw_bytes), dtype=torch.uint8).to(dev)
+    doff = torch.tensor(np.asarray(off, np.int64), device=dev)
+    dlen = torch.tensor(np.asarray(ln, np.int32), device=dev)
+    nb = int(lib.ouro_tpraos_pack_bytes(n))
+    arena = torch.zeros(nb, dtype=torch.uint8, device=dev)
+    status = torch.full((n,), 0xEE, dtype=torch.uint8, device=dev)
+    slot = torch.zeros(n, dtype=torch.int64, device=dev)
+    era = torch.zeros(n, dtype=torch.uint8, device=dev)
+    out = _native.TPraosBatch()
+    st = torch.cuda.current_stream()
+    rc = lib.ouro_tpraos_pack_cbor_device(ctypes.c_void_p(st.cuda_stream), raw.data_ptr(), raw.numel(),
+                                          doff.data_ptr(), dlen.data_ptr(), n, spkp, arena.data_ptr(),
+                                          nb, ctypes.byref(out), slot.data_ptr(), era.data_ptr(),
+                                          status.data_ptr())
+    assert rc == 0, rc
+    torch.cuda.synchronize()
+    host = arena.cpu().numpy()
+    base = arena.data_ptr()
+
+    def view(addr, dt, w):
+        cnt = n * (w or 1) * np.dtype(dt).itemsize
+        a = host[addr - base: addr - base + cnt].view(dt)
+        return a.reshape(n, w) if w else a
+
+    f = {"issuer_vk": view(out.issuer_vk, np.uint8, 32), "vrf_vk": view(out.vrf_vk, np.uint8, 32),
+         "eta_proof": view(out.eta_proof, np.uint8, 80),
+         "leader_proof": view(out.leader_proof, np.uint8, 80),
+         "hot_vk": view(out.hot_vk, np.uint8, 32),
+         "ocert_counter": view(out.ocert_counter, np.uint64, None),
+         "ocert_kes_period": view(out.ocert_kes_period, np.uint64, None),
+         "ocert_sigma": view(out.ocert_sigma, np.uint8, 64), "kes_t": view(out.kes_t, np.uint32, None),
+         "kes_sig": view(out.kes_sig, np.uint8, 448), "body_off": view(out.body_off, np.uint64, None),
+         "body_len": view(out.body_len, np.uint32, None),
+         "eta_output": view(out.eta_output, np.uint8, 64),
+         "leader_output": view(out.leader_output, np.uint8, 64)}
+    assert out.body == raw.data_ptr()
+    return f, status.cpu().numpy(), slot.cpu().numpy().view(np.uint64), era.cpu().numpy()
+
+
+def test_device_slicer_matches_host_slicer(gpu_lib, kats):
+    """The device slicer (same cbor.h code) against the host one on the golden
+    headers, every single-byte corruption of two of them, truncations, and
+    spans outside the buffer (device status OURO_PACK_ESPAN)."""
+    from ouroboros_network_amd import header as H
+
+    golden = [bytes.fromhex(h["raw"]) for h in kats["headers"]]
+    raws = list(golden)
+    for g in golden[:2]:
+        for pos in range(len(g)):
+            for x in (0x01, 0x80, 0xFF):
+                m = bytearray(g)
+                m[pos] ^= x
+                raws.append(bytes(m))
+        raws += [g[:k] for k in range(0, len(g), 7)]
+    ln = np.array([len(r) for r in raws], np.uint32)
+    off = np.zeros(len(raws), np.uint64)
+    off[1:] = np.cumsum(ln[:-1], dtype=np.uint64)
+    buf = b"".join(raws)
+    z = np.zeros((len(raws), 32), np.uint8)
+    hp = H.pack_cbor((buf, off, ln), eta_alpha=z, leader_alpha=z)
+    dev, status, slot, era = _device_pack(buf, off, ln)
+    np.testing.assert_array_equal(status, hp.status)
+    assert 0 < int((status == 0).sum()) < len(raws)
+    for k, v in dev.items():
+        np.testing.assert_array_equal(v, getattr(hp.batch, k), k)
+    np.testing.assert_array_equal(slot, hp.slot)
+    np.testing.assert_array_equal(era, hp.era)
+    # spans outside the buffer: rejected per header, neighbours unaffected
+    off2, ln2 = off[:3].copy(), ln[:3].copy()
+    off2[1] = len(buf) - 10
+    ln2[2] = len(buf) + 1
+    _, st2, _, _ = _device_pack(buf, off2, ln2)
+    assert st2.tolist() == [H.PACK_OK, H.PACK_ESPAN, H.PACK_ESPAN]
+
+
+def test_raw_headers_sliced_and_verified_on_device(gpu_lib):
+    """Synthetic raw headers in HBM -> device slicer -> header kernel, all on
+    one stream: every header valid, results equal to the host-sliced path."""
+    import ctypes
+
+    import torch
+
+    import bench
+    from ouroboros_network_amd import _native
+
+    lib = _native.load()
+    n = 4096
+    dev = torch.device("cuda", 0)
+    t, raw, rl = bench.synth_raw_headers(n, 64, dev)
+    off = torch.arange(n, dtype=torch.int64, device=dev) * rl
+    ln = torch.full((n,), rl, dtype=torch.int32, device=dev)
+    nb = int(lib.ouro_tpraos_pack_bytes(n))
+    arena = torch.zeros(nb, dtype=torch.uint8, device=dev)
+    status = torch.zeros(n, dtype=torch.uint8, device=dev)
+    out = _native.TPraosBatch()
+    st = torch.cuda.current_stream()
+    S = ctypes.c_void_p(st.cuda_stream)
+    assert lib.ouro_tpraos_pack_cbor_device(S, raw.data_ptr(), raw.numel(), off.data_ptr(),
+                                            ln.data_ptr(), n, 129600, arena.data_ptr(), nb,
+                                            ctypes.byref(out), None, None, status.data_ptr()) == 0
+    out.eta_alpha = t["eta_alpha"].data_ptr()
+    out.leader_alpha = t["leader_alpha"].data_ptr()
+    v = torch.zeros(n, dtype=torch.uint8, device=dev)
+    be = torch.zeros(n * 64, dtype=torch.uint8, device=dev)
+    bl = torch.zeros(n * 64, dtype=torch.uint8, device=dev)
+    assert lib.ouro_tpraos_verify_batch_device(S, ctypes.byref(out), v.data_ptr(), be.data_ptr(),
+                                               bl.data_ptr()) == 0
+    torch.cuda.synchronize()
+    assert (status.cpu() == 0).all()
+    assert (v.cpu() == 0x3F).all()
