@@ -8,6 +8,7 @@ from __future__ import annotations
 
 import ctypes
 import os
+import sys
 import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -135,6 +136,15 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
             raise NativeUnavailable(
                 f"{path} is not built; run `make -C ouroboros-network_amd` "
                 "(or __graft_entry__.build())")
+        # PyTorch wheels bundle their own libamdhip64 under the same soname as
+        # ROCm's: whichever a process loads first is the one both use, and
+        # torch.cuda only finds the GPU with its own.  So when torch is
+        # installed, load it before this library (a no-op if already loaded).
+        if "torch" not in sys.modules:
+            try:
+                import torch  # noqa: F401
+            except ImportError:
+                pass
         try:
             lib = ctypes.CDLL(path)
         except OSError as e:  # pragma: no cover - depends on the image
