@@ -48,6 +48,7 @@ OURO_FI int2 ldg2(const void* p) {
 OURO_FI int32_t ldg1(const void* p) { return *(const OURO_AS1 int32_t*)p; }
 OURO_FI uint64_t ldg8(const void* p) { return *(const OURO_AS1 uint64_t*)p; }
 OURO_FI uint32_t ldg_u8(const void* p) { return *(const OURO_AS1 uint8_t*)p; }
+OURO_FI uint32_t ldg_u16(const void* p) { return *(const OURO_AS1 uint16_t*)p; }
 OURO_FI void stg4(void* p, int4 v) {
   *(OURO_AS1 ouro_v4i*)p = ouro_v4i{v.x, v.y, v.z, v.w};
 }
@@ -60,6 +61,7 @@ OURO_FI int2 ldg2(const void* p) { return *static_cast<const int2*>(p); }
 OURO_FI int32_t ldg1(const void* p) { return *static_cast<const int32_t*>(p); }
 OURO_FI uint64_t ldg8(const void* p) { return *static_cast<const uint64_t*>(p); }
 OURO_FI uint32_t ldg_u8(const void* p) { return *static_cast<const uint8_t*>(p); }
+OURO_FI uint32_t ldg_u16(const void* p) { return *static_cast<const uint16_t*>(p); }
 OURO_FI void stg4(void* p, int4 v) { *static_cast<int4*>(p) = v; }
 OURO_FI void stg2(void* p, int2 v) { *static_cast<int2*>(p) = v; }
 OURO_FI void stg1(void* p, int32_t v) { *static_cast<int32_t*>(p) = v; }

@@ -332,6 +332,39 @@ OURO_FI void ge_p2_encode(uint32_t out[8], const ge_p2& p) {
 // ge25519_frombytes (negate = false) / ge25519_frombytes_negate_vartime
 // (negate = true).  y is read mod 2^255; x = 0 with the sign bit set is
 // accepted.  Returns false when (y^2 - 1)/(d y^2 + 1) is not a square.
+// Split around its exponentiation (the latency mode's wave-wide cores run
+// that on the wave, wide_cores.h): ge_decode_pre returns u v^7, ge_decode_post
+// takes (u v^7)^((p-5)/8).
+struct DecodePre { fe y, u, v, v3; };
+OURO_FI fe ge_decode_pre(DecodePre& d, const uint32_t s[8]) {
+  const fe one = fe_one();
+  d.y = fe_from_words(s);
+  fe u = fe_sq(d.y);
+  fe v = fe_mul(u, fe_d());
+  d.u = fe_sub(u, one);  // y^2 - 1
+  d.v = fe_add(v, one);  // d y^2 + 1
+  d.v3 = fe_mul(fe_sq(d.v), d.v);
+  return fe_mul(fe_mul(fe_sq(d.v3), d.v), d.u);  // u v^7
+}
+OURO_FI bool ge_decode_post(ge_p3* h, const DecodePre& d, const fe& pw, const uint32_t s[8],
+                            bool negate) {
+  const fe one = fe_one();
+  const fe y = d.y, u = d.u, v = d.v;
+  fe x = fe_mul(fe_mul(pw, d.v3), u);  // u v^3 (u v^7)^((p-5)/8)
+  fe vxx = fe_mul(fe_sq(x), v);
+  bool m_root = fe_iszero(fe_sub4(vxx, u));
+  bool p_root = fe_iszero(fe_add(vxx, u));
+  x = fe_select(x, fe_mul(x, fe_sqrtm1()), m_root);
+  const bool sign = (s[7] >> 31) != 0;
+  const bool flip = negate ? (fe_isnegative(x) == sign) : (fe_isnegative(x) != sign);
+  x = fe_select(fe_neg(x), x, flip);
+  h->X = x;
+  h->Y = y;
+  h->Z = one;
+  h->T = fe_mul(x, y);
+  return m_root || p_root;
+}
+
 OURO_FI bool ge_decode(ge_p3* h, const uint32_t s[8], bool negate) {
   const fe one = fe_one();
   fe y = fe_from_words(s);

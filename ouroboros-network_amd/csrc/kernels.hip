@@ -135,7 +135,7 @@ __global__ void __launch_bounds__(kBlock, OURO_WAVES) k_tpraos_verify(ouro_tprao
 // p50 0.5875 -> 0.5712 ms, profiles/r02d/ablat_rows_scan.json).
 __global__ void k_tpraos_cores(ouro_tpraos_batch b, const uint32_t* __restrict__ d_n,
                                int32_t* res_buf, int32_t* scratch,
-                               const int32_t* __restrict__ btab, int quad);
+                               const int32_t* __restrict__ btab, int mode, int wide_waves);
 __global__ void k_tpraos_finish(ouro_tpraos_batch b, const uint32_t* __restrict__ d_n,
                                 int32_t* res_buf, uint8_t* __restrict__ verdict,
                                 uint8_t* __restrict__ beta_eta, uint8_t* __restrict__ beta_leader,
@@ -283,10 +283,12 @@ int device_state(DeviceState** out) {
     if (std::string(prop.gcnArchName).rfind("gfx950", 0) != 0)
       return fail(OURO_ENODEV, std::string("device is ") + prop.gcnArchName + ", need gfx950");
     s.cus = prop.multiProcessorCount;
-    std::vector<int32_t> tab(kBTabWords);
+    // niels B tables, then their wave-wide form (latency mode, wide.h)
+    std::vector<int32_t> tab(kBTabWords + kBTabWideWords);
     build_btab(tab.data());
-    OURO_HIP(hipMalloc(&s.btab, sizeof(int32_t) * kBTabWords));
-    OURO_HIP(hipMemcpy(s.btab, tab.data(), sizeof(int32_t) * kBTabWords, hipMemcpyHostToDevice));
+    build_btab_wide(reinterpret_cast<uint16_t*>(tab.data() + kBTabWords), tab.data());
+    OURO_HIP(hipMalloc(&s.btab, sizeof(int32_t) * tab.size()));
+    OURO_HIP(hipMemcpy(s.btab, tab.data(), sizeof(int32_t) * tab.size(), hipMemcpyHostToDevice));
     for (int id = 0; id < kNumKernels; id++) {
       int per_cu = 0;
       OURO_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel_ptr(id), kBlock, 0));
@@ -450,6 +452,14 @@ int lat_quad() {
   return 1;
 }
 
+// Latency-mode cores run on one wave each (wide_cores.h): a mask over
+// tpraos.h HdrCore + kCoreGe/kCoreGl, default all eight (OURO_LAT_WIDE; 0 =
+// every core on lane quads, for A/B).
+int lat_wide_mask() {
+  if (const char* e = getenv("OURO_LAT_WIDE")) return (int)(strtol(e, nullptr, 0) & 0xff);
+  return 0xff;
+}
+
 // latency mode: eight cores per header (x4 lanes in quad mode), then the
 // finish; n and the option bits read from d_n[0..1].
 // Lanes used <= the kBlock-rounded count lowlat_scratch_words provides for.
@@ -466,10 +476,20 @@ int launch_lowlat(hipStream_t st, const ouro_tpraos_batch& b, const uint32_t* d_
     return (int)std::max<size_t>(1, std::min<size_t>(g, (size_t)ds->max_blocks[id] * per));
   };
   const int quad = lat_quad();
-  const int g1 = grid((size_t)kLatCores * n_cap << (quad ? 2 : 0), kCores);
+  // the wide cores on one wave each (nwide n_cap waves, rounded to whole
+  // workgroups) ahead of the other cores' lanes
+  const int wmask = lat_wide_mask();
+  const int nwide = __builtin_popcount((unsigned)wmask);
+  const size_t wide_waves = (size_t)nwide * n_cap;
+  const size_t wide_blocks = (wide_waves * 64 + blk - 1) / blk;
+  const size_t quad_items = (size_t)(kLatCores - nwide) * n_cap;
+  const int g1 = (int)wide_blocks + grid(quad_items << (quad ? 2 : 0), kCores);
   const int g2 = grid(n_cap << (quad ? 2 : 0), kFinish);
+  // timing probe: OURO_LAT_SKIP = mask of cores left out (verdicts then wrong)
+  const char* skip_env = getenv("OURO_LAT_SKIP");
+  const int skip = skip_env ? (int)(strtol(skip_env, nullptr, 0) & 0xff) : 0;
   hipLaunchKernelGGL(k_tpraos_cores, dim3(g1), dim3(blk), 0, st, b, d_n, res_buf, scratch,
-                     ds->btab, quad);
+                     ds->btab, quad | (skip << 8) | (wmask << 16), (int)(wide_blocks * blk / 64));
   if ((rc = launch_check())) return rc;
   hipLaunchKernelGGL(k_tpraos_finish, dim3(g2), dim3(blk), 0, st, b, d_n, res_buf, verdict, be,
                      bl, scratch, quad);

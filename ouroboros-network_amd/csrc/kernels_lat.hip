@@ -1,5 +1,6 @@
 // kernels_lat.hip -- the latency-mode kernels (configs[4] ChainSync windows):
-// eight cores per header on DPP lane quads, then the lane-pair finish.
+// eight cores per header, each on one wave (wide_cores.h) or on a DPP lane
+// quad, then the lane-pair finish.
 //
 // A translation unit of its own so that its lane routines use the row-order
 // field products (OURO_FE_SCAN=0): a lane quad issues one product per lane,
@@ -17,29 +18,138 @@
 #include "../../include/ouro_verify.h"
 #include "launch.h"
 
+#include "wide_cores.h"
+
 using namespace ouro;
 
-// Latency mode, launch 1: eight cores per header (work item w = core * n + i,
-// so each wave runs one core type), results to a per-header record.
-// quad = 1: each work item runs on the four lanes of a DPP quad, which share
-// its scratch slot and split every group operation's products (ge25519.h);
-// quad = 0: one lane per item.  n (d_n[0]) and the batch's optional members
-// (d_n[1], tpraos.h kOpt*) are read from device memory so a captured graph
-// serves any batch of n <= capacity.
+// One core of header i on one wave (wide_cores.h): the same checks and the
+// same record fields (lane 0 stores) as hdr_core with split V on a lane or
+// quad.  bw: the wide B tables (after the niels ones in btab).
+__device__ __noinline__ void hdr_core_wide(const ouro_tpraos_batch& b, size_t i, uint32_t opts,
+                                           int core, Slot res, const uint16_t* bw) {
+#if defined(__HIP_DEVICE_COMPILE__)  // wave-collective code (wide.h) is device-only
+  using namespace wide;
+  const bool lead = (threadIdx.x & 63u) == 0;
+  const bool leader = core == kCoreUl || core == kCoreVl || core == kCoreGl;
+  int32_t flag = 0;
+  switch (core) {
+    case kCoreOcert: {
+      uint32_t s[16], p[8], hv[8];
+      ld_words(s, b.ocert_sigma + 64 * i, 4);
+      ld_words(p, b.issuer_vk + 32 * i, 2);
+      ld_words(hv, b.hot_vk + 32 * i, 2);
+      OcertMsg m;
+      ocert_msg(m, hv, b.ocert_counter[i], b.ocert_kes_period[i]);
+      flag = ed25519_verify_wide(s, p, m, 48, bw) ? kFlagOk : 0;
+      break;
+    }
+    case kCoreKes: {
+      uint32_t hv[8];
+      ld_words(hv, b.hot_vk + 32 * i, 2);
+      const uint32_t* sw = reinterpret_cast<const uint32_t*>(b.kes_sig + 448 * i);
+      flag = sum6kes_verify_wide(hv, b.kes_t[i], sw, ShaGlobalTail{b.body + b.body_off[i]},
+                                 b.body_len[i], bw) ? kFlagOk : 0;
+      break;
+    }
+    case kCoreUe:
+    case kCoreUl: {
+      uint32_t p[8], pi[20];
+      ld_words(p, b.vrf_vk + 32 * i, 2);
+      ld_words(pi, (leader ? b.leader_proof : b.eta_proof) + 80 * i, 5);
+      ge_p2 U;
+      flag = vrf_u_wide(U, p, pi, bw) ? kFlagOk : 0;
+      if (lead) st_point(res, leader ? kPtUl : kPtUe, U.X, U.Y, U.Z);
+      break;
+    }
+    case kCoreVe:
+    case kCoreVl: {
+      uint32_t p[8], pi[20];
+      ld_words(p, b.vrf_vk + 32 * i, 2);
+      ld_words(pi, (leader ? b.leader_proof : b.eta_proof) + 80 * i, 5);
+      SeedMsg alpha;
+      hdr_seed(alpha, b, i, leader, opts);
+      ge_p3 H;
+      ge_p2 V;
+      vrf_sh(H, V, p, pi, alpha);
+      if (lead) {
+        st_point(res, leader ? kPtHl : kPtHe, H.X, H.Y, H.Z);
+        st_point(res, leader ? kPtVl : kPtVe, V.X, V.Y, V.Z);
+      }
+      flag = kFlagOk;
+      break;
+    }
+    default: {  // kCoreGe / kCoreGl
+      uint32_t pi[20];
+      ld_words(pi, (leader ? b.leader_proof : b.eta_proof) + 80 * i, 5);
+      ge_p2 part;
+      ge_p3 G8;
+      flag = vrf_gamma_wide(part, G8, pi);
+      if (lead) {
+        st_point_at(res + kLatPart + (leader ? kPtWords : 0), part.X, part.Y, part.Z);
+        st_point(res, leader ? kPtG8l : kPtG8e, G8.X, G8.Y, G8.Z);
+      }
+      break;
+    }
+  }
+  if (lead) stg1(res.word(kResFlags + core), flag);
+#endif
+}
+
+// the k-th set bit of m (k < popcount(m))
+__device__ __forceinline__ int nth_set_bit(uint32_t m, int k) {
+  for (int c = 0; c < 8; c++) {
+    if ((m >> c) & 1u) {
+      if (k == 0) return c;
+      k--;
+    }
+  }
+  return 7;
+}
+// the k-th clear bit of m among bits 0..7
+__device__ __forceinline__ int nth_clear_bit(uint32_t m, int k) { return nth_set_bit(~m & 0xffu, k); }
+
+// Latency mode, launch 1: eight cores per header, results to a per-header
+// record.  `mode` bit 0: the cores not run wide go on DPP lane quads (four
+// lanes share a scratch slot and split every group operation's products,
+// ge25519.h) or one lane each; bits 8..15: cores to skip (a timing probe,
+// OURO_LAT_SKIP; the verdicts are then wrong); bits 16..23: the cores run on
+// one wave each (wide_cores.h, OURO_LAT_WIDE).  The first wide_waves waves of
+// the grid run the wide items (wave w: core number w % nwide of header
+// w / nwide), the lanes after them the other cores (work item c * n + i:
+// core number c of header i, so each wave runs one core type).  n (d_n[0])
+// and the batch's optional members (d_n[1], tpraos.h kOpt*) are read from
+// device memory so a captured graph serves any batch of n <= capacity.
 __global__ void __launch_bounds__(kBlock, OURO_WAVES) k_tpraos_cores(ouro_tpraos_batch b,
                                                             const uint32_t* __restrict__ d_n,
                                                             int32_t* res_buf, int32_t* scratch,
                                                             const int32_t* __restrict__ btab,
-                                                            int quad) {
+                                                            int mode, int wide_waves) {
   const size_t n = d_n[0];
   const uint32_t opts = d_n[1];
+  const int quad = mode & 1;
+  const uint32_t skip = ((uint32_t)mode >> 8) & 0xffu;
+  const uint32_t wmask = ((uint32_t)mode >> 16) & 0xffu;
+  const int nwide = __builtin_popcount(wmask);
+  const size_t gtid = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const size_t wide_lanes = (size_t)wide_waves * 64;
+  if (gtid < wide_lanes) {  // wave-uniform
+    const size_t wv = gtid >> 6, i = wv / nwide;
+    const int core = nth_set_bit(wmask, (int)(wv % nwide));
+    if (i < n && !((skip >> core) & 1u))
+      hdr_core_wide(b, i, opts, core, slot_of(res_buf, i, kLatResWords),
+                    reinterpret_cast<const uint16_t*>(btab + kBTabWords));
+    return;
+  }
   const int sh = quad ? 2 : 0;
-  const size_t tid = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) >> sh;
-  const size_t nth = ((size_t)gridDim.x * blockDim.x) >> sh;
+  const size_t tid = (gtid - wide_lanes) >> sh;
+  const size_t nth = ((size_t)gridDim.x * blockDim.x - wide_lanes) >> sh;
   const Slot lane = slot_of(scratch, tid, kSlotWords);
-  for (size_t w = tid; w < (size_t)kLatCores * n; w += nth) {
-    const int core = (int)(w / n);
-    const size_t i = w - (size_t)core * n;
+  const int ncores = kLatCores - nwide;
+  for (size_t w = tid; w < (size_t)ncores * n; w += nth) {
+    const int c = (int)(w / n);
+    const size_t i = w - (size_t)c * n;
+    const int core = nth_clear_bit(wmask, c);
+    if ((skip >> core) & 1u) continue;
     hdr_core(b, i, opts, core, lane, slot_of(res_buf, i, kLatResWords), btab, /*share_key=*/false,
              /*split=*/true, quad != 0);
   }

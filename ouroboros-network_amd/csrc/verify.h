@@ -458,38 +458,12 @@ OURO_FI int wave_max_small(int x) {
 // with h = SHA-512(R || A || M) mod L.  The doubling chain is ~130 bits
 // instead of 253, and no inversion is needed: the result is compared to the
 // identity projectively.
+// The scalar side of the half-size equation: h = SHA-512(R || A || M) mod L,
+// its lattice pair (c0, c1) and b = c1 S mod L.
 template <class Tail>
-OURO_HD inline bool ed25519_verify_lane(const uint32_t sig[16], const uint32_t pk[8],
-                                        const Tail& msg, uint32_t mlen, Slot lane,
-                                        const int32_t* btab, bool byron = false,
-                                        bool quad = false) {
-  uint32_t R[8], S[8];
-#pragma unroll
-  for (int i = 0; i < 8; i++) {
-    R[i] = sig[i];
-    S[i] = sig[8 + i];
-  }
-  bool ok;
-  if (byron) {
-    ok = (S[7] >> 29) == 0;  // only the top three bits of S
-  } else {
-    ok = sc_is_canonical(S) && !ge_has_small_order(R);
-    ok = ok && ge_is_canonical(pk) && !ge_has_small_order(pk);
-  }
-  ge_p3 negA, negR;
-  bool okA, okR;
-  if (quad) {
-    ge_decode_pair_quad(&negA, &okA, &negR, &okR, pk, R, true);
-  } else {
-    okA = ge_decode(&negA, pk, true);
-    okR = ge_decode(&negR, R, true);
-  }
-  ok = okA && ok;
-  // encode(R') == R_bytes  <=>  R_bytes is the canonical encoding of R' (a point)
-  ok = ge_is_canonical(R) && ok;
-  ok = okR && ok;
-  ok = ok && !(fe_iszero(negR.X) && (R[7] >> 31) != 0);
-  // h = SHA-512(R || A || M) mod L
+OURO_HD inline void ed25519_scalars(HalfScalars& hs, uint32_t b[8], const uint32_t R[8],
+                                    const uint32_t S[8], const uint32_t pk[8], const Tail& msg,
+                                    uint32_t mlen) {
   uint32_t pre[16];
 #pragma unroll
   for (int i = 0; i < 8; i++) {
@@ -501,10 +475,9 @@ OURO_HD inline bool ed25519_verify_lane(const uint32_t sig[16], const uint32_t p
   uint32_t hw[16], h[8];
   sha512_digest_words(hw, H);
   sc_reduce512(h, hw);
-  HalfScalars hs;
   ed25519_half_scalars(hs, h);
   // b = c1 S mod L
-  uint32_t prod[16], b[8];
+  uint32_t prod[16];
 #pragma unroll
   for (int i = 0; i < 16; i++) prod[i] = 0;
 #pragma unroll
@@ -519,6 +492,53 @@ OURO_HD inline bool ed25519_verify_lane(const uint32_t sig[16], const uint32_t p
     prod[i + 8] = (uint32_t)carry;
   }
   sc_reduce512(b, prod);
+}
+
+// the encoding checks on (S, R, A) before decoding (libsodium / Byron rules)
+OURO_FI bool ed25519_precheck(const uint32_t R[8], const uint32_t S[8], const uint32_t pk[8],
+                              bool byron) {
+  if (byron) return (S[7] >> 29) == 0;  // only the top three bits of S
+  bool ok = sc_is_canonical(S) && !ge_has_small_order(R);
+  return ok && ge_is_canonical(pk) && !ge_has_small_order(pk);
+}
+
+// sig = R || S (16 words), pk (8 words), message bytes from global memory.
+// Accepts iff libsodium 1.0.18 does (App. B.1) -- or, for ByronDSIGN, the
+// donna-derived cardano-crypto rule (App. B.5) -- through the equivalent
+// half-size equation of lattice.h:
+//   R_bytes canonical, decodable, x = 0 only with sign 0, and
+//   [c1 S mod L]B + [c0](-A) + [c1](-R) == O,  c0 = c1 h (mod 8L), c1 odd,
+// with h = SHA-512(R || A || M) mod L.  The doubling chain is ~130 bits
+// instead of 253, and no inversion is needed: the result is compared to the
+// identity projectively.
+template <class Tail>
+OURO_HD inline bool ed25519_verify_lane(const uint32_t sig[16], const uint32_t pk[8],
+                                        const Tail& msg, uint32_t mlen, Slot lane,
+                                        const int32_t* btab, bool byron = false,
+                                        bool quad = false) {
+  uint32_t R[8], S[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    R[i] = sig[i];
+    S[i] = sig[8 + i];
+  }
+  bool ok = ed25519_precheck(R, S, pk, byron);
+  ge_p3 negA, negR;
+  bool okA, okR;
+  if (quad) {
+    ge_decode_pair_quad(&negA, &okA, &negR, &okR, pk, R, true);
+  } else {
+    okA = ge_decode(&negA, pk, true);
+    okR = ge_decode(&negR, R, true);
+  }
+  ok = okA && ok;
+  // encode(R') == R_bytes  <=>  R_bytes is the canonical encoding of R' (a point)
+  ok = ge_is_canonical(R) && ok;
+  ok = okR && ok;
+  ok = ok && !(fe_iszero(negR.X) && (R[7] >> 31) != 0);
+  HalfScalars hs;
+  uint32_t b[8];
+  ed25519_scalars(hs, b, R, S, pk, msg, mlen);
   // [|c0|](+-A) + [c1](-R) + [b]B, one ~130-bit doubling chain
   build_table(lane + kSlotTab1, hs.c0_neg ? ge_p3_neg(negA) : negA, quad);
   build_table(lane + kSlotTab2, negR, quad);
@@ -561,7 +581,10 @@ OURO_HD inline bool ed25519_verify_lane(const uint32_t sig[16], const uint32_t p
 // A^2 - 4 is a non-square) and m != 0 (neither (A-1)/2 nor 1/(2(A-1)) is a
 // square; tools/check_elligator_exceptions.py), so no inverse of zero can
 // occur where libsodium would have computed one.
-OURO_HD inline ge_p3 elligator2_h(const uint32_t r[8]) {
+// pow22523: z -> z^(2^252 - 3); the latency mode's wave-wide item passes the
+// wide exponentiation (wide.h), everything else fe_pow22523.
+template <class Pow>
+OURO_HD inline ge_p3 elligator2_h_with(const uint32_t r[8], Pow pow22523) {
   const fe A = fe_mont_a();
   fe rr = fe_from_words(r);
   fe r2 = fe_sq(rr);
@@ -573,7 +596,7 @@ OURO_HD inline ge_p3 elligator2_h(const uint32_t r[8]) {
   // beta = num W^3 (num W^7)^((p-5)/8)
   fe W3 = fe_mul(fe_sq(W), W);
   fe W7 = fe_mul(fe_sq(W3), W);
-  fe beta = fe_mul(fe_mul(num, W3), fe_pow22523(fe_mul(num, W7)));
+  fe beta = fe_mul(fe_mul(num, W3), pow22523(fe_mul(num, W7)));
   fe vxx = fe_mul(fe_sq(beta), W);
   const bool lam_p1 = fe_iszero(fe_sub4(vxx, num));
   const bool lam_m1 = fe_iszero(fe_add(vxx, num));
@@ -590,6 +613,9 @@ OURO_HD inline ge_p3 elligator2_h(const uint32_t r[8]) {
   const fe nc = fe_carry(n);
   ge_p3 P{fe_mul(x, m), nc, m, fe_mul(x, nc)};
   return ge_mul8(P);
+}
+OURO_HD inline ge_p3 elligator2_h(const uint32_t r[8]) {
+  return elligator2_h_with(r, [](const fe& z) { return fe_pow22523(z); });
 }
 
 // The straight restatement of ge25519_from_uniform (4 exponentiations), kept
@@ -735,11 +761,10 @@ OURO_HD inline bool vrf03_verify_lane(uint32_t beta[16], const uint32_t pk[8],
 // ---- Sum6KES --------------------------------------------------------------------
 // sig (448 B) is read from global memory: leaf signature, then (vk0, vk1) for
 // levels 1..6 bottom-up; verification walks top-down from the root vk.
-template <class Tail>
-OURO_HD inline bool sum6kes_verify_lane(const uint32_t vk[8], uint32_t t, const uint32_t* sigw,
-                                        const Tail& msg, uint32_t mlen, Slot lane,
-                                        const int32_t* btab, bool quad = false) {
-  uint32_t cur[8];
+// the Merkle walk: checks the six (vk0, vk1) levels against the root vk and
+// returns the leaf's verification key in cur and its signature in sig
+OURO_HD inline bool sum6kes_walk(uint32_t cur[8], uint32_t sig[16], const uint32_t vk[8],
+                                 uint32_t t, const uint32_t* sigw) {
 #pragma unroll
   for (int i = 0; i < 8; i++) cur[i] = vk[i];
   bool ok = true;
@@ -761,12 +786,20 @@ OURO_HD inline bool sum6kes_verify_lane(const uint32_t vk[8], uint32_t t, const 
 #pragma unroll
     for (int i = 0; i < 8; i++) cur[i] = right ? pw[8 + i] : pw[i];
   }
-  uint32_t sig[16];
 #pragma unroll
   for (int i = 0; i < 4; i++) {
     const int4 v = ldg4(sigw + 4 * i);
     sig[4 * i] = v.x; sig[4 * i + 1] = v.y; sig[4 * i + 2] = v.z; sig[4 * i + 3] = v.w;
   }
+  return ok;
+}
+
+template <class Tail>
+OURO_HD inline bool sum6kes_verify_lane(const uint32_t vk[8], uint32_t t, const uint32_t* sigw,
+                                        const Tail& msg, uint32_t mlen, Slot lane,
+                                        const int32_t* btab, bool quad = false) {
+  uint32_t cur[8], sig[16];
+  const bool ok = sum6kes_walk(cur, sig, vk, t, sigw);
   const bool leaf = ed25519_verify_lane(sig, cur, msg, mlen, lane, btab, false, quad);
   return ok && leaf;
 }
@@ -819,6 +852,25 @@ inline void build_btab(int32_t* out) {
   ge_p3 B128 = B;
   for (int i = 0; i < 128; i++) B128 = ge_p1p1_to_p3(ge_p3_dbl(B128));
   build_btab_one(out + (size_t)kBTabEntries * kNielsWords, B128);
+}
+
+// The fixed-base tables in the latency mode's wave-wide form (wide.h
+// bw_operand), stored after the niels ones: per entry the canonical 16-bit
+// limbs of y - x, y + x and 2dxy.
+constexpr int kBWideU16 = 48;
+constexpr size_t kBTabWideWords = (size_t)kBTabEntries * kBWideU16;  // both halves, int32 words
+inline void build_btab_wide(uint16_t* out, const int32_t* niels) {
+  for (size_t e = 0; e < 2 * (size_t)kBTabEntries; e++) {
+    const int32_t* q = niels + e * kNielsWords;
+    for (int k = 0; k < 3; k++) {
+      const int32_t* c = q + (k == 0 ? 10 : (k == 1 ? 0 : 20));  // y - x, y + x, 2dxy
+      const fe f = fe_make(c[0], c[1], c[2], c[3], c[4], c[5], c[6], c[7], c[8], c[9]);
+      uint32_t w[8];
+      fe_to_words(w, f);
+      for (int j = 0; j < 16; j++)
+        out[e * kBWideU16 + 16 * k + j] = (uint16_t)((w[j >> 1] >> (16 * (j & 1))) & 0xffffu);
+    }
+  }
 }
 
 }  // namespace ouro

@@ -1,0 +1,213 @@
+// wide_test.hip -- TEST-ONLY: the wave-wide arithmetic of wide.h checked
+// against the lane-local routines it replaces (fe25519.h / ge25519.h), on the
+// device, one wave per case.  tests/test_gpu_wide.py drives it; the product
+// library does not contain this file.
+#include <hip/hip_runtime.h>
+
+#include "verify.h"
+#include "wide_cores.h"
+
+using namespace ouro;
+
+namespace {
+
+__device__ uint64_t mix64(uint64_t z) {
+  z += 0x9e3779b97f4a7c15ull;
+  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+  z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+  return z ^ (z >> 31);
+}
+__device__ void rand_words(uint32_t w[8], uint64_t seed, uint64_t tag) {
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    const uint64_t v = mix64(seed * 0x100000001b3ull + tag * 131 + k);
+    w[2 * k] = (uint32_t)v;
+    w[2 * k + 1] = (uint32_t)(v >> 32);
+  }
+}
+__device__ bool same_fe(const fe& a, const fe& b) {
+  uint32_t x[8], y[8];
+  fe_to_words(x, a);
+  fe_to_words(y, b);
+  uint32_t d = 0;
+#pragma unroll
+  for (int k = 0; k < 8; k++) d |= x[k] ^ y[k];
+  return d == 0;
+}
+__device__ void enc_p3(uint32_t e[8], const fe& X, const fe& Y, const fe& Z) {
+  ge_encode_with_inv(e, X, Y, fe_invert(Z));
+}
+#if defined(__HIP_DEVICE_COMPILE__)
+__device__ bool same_point(const ge_p3& P, const wide::pw& W) {
+  uint32_t a[8], b[8];
+  enc_p3(a, P.X, P.Y, P.Z);
+  enc_p3(b, wide::fw_to_fe(W.X), wide::fw_to_fe(W.Y), wide::fw_to_fe(W.Z));
+  uint32_t d = 0;
+#pragma unroll
+  for (int k = 0; k < 8; k++) d |= a[k] ^ b[k];
+  // T consistent: X Y = Z T
+  const fe xy = fe_mul(wide::fw_to_fe(W.X), wide::fw_to_fe(W.Y));
+  const fe zt = fe_mul(wide::fw_to_fe(W.Z), wide::fw_to_fe(W.T));
+  return d == 0 && same_fe(xy, zt);
+}
+#endif
+
+constexpr int kTests = 10;
+
+// out[wave * kTests + t] = 1 when test t passed; dbg (wave 0): fw_mul's
+// sixteen row-0 limbs, then the expected canonical words
+#ifndef WT_BOUNDS
+#define WT_BOUNDS 64
+#endif
+__global__ void __launch_bounds__(WT_BOUNDS) k_wide_selftest(uint64_t seed, int32_t* out, int32_t* dbg) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  using namespace wide;
+  const Lanes L = lanes();
+  const uint64_t wv = blockIdx.x;
+  const uint64_t sd = seed ^ (wv << 20);
+  uint32_t wa[8], wb[8], wr[8];
+  rand_words(wa, sd, 1);
+  rand_words(wb, sd, 2);
+  rand_words(wr, sd, 3);
+  wa[7] &= 0x7fffffffu;
+  wb[7] &= 0x7fffffffu;
+  wr[7] &= 0x7fffffffu;
+  if (wv == 1) {  // edge: p - 1 and 0
+    for (int k = 0; k < 8; k++) { wa[k] = 0xffffffffu; wb[k] = 0u; }
+    wa[0] = 0xffffffecu;
+    wa[7] = 0x7fffffffu;
+  }
+  if (wv == 2) {  // edge: p - 1 squared, 2^255 - 20 times 2^255 - 20
+    for (int k = 0; k < 8; k++) wa[k] = wb[k] = 0xffffffffu;
+    wa[0] = wb[0] = 0xffffffecu;
+    wa[7] = wb[7] = 0x7fffffffu;
+  }
+  const fe a = fe_from_words(wa), b = fe_from_words(wb);
+  int32_t res[kTests];
+  // 0: conversion round trip
+  res[0] = same_fe(fw_to_fe(fe_to_fw(a, L)), a) && same_fe(fw_to_fe(fe_to_fw(b, L)), b);
+  // 1: product
+  const int32_t m = fw_mul(fe_to_fw(a, L), fe_to_fw(b, L), L);
+  res[1] = same_fe(fw_to_fe(m), fe_mul(a, b));
+  if (wv == 0 && threadIdx.x < 16) {
+    dbg[threadIdx.x] = m;
+    uint32_t e[8];
+    fe_to_words(e, fe_mul(a, b));
+    if (threadIdx.x < 8) dbg[16 + threadIdx.x] = (int32_t)e[threadIdx.x];
+  }
+  // 2: square, and a chain of 20 squarings (bounds stay closed)
+  int32_t sq = fw_sq(fe_to_fw(a, L), L);
+  fe sq_ref = fe_sq(a);
+  bool ok = same_fe(fw_to_fe(sq), sq_ref);
+  for (int k = 0; k < 20; k++) {
+    sq = fw_sq(sq, L);
+    sq_ref = fe_sq(sq_ref);
+  }
+  res[2] = ok && same_fe(fw_to_fe(sq), sq_ref);
+  // 3: z^(2^252 - 3)
+  res[3] = same_fe(fw_to_fe(fw_pow22523(fe_to_fw(a, L))), fe_pow22523(a));
+  // points: Elligator2 images
+  const ge_p3 P = elligator2_h(wa), Q = elligator2_h(wb);
+  const pw Pw = pw_from_p3(P, L), Qw = pw_from_p3(Q, L);
+  const int32_t d2 = fe_to_fw(fe_d2(), L);
+  // 4: doubling (twice, the second from a wide result)
+  const ge_p3 P2 = ge_p1p1_to_p3(ge_p3_dbl(P));
+  const ge_p3 P4 = ge_p1p1_to_p3(ge_p3_dbl(P2));
+  const pw P2w = pw_dbl(Pw, L);
+  res[4] = same_point(P2, P2w) && same_point(P4, pw_dbl(P2w, L));
+  // 5: P + Q and P - Q, then (P + Q) + (P + Q) via add
+  const ge_cached Qc = ge_p3_to_cached(Q);
+  const cw qw = pw_cached(Qw, d2, L);
+  const ge_p3 S = ge_p1p1_to_p3(ge_add_cached(P, Qc, false));
+  const ge_p3 D = ge_p1p1_to_p3(ge_add_cached(P, Qc, true));
+  const pw Sw = pw_add(Pw, qw.pos, L);
+  const pw Dw = pw_add(Pw, qw.neg, L);
+  const cw sw = pw_cached(Sw, d2, L);
+  const ge_p3 SS = ge_p1p1_to_p3(ge_add_cached(S, ge_p3_to_cached(S), false));
+  res[5] = same_point(S, Sw) && same_point(D, Dw) && same_point(SS, pw_add(Sw, sw.pos, L));
+  // 6: [s]P, s reduced mod L, against double-and-add on the lane
+  uint32_t s[8];
+  sc_reduce256(s, wr);
+  TabW tab;
+  tab_build(tab, Pw, d2, L);
+  const pw R = pw_scalarmult(tab, s, L);
+  ge_p3 acc = ge_p3_identity();
+  const ge_cached Pc = ge_p3_to_cached(P);
+  for (int bit = 252; bit >= 0; bit--) {
+    acc = ge_p1p1_to_p3(ge_p3_dbl(acc));
+    if ((s[bit >> 5] >> (bit & 31)) & 1u) acc = ge_p1p1_to_p3(ge_add_cached(acc, Pc, false));
+  }
+  res[6] = same_point(acc, R);
+  // 7: the identity through an addition and a doubling
+  const pw I = pw_identity(L);
+  res[7] = same_point(P, pw_add(I, pw_cached(Pw, d2, L).pos, L)) &&
+           same_point(ge_p3_identity(), pw_dbl(I, L));
+  // 8, 9: the latency mode's [s]H item (wide_vrf.h) against the lane
+  // routines: H = Elligator2(SHA-512(suite || 0x01 || pk || alpha)), [s]H
+  {
+    uint32_t pk[8], pi[20];
+    rand_words(pk, sd, 4);
+    rand_words(pi, sd, 5);
+    rand_words(pi + 8, sd, 6);
+    rand_words(pi + 12, sd, 7);
+    SeedMsg alpha;
+    rand_words(alpha.w, sd, 8);
+    ge_p3 Hw;
+    ge_p2 Vw;
+    vrf_sh(Hw, Vw, pk, pi, alpha);
+    uint32_t pre[9];
+    pre[0] = 0x04u | (0x01u << 8) | (pk[0] << 16);
+    for (int k = 1; k < 8; k++) pre[k] = (pk[k - 1] >> 16) | (pk[k] << 16);
+    pre[8] = pk[7] >> 16;
+    uint64_t Hs[8];
+    sha512_prefixed<34>(Hs, pre, alpha, 32);
+    uint32_t rw[16];
+    sha512_digest_words(rw, Hs);
+    rw[7] &= 0x7fffffffu;
+    const ge_p3 Href = elligator2_h(rw);
+    uint32_t e1[8], e2[8];
+    enc_p3(e1, Href.X, Href.Y, Href.Z);
+    enc_p3(e2, Hw.X, Hw.Y, Hw.Z);
+    uint32_t dd = 0;
+    for (int k = 0; k < 8; k++) dd |= e1[k] ^ e2[k];
+    res[8] = dd == 0;
+    uint32_t sv[8];
+    sc_reduce256(sv, pi + 12);
+    ge_p3 acc2 = ge_p3_identity();
+    const ge_cached Hc = ge_p3_to_cached(Href);
+    for (int bit = 252; bit >= 0; bit--) {
+      acc2 = ge_p1p1_to_p3(ge_p3_dbl(acc2));
+      if ((sv[bit >> 5] >> (bit & 31)) & 1u) acc2 = ge_p1p1_to_p3(ge_add_cached(acc2, Hc, false));
+    }
+    enc_p3(e1, acc2.X, acc2.Y, acc2.Z);
+    enc_p3(e2, Vw.X, Vw.Y, Vw.Z);
+    dd = 0;
+    for (int k = 0; k < 8; k++) dd |= e1[k] ^ e2[k];
+    res[9] = dd == 0;
+  }
+  if (threadIdx.x == 0)
+    for (int t = 0; t < kTests; t++) out[wv * kTests + t] = res[t];
+#endif
+}
+
+}  // namespace
+
+extern "C" {
+// waves cases from seed; out: waves * 10 int32 (1 = pass), dbg: 24 int32.
+// Returns 0, or -2 on a HIP error.
+int ouro_wide_selftest(int waves, uint64_t seed, int32_t* out, int32_t* dbg) {
+  int32_t *d_out = nullptr, *d_dbg = nullptr;
+  if (hipMalloc(&d_out, sizeof(int32_t) * waves * kTests) != hipSuccess) return -2;
+  if (hipMalloc(&d_dbg, sizeof(int32_t) * 24) != hipSuccess) return -2;
+  (void)hipMemset(d_out, 0xff, sizeof(int32_t) * waves * kTests);
+  hipLaunchKernelGGL(k_wide_selftest, dim3(waves), dim3(64), 0, 0, seed, d_out, d_dbg);
+  int rc = hipDeviceSynchronize() == hipSuccess && hipGetLastError() == hipSuccess ? 0 : -2;
+  if (!rc) {
+    rc |= hipMemcpy(out, d_out, sizeof(int32_t) * waves * kTests, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -2;
+    rc |= hipMemcpy(dbg, d_dbg, sizeof(int32_t) * 24, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -2;
+  }
+  (void)hipFree(d_out);
+  (void)hipFree(d_dbg);
+  return rc;
+}
+}
