@@ -55,7 +55,7 @@ __device__ __forceinline__ Lanes lanes() {
 __device__ __forceinline__ int32_t s24(int32_t x) { return (x << 8) >> 8; }
 template <int C>
 __device__ __forceinline__ int32_t dpp(int32_t x) {
-  return __builtin_amdgcn_mov_dpp(x, C, 0xf, 0xf, false);
+  return __builtin_amdgcn_mov_dpp(x, C, 0xf, 0xf, true);  // bound_ctrl: DPP-combinable
 }
 __device__ __forceinline__ int32_t ror1(int32_t x) { return dpp<0x121>(x); }  // lane j <- j-1
 template <int I>
@@ -74,20 +74,25 @@ __device__ __forceinline__ int32_t fw_carry(int64_t acc, int32_t fac) {
   return s24(ror1(hi)) * s24(fac) + lo;
 }
 
+#ifndef OURO_FW_ACC2
+#define OURO_FW_ACC2 1  // A/B switch: even and odd steps in two accumulators
+#endif
 template <int I>
-__device__ __forceinline__ void fw_mul_steps(int64_t& acc, int32_t& G, int32_t f, int32_t fac) {
+__device__ __forceinline__ void fw_mul_steps(int64_t& acc0, int64_t& acc1, int32_t& G, int32_t f,
+                                             int32_t fac) {
   if constexpr (I > 0) G = s24(ror1(G)) * s24(fac);
   const int64_t p = (int64_t)bcast<I>(f) * G;
-  if constexpr (I == 0) acc = p; else acc += p;
-  if constexpr (I < 15) fw_mul_steps<I + 1>(acc, G, f, fac);
+  int64_t& acc = (OURO_FW_ACC2 && (I & 1)) ? acc1 : acc0;
+  if constexpr (I == 0 || (OURO_FW_ACC2 && I == 1)) acc = p; else acc += p;
+  if constexpr (I < 15) fw_mul_steps<I + 1>(acc0, acc1, G, f, fac);
 }
 
 // f * g per row (g: the narrow operand, |g| <= 196,833 per limb)
 __device__ __forceinline__ int32_t fw_mul(int32_t f, int32_t g, const Lanes& L) {
-  int64_t acc;
+  int64_t acc0, acc1 = 0;
   int32_t G = g;
-  fw_mul_steps<0>(acc, G, f, L.fac);
-  return fw_carry(acc, L.fac);
+  fw_mul_steps<0>(acc0, acc1, G, f, L.fac);
+  return fw_carry(OURO_FW_ACC2 ? acc0 + acc1 : acc0, L.fac);
 }
 __device__ __forceinline__ int32_t fw_sq(int32_t f, const Lanes& L) { return fw_mul(f, f, L); }
 
