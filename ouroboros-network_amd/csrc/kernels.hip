@@ -135,7 +135,9 @@ __global__ void __launch_bounds__(kBlock, OURO_WAVES) k_tpraos_verify(ouro_tprao
 // p50 0.5875 -> 0.5712 ms, profiles/r02d/ablat_rows_scan.json).
 __global__ void k_tpraos_cores(ouro_tpraos_batch b, const uint32_t* __restrict__ d_n,
                                int32_t* res_buf, int32_t* scratch,
-                               const int32_t* __restrict__ btab, int mode, int wide_waves);
+                               const int32_t* __restrict__ btab, int mode, int wide_waves,
+                               uint8_t* __restrict__ verdict, uint8_t* __restrict__ beta_eta,
+                               uint8_t* __restrict__ beta_leader);
 __global__ void k_tpraos_finish(ouro_tpraos_batch b, const uint32_t* __restrict__ d_n,
                                 int32_t* res_buf, uint8_t* __restrict__ verdict,
                                 uint8_t* __restrict__ beta_eta, uint8_t* __restrict__ beta_leader,
@@ -460,6 +462,11 @@ int lat_wide_mask() {
   return 0xff;
 }
 
+int lat_fuse() {
+  if (const char* e = getenv("OURO_LAT_FUSE")) return atoi(e) != 0;
+  return 1;
+}
+
 // latency mode: eight cores per header (x4 lanes in quad mode), then the
 // finish; n and the option bits read from d_n[0..1].
 // Lanes used <= the kBlock-rounded count lowlat_scratch_words provides for.
@@ -488,9 +495,14 @@ int launch_lowlat(hipStream_t st, const ouro_tpraos_batch& b, const uint32_t* d_
   // timing probe: OURO_LAT_SKIP = mask of cores left out (verdicts then wrong)
   const char* skip_env = getenv("OURO_LAT_SKIP");
   const int skip = skip_env ? (int)(strtol(skip_env, nullptr, 0) & 0xff) : 0;
+  // fused (all eight cores wide): the last core of a header finishes it, no
+  // second launch (OURO_LAT_FUSE=0 keeps the finish launch, for A/B)
+  const bool fused = wmask == 0xff && lat_fuse();
   hipLaunchKernelGGL(k_tpraos_cores, dim3(g1), dim3(blk), 0, st, b, d_n, res_buf, scratch,
-                     ds->btab, quad | (skip << 8) | (wmask << 16), (int)(wide_blocks * blk / 64));
+                     ds->btab, quad | (skip << 8) | (wmask << 16) | (fused ? 1 << 24 : 0),
+                     (int)(wide_blocks * blk / 64), verdict, be, bl);
   if ((rc = launch_check())) return rc;
+  if (fused) return OURO_OK;
   hipLaunchKernelGGL(k_tpraos_finish, dim3(g2), dim3(blk), 0, st, b, d_n, res_buf, verdict, be,
                      bl, scratch, quad);
   return launch_check();
@@ -883,6 +895,8 @@ int hdr_batch_once(const ouro_tpraos_batch* b, const HdrOut& o, bool lowlat) {
     int32_t* res = sg.out<int32_t>(slot_region_words(n, kLatResWords));
     int32_t* scr = sg.out<int32_t>(lowlat_scratch_words(ds, n));
     if (sg.rc) return sg.rc;
+    // the fused launch's arrival counters start at zero (its tails reset them)
+    OURO_HIP(hipMemsetAsync(res, 0, sizeof(int32_t) * slot_region_words(n, kLatResWords), st));
     // (nw is read by the H2D above; this frame outlives the sync below)
     if ((rc = launch_lowlat(st, s.d, d_n, n, res, scr, s.ver, s.be, s.bl))) return rc;
   } else if ((rc = launch_hdr(st, s.d, s.ver, s.be, s.bl))) {
@@ -1237,6 +1251,8 @@ int plan_build(ouro_tpraos_plan* p) {
   OURO_HIP(hipMalloc(&p->d_in, p->in_bytes));
   OURO_HIP(hipMalloc(&p->d_out, p->out_bytes));
   OURO_HIP(hipMalloc(&p->res, sizeof(int32_t) * slot_region_words(p->cap, kLatResWords)));
+  // the fused launch's arrival counters start at zero (its tails reset them)
+  OURO_HIP(hipMemset(p->res, 0, sizeof(int32_t) * slot_region_words(p->cap, kLatResWords)));
   OURO_HIP(hipMalloc(&p->scratch, sizeof(int32_t) * lowlat_scratch_words(ds, p->cap)));
   memset(p->h_in, 0, p->in_bytes);
   uint8_t* d = p->d_in;

@@ -25,8 +25,10 @@ using namespace ouro;
 // One core of header i on one wave (wide_cores.h): the same checks and the
 // same record fields (lane 0 stores) as hdr_core with split V on a lane or
 // quad.  bw: the wide B tables (after the niels ones in btab).
+// fused: U, V and Gamma cores store encodings and beta instead of points
+// (the whole V on the V core; hdr_tail_wide finishes), for the fused launch.
 __device__ __noinline__ void hdr_core_wide(const ouro_tpraos_batch& b, size_t i, uint32_t opts,
-                                           int core, Slot res, const uint16_t* bw) {
+                                           int core, Slot res, const uint16_t* bw, bool fused) {
 #if defined(__HIP_DEVICE_COMPILE__)  // wave-collective code (wide.h) is device-only
   using namespace wide;
   const bool lead = (threadIdx.x & 63u) == 0;
@@ -58,7 +60,13 @@ __device__ __noinline__ void hdr_core_wide(const ouro_tpraos_batch& b, size_t i,
       ld_words(pi, (leader ? b.leader_proof : b.eta_proof) + 80 * i, 5);
       ge_p2 U;
       flag = vrf_u_wide(U, p, pi, bw) ? kFlagOk : 0;
-      if (lead) st_point(res, leader ? kPtUl : kPtUe, U.X, U.Y, U.Z);
+      if (fused) {
+        uint32_t enc[8];
+        encode_p2(enc, U);
+        if (lead) st_words8(res + kLatEnc + 8 * (3 * (int)leader + 1), enc);
+      } else if (lead) {
+        st_point(res, leader ? kPtUl : kPtUe, U.X, U.Y, U.Z);
+      }
       break;
     }
     case kCoreVe:
@@ -68,6 +76,16 @@ __device__ __noinline__ void hdr_core_wide(const ouro_tpraos_batch& b, size_t i,
       ld_words(pi, (leader ? b.leader_proof : b.eta_proof) + 80 * i, 5);
       SeedMsg alpha;
       hdr_seed(alpha, b, i, leader, opts);
+      if (fused) {
+        uint32_t Henc[8], Venc[8];
+        vrf_v_full_wide(Henc, Venc, p, pi, alpha);
+        if (lead) {
+          st_words8(res + kLatEnc + 8 * (3 * (int)leader + 0), Henc);
+          st_words8(res + kLatEnc + 8 * (3 * (int)leader + 2), Venc);
+        }
+        flag = kFlagOk;
+        break;
+      }
       ge_p3 H;
       ge_p2 V;
       vrf_sh(H, V, p, pi, alpha);
@@ -81,6 +99,15 @@ __device__ __noinline__ void hdr_core_wide(const ouro_tpraos_batch& b, size_t i,
     default: {  // kCoreGe / kCoreGl
       uint32_t pi[20];
       ld_words(pi, (leader ? b.leader_proof : b.eta_proof) + 80 * i, 5);
+      if (fused) {
+        uint32_t beta[16];
+        flag = vrf_gamma_beta_wide(beta, pi);
+        if (lead) {
+          st_words8(res + kLatBeta + 16 * (int)leader, beta);
+          st_words8(res + kLatBeta + 16 * (int)leader + 8, beta + 8);
+        }
+        break;
+      }
       ge_p2 part;
       ge_p3 G8;
       flag = vrf_gamma_wide(part, G8, pi);
@@ -113,7 +140,9 @@ __device__ __forceinline__ int nth_clear_bit(uint32_t m, int k) { return nth_set
 // lanes share a scratch slot and split every group operation's products,
 // ge25519.h) or one lane each; bits 8..15: cores to skip (a timing probe,
 // OURO_LAT_SKIP; the verdicts are then wrong); bits 16..23: the cores run on
-// one wave each (wide_cores.h, OURO_LAT_WIDE).  The first wide_waves waves of
+// one wave each (wide_cores.h, OURO_LAT_WIDE); bit 24 (all eight wide): the
+// fused form -- each core encodes its points, the header's last core to
+// arrive runs the finish (hdr_tail_wide), and there is no second launch.  The first wide_waves waves of
 // the grid run the wide items (wave w: core number w % nwide of header
 // w / nwide), the lanes after them the other cores (work item c * n + i:
 // core number c of header i, so each wave runs one core type).  n (d_n[0])
@@ -123,21 +152,31 @@ __global__ void __launch_bounds__(kBlock, OURO_WAVES) k_tpraos_cores(ouro_tpraos
                                                             const uint32_t* __restrict__ d_n,
                                                             int32_t* res_buf, int32_t* scratch,
                                                             const int32_t* __restrict__ btab,
-                                                            int mode, int wide_waves) {
+                                                            int mode, int wide_waves,
+                                                            uint8_t* __restrict__ verdict,
+                                                            uint8_t* __restrict__ beta_eta,
+                                                            uint8_t* __restrict__ beta_leader) {
   const size_t n = d_n[0];
   const uint32_t opts = d_n[1];
   const int quad = mode & 1;
   const uint32_t skip = ((uint32_t)mode >> 8) & 0xffu;
   const uint32_t wmask = ((uint32_t)mode >> 16) & 0xffu;
   const int nwide = __builtin_popcount(wmask);
+  const bool fused = ((uint32_t)mode >> 24) & 1u;
   const size_t gtid = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   const size_t wide_lanes = (size_t)wide_waves * 64;
   if (gtid < wide_lanes) {  // wave-uniform
     const size_t wv = gtid >> 6, i = wv / nwide;
     const int core = nth_set_bit(wmask, (int)(wv % nwide));
-    if (i < n && !((skip >> core) & 1u))
-      hdr_core_wide(b, i, opts, core, slot_of(res_buf, i, kLatResWords),
-                    reinterpret_cast<const uint16_t*>(btab + kBTabWords));
+    if (i >= n) return;
+    const Slot res = slot_of(res_buf, i, kLatResWords);
+    if (!((skip >> core) & 1u))
+      hdr_core_wide(b, i, opts, core, res, reinterpret_cast<const uint16_t*>(btab + kBTabWords),
+                    fused);
+#if defined(__HIP_DEVICE_COMPILE__)
+    if (fused && wide::arrive_last(res.word(kLatCtr)))
+      wide::hdr_tail_wide(b, i, opts, res, verdict, beta_eta, beta_leader);
+#endif
     return;
   }
   const int sh = quad ? 2 : 0;

@@ -29,9 +29,14 @@ enum HdrPoint { kPtHe = 0, kPtUe, kPtVe, kPtG8e, kPtHl, kPtUl, kPtVl, kPtG8l, kH
 constexpr int kPtWords = 36;                          // X, Y, Z at a 12-word stride
 constexpr int kResFlags = kHdrPoints * kPtWords;      // 6 flag words, one per core
 constexpr int kResWords = kResFlags + 8;              // 296 words (16-B multiple)
-// latency mode: the record plus the two -[c]Gamma partial points
+// latency mode: the record plus the two -[c]Gamma partial points, and for the
+// fused wave-wide mode (kernels_lat.hip) per VRF the encodings of H, U, V
+// (8 words each), its beta (16 words), and the header's arrival counter
 constexpr int kLatPart = kResWords;
-constexpr int kLatResWords = kResWords + 2 * kPtWords;  // 368 words (16-B multiple)
+constexpr int kLatEnc = kLatPart + 2 * kPtWords;      // enc(which, k) at kLatEnc + 8 (3 which + k)
+constexpr int kLatBeta = kLatEnc + 48;                // beta(which) at kLatBeta + 16 which
+constexpr int kLatCtr = kLatBeta + 32;
+constexpr int kLatResWords = kLatCtr + 4;             // 452 words (16-B multiple)
 enum HdrCore { kCoreOcert = 0, kCoreKes, kCoreUe, kCoreUl, kCoreVe, kCoreVl, kHdrCores,
                // latency mode splits each V = [s]H - [c]Gamma over two lanes: the V
                // cores do [s]H (252-bit chain), these do -[c]Gamma (128-bit chain)
@@ -202,6 +207,36 @@ OURO_FI void pack_shifted(uint32_t* dst, int word0, const uint32_t p[8]) {
 #pragma unroll
   for (int i = 1; i < 8; i++) dst[word0 - 1 + i] = (p[i - 1] >> 16) | (p[i] << 16);
   dst[word0 + 7] = p[7] >> 16;
+}
+
+// beta = SHA-512(suite || 0x03 || encode([8]Gamma))
+OURO_HD inline void vrf_beta(uint32_t beta[16], const uint32_t G8enc[8]) {
+  uint32_t bp[9];
+  bp[0] = 0x04u | (0x03u << 8);
+  pack_shifted(bp, 1, G8enc);
+  uint64_t Hb[8];
+  sha512_prefixed<34>(Hb, bp, ShaNoTail{}, 0);
+  sha512_digest_words(beta, Hb);
+}
+
+// c' = SHA-512(suite || 0x02 || H || Gamma || U || V)[0..16) == c
+OURO_HD inline bool vrf_challenge_ok(const uint32_t Henc[8], const uint32_t Genc[8],
+                                     const uint32_t Uenc[8], const uint32_t Venc[8],
+                                     const uint32_t c[4]) {
+  uint32_t hp[33];
+  hp[0] = 0x04u | (0x02u << 8);
+  pack_shifted(hp, 1, Henc);
+  pack_shifted(hp, 9, Genc);
+  pack_shifted(hp, 17, Uenc);
+  pack_shifted(hp, 25, Venc);
+  uint64_t Hc[8];
+  sha512_prefixed<130>(Hc, hp, ShaNoTail{}, 0);
+  uint32_t cw[16];
+  sha512_digest_words(cw, Hc);
+  bool ceq = true;
+#pragma unroll
+  for (int i = 0; i < 4; i++) ceq = ceq && cw[i] == c[i];
+  return ceq;
 }
 
 // c' check and beta for one VRF; H/U/V/G8 encodings given

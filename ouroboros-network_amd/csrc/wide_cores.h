@@ -81,12 +81,41 @@ __device__ __forceinline__ bool ed25519_verify_wide(const uint32_t sig[16], cons
   return ok && pw_is_identity(Q);
 }
 
+// verify.h sum6kes_walk with the six Blake2b hashes at once: lane k hashes
+// the (vk0, vk1) pair of level k + 1 (lanes 6.. repeat them), then the walk
+// reads each level's digest out of its lane
+__device__ __forceinline__ bool sum6kes_walk_wide(uint32_t cur[8], uint32_t sig[16],
+                                                  const uint32_t vk[8], uint32_t t,
+                                                  const uint32_t* sigw) {
+  const int mine = (int)((threadIdx.x & 63u) % 6u);
+  uint32_t pw[16], h[8];
+  ld_words(pw, reinterpret_cast<const uint8_t*>(sigw + 16 + 16 * mine), 4);
+  blake2b256_64(h, pw);
+#pragma unroll
+  for (int i = 0; i < 8; i++) cur[i] = vk[i];
+  bool ok = true;
+#pragma unroll
+  for (int k = 6; k >= 1; k--) {
+    uint32_t pk[16];
+    ld_words(pk, reinterpret_cast<const uint8_t*>(sigw + 16 + 16 * (k - 1)), 4);
+#pragma unroll
+    for (int i = 0; i < 8; i++) ok = ok && (uint32_t)__builtin_amdgcn_readlane((int)h[i], k - 1) == cur[i];
+    const uint32_t half = 1u << (k - 1);
+    const bool right = t >= half;
+    t = right ? t - half : t;
+#pragma unroll
+    for (int i = 0; i < 8; i++) cur[i] = right ? pk[8 + i] : pk[i];
+  }
+  ld_words(sig, reinterpret_cast<const uint8_t*>(sigw), 4);
+  return ok;
+}
+
 template <class Tail>
 __device__ __forceinline__ bool sum6kes_verify_wide(const uint32_t vk[8], uint32_t t,
                                                     const uint32_t* sigw, const Tail& msg,
                                                     uint32_t mlen, const uint16_t* bw) {
   uint32_t cur[8], sig[16];
-  const bool ok = sum6kes_walk(cur, sig, vk, t, sigw);
+  const bool ok = sum6kes_walk_wide(cur, sig, vk, t, sigw);
   const bool leaf = ed25519_verify_wide(sig, cur, msg, mlen, bw);
   return ok && leaf;
 }
@@ -158,6 +187,134 @@ __device__ __forceinline__ void vrf_sh(ge_p3& H, ge_p2& V, const uint32_t pk[8],
   TabW tab;
   tab_build(tab, pw_from_p3(H, L), d2_wide(L), L);
   V = pw_to_p2(pw_scalarmult(tab, s, L));
+}
+
+// ---- fused mode: each core encodes the points it makes ----------------------
+// canonical encoding of a p2 point (one inversion, on the lane: divsteps)
+__device__ __forceinline__ void encode_p2(uint32_t enc[8], const ge_p2& P) {
+  ge_encode_with_inv(enc, P.X, P.Y, fe_invert_vartime(P.Z));
+}
+
+// The whole V = [s]H - [c]Gamma on one wave: Elligator2's exponentiation on
+// rows 0/2 and Gamma's decode on rows 1/3 at once, then one chain over the
+// tables of H and -Gamma (s: 64 windows, c: 33).  H and V encoded with one
+// inversion.  (Gamma's acceptance checks are the Gamma core's.)
+template <class Tail>
+__device__ __forceinline__ void vrf_v_full_wide(uint32_t Henc[8], uint32_t Venc[8],
+                                                const uint32_t pk[8], const uint32_t pi[20],
+                                                const Tail& alpha) {
+  const Lanes L = lanes();
+  uint32_t G[8], c[8], s_raw[8], s[8];
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    G[k] = pi[k];
+    c[k] = k < 4 ? pi[8 + k] : 0u;
+    s_raw[k] = pi[12 + k];
+  }
+  sc_reduce256(s, s_raw);
+  uint32_t pre[9];
+  pre[0] = 0x04u | (0x01u << 8) | (pk[0] << 16);
+#pragma unroll
+  for (int k = 1; k < 8; k++) pre[k] = (pk[k - 1] >> 16) | (pk[k] << 16);
+  pre[8] = pk[7] >> 16;
+  uint64_t Hs[8];
+  sha512_prefixed<34>(Hs, pre, alpha, 32);
+  uint32_t rw[16];
+  sha512_digest_words(rw, Hs);
+  rw[7] &= 0x7fffffffu;
+  DecodePre dg;
+  const fe tg = ge_decode_pre(dg, G);
+  fe gpow;
+  const ge_p3 H = elligator2_h_with(rw, [&](const fe& z) {
+    const int32_t x = L.odd ? fe_to_fw(tg, L) : fe_to_fw(z, L);
+    const int32_t y = fw_pow22523(x);
+    gpow = fw_to_fe(y, 1);
+    return fw_to_fe(y, 0);
+  });
+  ge_p3 Gamma;
+  ge_decode_post(&Gamma, dg, gpow, G, false);
+  const int32_t d2 = d2_wide(L);
+  TabW tH, tG;
+  tab_build(tH, pw_from_p3(H, L), d2, L);
+  tab_build(tG, pw_from_p3(ge_p3_neg(Gamma), L), d2, L);
+  const ge_p2 V = pw_to_p2(pw_dsm<true, false>(tH, s, 64, tG, c, 33, s, nullptr, L));
+  const fe zz = fe_mul(H.Z, V.Z);
+  const fe inv = fe_invert_vartime(zz);
+  ge_encode_with_inv(Henc, H.X, H.Y, fe_mul(inv, V.Z));
+  ge_encode_with_inv(Venc, V.X, V.Y, fe_mul(inv, H.Z));
+}
+
+// The Gamma core: acceptance checks, [8]Gamma and beta = SHA-512(suite ||
+// 0x03 || encode([8]Gamma)); returns the flag word (with kFlagGammaX0)
+__device__ __forceinline__ int32_t vrf_gamma_beta_wide(uint32_t beta[16], const uint32_t pi[20]) {
+  const Lanes L = lanes();
+  uint32_t G[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) G[i] = pi[i];
+  ge_p3 Gamma;
+  bool ok = ge_is_canonical(G);
+  ok = ge_decode_wide(&Gamma, G, false) && ok;
+  const pw G8w = pw_dbl(pw_dbl(pw_dbl(pw_from_p3(Gamma, L), L), L), L);
+  uint32_t enc[8];
+  encode_p2(enc, pw_to_p2(G8w));
+  vrf_beta(beta, enc);
+  return (ok ? kFlagOk : 0) | (fe_iszero(Gamma.X) ? kFlagGammaX0 : 0);
+}
+
+// Arrival of one core of header i: this wave's record stores are released,
+// the header's counter bumped; true for the eighth core (then acquired).
+__device__ __forceinline__ bool arrive_last(int32_t* ctr) {
+  __threadfence();
+  uint32_t old = 0;
+  if ((threadIdx.x & 63u) == 0) old = atomicAdd(reinterpret_cast<unsigned int*>(ctr), 1u);
+  old = (uint32_t)__builtin_amdgcn_readlane((int)old, 0);
+  if (old != (uint32_t)kLatCores - 1) return false;
+  __threadfence();
+  return true;
+}
+
+// The tail of header i on the last core's wave: both VRFs at once (lanes
+// 0..31 the eta VRF, 32..63 the leader VRF) -- challenge check from the
+// record's encodings, beta, claimed-output bits, the eta nonce -- and the
+// verdict; the counter is reset for the next launch.  Same bits and outputs
+// as k_tpraos_finish (tpraos.h vrf_finish_split).
+__device__ __forceinline__ void hdr_tail_wide(const ouro_tpraos_batch& b, size_t i, uint32_t opts,
+                                              Slot res, uint8_t* verdict, uint8_t* beta_eta,
+                                              uint8_t* beta_leader) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const int which = (int)(lane >> 5);
+  auto fl = [&](int core) { return ldg1(res.word(kResFlags + core)); };
+  const int32_t fu = fl(which ? kCoreUl : kCoreUe), fv = fl(which ? kCoreVl : kCoreVe);
+  const int32_t fg = fl(which ? kCoreGl : kCoreGe);
+  uint32_t pi[20], Henc[8], Uenc[8], Venc[8], Genc[8], c[4], beta[16];
+  ld_words(pi, (which ? b.leader_proof : b.eta_proof) + 80 * i, 5);
+  ld_words8(Henc, res + kLatEnc + 8 * (3 * which + 0));
+  ld_words8(Uenc, res + kLatEnc + 8 * (3 * which + 1));
+  ld_words8(Venc, res + kLatEnc + 8 * (3 * which + 2));
+#pragma unroll
+  for (int k = 0; k < 8; k++) Genc[k] = pi[k];
+  if (fg & kFlagGammaX0) Genc[7] &= 0x7fffffffu;
+#pragma unroll
+  for (int k = 0; k < 4; k++) c[k] = pi[8 + k];
+  const bool ceq = vrf_challenge_ok(Henc, Genc, Uenc, Venc, c);
+  const bool ok = (fu & fv & fg & kFlagOk) && ceq;
+  ld_words8(beta, res + kLatBeta + 16 * which);
+  ld_words8(beta + 8, res + kLatBeta + 16 * which + 8);
+#pragma unroll
+  for (int k = 0; k < 16; k++) beta[k] = ok ? beta[k] : 0u;
+  uint32_t bit = ok ? (which ? 0x08u : 0x04u) : 0u;
+  bit |= hdr_claim_bit(b, i, opts, which, ok, beta);
+  uint8_t* dst = which ? beta_leader : beta_eta;
+  if ((lane & 31u) == 0 && dst) st_words(dst + 64 * i, beta, 4);
+  if (lane == 0) hdr_eta_nonce(b, i, opts, beta);
+  const uint32_t other = (uint32_t)__builtin_amdgcn_readlane((int)bit, 32);
+  if (lane == 0) {
+    uint32_t v = bit | other;
+    if (fl(kCoreOcert) & kFlagOk) v |= 0x01u;
+    if (fl(kCoreKes) & kFlagOk) v |= 0x02u;
+    verdict[i] = (uint8_t)v;
+    stg1(res.word(kLatCtr), 0);
+  }
 }
 
 }  // namespace wide

@@ -65,11 +65,20 @@ def test_throughput_paths(gpu_lib, kats, monkeypatch, chunk):
     assert list(v[:6]) == [0x3F, 0x3F, 0x03, 0x2B, 0x1F, 0x2F]
 
 
-@pytest.mark.parametrize("quad", ["1", "0"], ids=["lane_quads", "one_lane"])
-def test_latency_paths(gpu_lib, kats, monkeypatch, quad):
+LAT_FORMS = {
+    "wide_fused": {},
+    "wide_finish_launch": {"OURO_LAT_FUSE": "0"},
+    "lane_quads": {"OURO_LAT_WIDE": "0", "OURO_LAT_QUAD": "1"},
+    "one_lane": {"OURO_LAT_WIDE": "0", "OURO_LAT_QUAD": "0"},
+}
+
+
+@pytest.mark.parametrize("form", list(LAT_FORMS))
+def test_latency_paths(gpu_lib, kats, monkeypatch, form):
     from ouroboros_network_amd.tpraos import HeaderPlan, verify_headers_lowlat
 
-    monkeypatch.setenv("OURO_LAT_QUAD", quad)
+    for k, v in LAT_FORMS[form].items():
+        monkeypatch.setenv(k, v)
     cases = _cases(kats)
     for name, batch in cases.items():
         want = _oracle(batch)

@@ -221,15 +221,25 @@ def _golden_variants(kats):
     return HC.golden_variants(kats, stride=1)
 
 
-@pytest.mark.parametrize("quad", ["1", "0"], ids=["lane_quads", "one_lane"])
-def test_lowlat_equals_throughput_and_oracle(gpu_lib, kats, monkeypatch, quad):
-    """Latency mode (eight cores per header + finish launch; each core on a
-    DPP lane quad that splits every group operation's products, or on one
-    lane) gives the same verdict bits and outputs as the throughput kernel and
-    the oracle."""
+LAT_FORMS = {
+    "wide_fused": {},  # default: every core on one wave, the last core finishes
+    "wide_finish_launch": {"OURO_LAT_FUSE": "0"},
+    "lane_quads": {"OURO_LAT_WIDE": "0", "OURO_LAT_QUAD": "1"},
+    "one_lane": {"OURO_LAT_WIDE": "0", "OURO_LAT_QUAD": "0"},
+}
+
+
+@pytest.mark.parametrize("form", list(LAT_FORMS))
+def test_lowlat_equals_throughput_and_oracle(gpu_lib, kats, monkeypatch, form):
+    """Latency mode (eight cores per header: each on one wave with wave-wide
+    field arithmetic, its last core finishing the header -- or with a finish
+    launch -- or each on a DPP lane quad that splits every group operation's
+    products, or on one lane) gives the same verdict bits and outputs as the
+    throughput kernel and the oracle."""
     from ouroboros_network_amd.tpraos import verify_headers, verify_headers_lowlat
 
-    monkeypatch.setenv("OURO_LAT_QUAD", quad)
+    for k, v in LAT_FORMS[form].items():
+        monkeypatch.setenv(k, v)
 
     batch = _golden_variants(kats)
     wv, wbe, wbl = O.tpraos_verify_batch(batch)
