@@ -487,7 +487,11 @@ int launch_lowlat(hipStream_t st, const ouro_tpraos_batch& b, const uint32_t* d_
   // workgroups) ahead of the other cores' lanes
   const int wmask = lat_wide_mask();
   const int nwide = __builtin_popcount((unsigned)wmask);
-  const size_t wide_waves = (size_t)nwide * n_cap;
+  // fused (all eight cores wide): the last core of a header finishes it, no
+  // second launch (OURO_LAT_FUSE=0 keeps the finish launch, for A/B); its
+  // two Ed25519 checks take two waves each (kernels_lat.hip kFusedItems)
+  const bool fused = wmask == 0xff && lat_fuse();
+  const size_t wide_waves = (size_t)(fused ? kLatCores + 2 : nwide) * n_cap;
   const size_t wide_blocks = (wide_waves * 64 + blk - 1) / blk;
   const size_t quad_items = (size_t)(kLatCores - nwide) * n_cap;
   const int g1 = (int)wide_blocks + grid(quad_items << (quad ? 2 : 0), kCores);
@@ -495,9 +499,6 @@ int launch_lowlat(hipStream_t st, const ouro_tpraos_batch& b, const uint32_t* d_
   // timing probe: OURO_LAT_SKIP = mask of cores left out (verdicts then wrong)
   const char* skip_env = getenv("OURO_LAT_SKIP");
   const int skip = skip_env ? (int)(strtol(skip_env, nullptr, 0) & 0xff) : 0;
-  // fused (all eight cores wide): the last core of a header finishes it, no
-  // second launch (OURO_LAT_FUSE=0 keeps the finish launch, for A/B)
-  const bool fused = wmask == 0xff && lat_fuse();
   hipLaunchKernelGGL(k_tpraos_cores, dim3(g1), dim3(blk), 0, st, b, d_n, res_buf, scratch,
                      ds->btab, quad | (skip << 8) | (wmask << 16) | (fused ? 1 << 24 : 0),
                      (int)(wide_blocks * blk / 64), verdict, be, bl);

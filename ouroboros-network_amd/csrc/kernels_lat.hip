@@ -122,6 +122,61 @@ __device__ __noinline__ void hdr_core_wide(const ouro_tpraos_batch& b, size_t i,
 #endif
 }
 
+// Fused mode: ten items per header -- the eight cores, with the OCERT and
+// KES Ed25519 checks each split into a points item (0 / 1) and a scalars
+// item (8 / 9) whose second to arrive runs the chain (wide_cores.h ed_*).
+// Every finished core arrives at the header's counter; the eighth runs the
+// finish (hdr_tail_wide).  skip: the timing probe's mask (cores 0..7).
+constexpr int kFusedItems = kLatCores + 2;
+__device__ __noinline__ void hdr_item_fused(const ouro_tpraos_batch& b, size_t i, uint32_t opts,
+                                            int item, Slot res, const uint16_t* bw, uint32_t skip,
+                                            uint8_t* verdict, uint8_t* beta_eta,
+                                            uint8_t* beta_leader) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  using namespace wide;
+  const bool lead = (threadIdx.x & 63u) == 0;
+  if (item == kCoreOcert || item == kCoreKes || item >= kLatCores) {
+    const int e = item >= kLatCores ? item - kLatCores : item;  // 0 OCERT, 1 KES
+    const bool scal = item >= kLatCores;
+    const Slot ed = res + kLatEd + kEdWords * e;
+    const bool skipped = (skip >> e) & 1u;
+    if (!skipped && e == 0) {
+      uint32_t s[16], p[8], hv[8];
+      ld_words(s, b.ocert_sigma + 64 * i, 4);
+      ld_words(p, b.issuer_vk + 32 * i, 2);
+      ld_words(hv, b.hot_vk + 32 * i, 2);
+      if (scal) {
+        OcertMsg m;
+        ocert_msg(m, hv, b.ocert_counter[i], b.ocert_kes_period[i]);
+        ed_scalars_item(ed, s, p, m, 48);
+      } else {
+        ed_points_item(ed, s, p, true);
+      }
+    } else if (!skipped) {
+      uint32_t hv[8], cur[8], sig[16];
+      ld_words(hv, b.hot_vk + 32 * i, 2);
+      const uint32_t* sw = reinterpret_cast<const uint32_t*>(b.kes_sig + 448 * i);
+      const bool walk_ok = sum6kes_walk_wide(cur, sig, hv, b.kes_t[i], sw);
+      if (scal)
+        ed_scalars_item(ed, sig, cur, ShaGlobalTail{b.body + b.body_off[i]}, b.body_len[i]);
+      else
+        ed_points_item(ed, sig, cur, walk_ok);
+    }
+    if (!arrive_last(ed.word(125), 2)) return;
+    int32_t flag = 0;
+    if (skipped) {
+      if (lead) stg1(ed.word(125), 0);
+    } else {
+      flag = ed_chain(ed, bw) ? kFlagOk : 0;
+    }
+    if (lead) stg1(res.word(kResFlags + e), flag);
+  } else if (!((skip >> item) & 1u)) {
+    hdr_core_wide(b, i, opts, item, res, bw, true);
+  }
+  if (arrive_last(res.word(kLatCtr))) hdr_tail_wide(b, i, opts, res, verdict, beta_eta, beta_leader);
+#endif
+}
+
 // the k-th set bit of m (k < popcount(m))
 __device__ __forceinline__ int nth_set_bit(uint32_t m, int k) {
   for (int c = 0; c < 8; c++) {
@@ -141,10 +196,11 @@ __device__ __forceinline__ int nth_clear_bit(uint32_t m, int k) { return nth_set
 // ge25519.h) or one lane each; bits 8..15: cores to skip (a timing probe,
 // OURO_LAT_SKIP; the verdicts are then wrong); bits 16..23: the cores run on
 // one wave each (wide_cores.h, OURO_LAT_WIDE); bit 24 (all eight wide): the
-// fused form -- each core encodes its points, the header's last core to
-// arrive runs the finish (hdr_tail_wide), and there is no second launch.  The first wide_waves waves of
+// fused form -- ten items per header (hdr_item_fused), each core encodes its
+// points, the header's last core to arrive runs the finish (hdr_tail_wide),
+// and there is no second launch.  The first wide_waves waves of
 // the grid run the wide items (wave w: core number w % nwide of header
-// w / nwide), the lanes after them the other cores (work item c * n + i:
+// w / nwide; fused: item w % 10 of header w / 10), the lanes after them the other cores (work item c * n + i:
 // core number c of header i, so each wave runs one core type).  n (d_n[0])
 // and the batch's optional members (d_n[1], tpraos.h kOpt*) are read from
 // device memory so a captured graph serves any batch of n <= capacity.
@@ -165,18 +221,20 @@ __global__ void __launch_bounds__(kBlock, OURO_WAVES) k_tpraos_cores(ouro_tpraos
   const bool fused = ((uint32_t)mode >> 24) & 1u;
   const size_t gtid = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   const size_t wide_lanes = (size_t)wide_waves * 64;
+  if (gtid < wide_lanes && fused) {  // wave-uniform
+    const size_t wv = gtid >> 6, i = wv / kFusedItems;
+    if (i < n)
+      hdr_item_fused(b, i, opts, (int)(wv % kFusedItems), slot_of(res_buf, i, kLatResWords),
+                     reinterpret_cast<const uint16_t*>(btab + kBTabWords), skip, verdict,
+                     beta_eta, beta_leader);
+    return;
+  }
   if (gtid < wide_lanes) {  // wave-uniform
     const size_t wv = gtid >> 6, i = wv / nwide;
     const int core = nth_set_bit(wmask, (int)(wv % nwide));
-    if (i >= n) return;
-    const Slot res = slot_of(res_buf, i, kLatResWords);
-    if (!((skip >> core) & 1u))
-      hdr_core_wide(b, i, opts, core, res, reinterpret_cast<const uint16_t*>(btab + kBTabWords),
-                    fused);
-#if defined(__HIP_DEVICE_COMPILE__)
-    if (fused && wide::arrive_last(res.word(kLatCtr)))
-      wide::hdr_tail_wide(b, i, opts, res, verdict, beta_eta, beta_leader);
-#endif
+    if (i < n && !((skip >> core) & 1u))
+      hdr_core_wide(b, i, opts, core, slot_of(res_buf, i, kLatResWords),
+                    reinterpret_cast<const uint16_t*>(btab + kBTabWords), false);
     return;
   }
   const int sh = quad ? 2 : 0;

@@ -36,7 +36,11 @@ constexpr int kLatPart = kResWords;
 constexpr int kLatEnc = kLatPart + 2 * kPtWords;      // enc(which, k) at kLatEnc + 8 (3 which + k)
 constexpr int kLatBeta = kLatEnc + 48;                // beta(which) at kLatBeta + 16 which
 constexpr int kLatCtr = kLatBeta + 32;
-constexpr int kLatResWords = kLatCtr + 4;             // 452 words (16-B multiple)
+// fused mode, each Ed25519 check (OCERT, KES leaf) split over two waves
+// (wide_cores.h): its scalars, decoded points and arrival counter
+constexpr int kLatEd = kLatCtr + 4;                   // Ed record e at kLatEd + kEdWords e
+constexpr int kEdWords = 128;
+constexpr int kLatResWords = kLatEd + 2 * kEdWords;   // 708 words (16-B multiple)
 enum HdrCore { kCoreOcert = 0, kCoreKes, kCoreUe, kCoreUl, kCoreVe, kCoreVl, kHdrCores,
                // latency mode splits each V = [s]H - [c]Gamma over two lanes: the V
                // cores do [s]H (252-bit chain), these do -[c]Gamma (128-bit chain)

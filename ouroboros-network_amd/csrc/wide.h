@@ -169,7 +169,9 @@ __device__ __forceinline__ int32_t fw_sqn(int32_t t, int n, const Lanes& L) {
   for (int i = 0; i < n; i++) t = fw_sq(t, L);
   return t;
 }
-__device__ __noinline__ int32_t fw_pow22523(int32_t z) {
+// z^(2^252 - 3) (mode 1: the square-root helper) or z^(p - 2) (mode 0: the
+// inversion), fe25519.h fe_pow_chain's addition chain
+__device__ __noinline__ int32_t fw_pow_chain(int32_t z, int mode) {
   const Lanes L = lanes();
   const int32_t z2 = fw_sq(z, L);
   int32_t t = fw_sqn(z2, 2, L);
@@ -184,8 +186,10 @@ __device__ __noinline__ int32_t fw_pow22523(int32_t z) {
   const int32_t z100 = fw_mul(fw_sqn(z50, 50, L), z50, L);
   t = fw_mul(fw_sqn(z100, 100, L), z100, L);              // 2^200 - 1
   const int32_t z250 = fw_mul(fw_sqn(t, 50, L), z50, L);
-  return fw_mul(fw_sqn(z250, 2, L), z, L);                // 2^252 - 3
+  return fw_mul(fw_sqn(z250, mode ? 2 : 5, L), mode ? z : z11, L);  // 2^252 - 3 | 2^255 - 21
 }
+__device__ __forceinline__ int32_t fw_pow22523(int32_t z) { return fw_pow_chain(z, 1); }
+__device__ __forceinline__ int32_t fw_invert(int32_t z) { return fw_pow_chain(z, 0); }
 
 // ---- group operations ----------------------------------------------------------
 struct pw { int32_t X, Y, Z, T; };  // extended point, coordinates replicated

@@ -190,9 +190,18 @@ __device__ __forceinline__ void vrf_sh(ge_p3& H, ge_p2& V, const uint32_t pk[8],
 }
 
 // ---- fused mode: each core encodes the points it makes ----------------------
-// canonical encoding of a p2 point (one inversion, on the lane: divsteps)
+// Z^-1 on the wave (z^(p-2): ~265 wave-wide products, 12 us less than the
+// lane's divsteps inversion, OURO_WIDE_INV=0)
+#ifndef OURO_WIDE_INV
+#define OURO_WIDE_INV 1
+#endif
+__device__ __forceinline__ fe invert_wide(const fe& z) {
+  if (OURO_WIDE_INV) return fw_to_fe(fw_invert(fe_to_fw(z, lanes())));
+  return fe_invert_vartime(z);
+}
+// canonical encoding of a p2 point (one inversion)
 __device__ __forceinline__ void encode_p2(uint32_t enc[8], const ge_p2& P) {
-  ge_encode_with_inv(enc, P.X, P.Y, fe_invert_vartime(P.Z));
+  ge_encode_with_inv(enc, P.X, P.Y, invert_wide(P.Z));
 }
 
 // The whole V = [s]H - [c]Gamma on one wave: Elligator2's exponentiation on
@@ -239,7 +248,7 @@ __device__ __forceinline__ void vrf_v_full_wide(uint32_t Henc[8], uint32_t Venc[
   tab_build(tG, pw_from_p3(ge_p3_neg(Gamma), L), d2, L);
   const ge_p2 V = pw_to_p2(pw_dsm<true, false>(tH, s, 64, tG, c, 33, s, nullptr, L));
   const fe zz = fe_mul(H.Z, V.Z);
-  const fe inv = fe_invert_vartime(zz);
+  const fe inv = invert_wide(zz);
   ge_encode_with_inv(Henc, H.X, H.Y, fe_mul(inv, V.Z));
   ge_encode_with_inv(Venc, V.X, V.Y, fe_mul(inv, H.Z));
 }
@@ -261,16 +270,88 @@ __device__ __forceinline__ int32_t vrf_gamma_beta_wide(uint32_t beta[16], const 
   return (ok ? kFlagOk : 0) | (fe_iszero(Gamma.X) ? kFlagGammaX0 : 0);
 }
 
-// Arrival of one core of header i: this wave's record stores are released,
-// the header's counter bumped; true for the eighth core (then acquired).
-__device__ __forceinline__ bool arrive_last(int32_t* ctr) {
+// Arrival at a counter of `parties` waves: this wave's record stores are
+// released, the counter bumped; true for the last party (then acquired).
+__device__ __forceinline__ bool arrive_last(int32_t* ctr, uint32_t parties = kLatCores) {
   __threadfence();
   uint32_t old = 0;
   if ((threadIdx.x & 63u) == 0) old = atomicAdd(reinterpret_cast<unsigned int*>(ctr), 1u);
   old = (uint32_t)__builtin_amdgcn_readlane((int)old, 0);
-  if (old != (uint32_t)kLatCores - 1) return false;
+  if (old != parties - 1) return false;
   __threadfence();
   return true;
+}
+
+// ---- fused mode: an Ed25519 check over two waves ------------------------------
+// The points item (encoding checks, both decodes: one exponentiation time) and
+// the scalars item (SHA-512 of R || A || M -- five blocks for a KES body --,
+// reduction, the lattice pair, b = c1 S) run at once; the second to arrive
+// builds the tables and runs the chain (ed_chain).  Record words (Slot e):
+// c0 0, c1 8, b 16, nw 24, c0_neg 25 | -A 28 (X, Y, Z, T at 12-word stride),
+// -R 76, points ok 124, counter 125.
+__device__ __forceinline__ void ed_points_item(Slot e, const uint32_t sig[16],
+                                               const uint32_t pk[8], bool extra_ok) {
+  uint32_t R[8], S[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    R[i] = sig[i];
+    S[i] = sig[8 + i];
+  }
+  bool ok = ed25519_precheck(R, S, pk, false) && extra_ok;
+  ge_p3 negA, negR;
+  bool okA, okR;
+  ge_decode_pair_wide(&negA, &okA, &negR, &okR, pk, R, true);
+  ok = okA && ok;
+  ok = ge_is_canonical(R) && ok;
+  ok = okR && ok;
+  ok = ok && !(fe_iszero(negR.X) && (R[7] >> 31) != 0);
+  if ((threadIdx.x & 63u) == 0) {
+    st_fe(e + 28, negA.X); st_fe(e + 40, negA.Y); st_fe(e + 52, negA.Z); st_fe(e + 64, negA.T);
+    st_fe(e + 76, negR.X); st_fe(e + 88, negR.Y); st_fe(e + 100, negR.Z); st_fe(e + 112, negR.T);
+    stg1(e.word(124), ok ? 1 : 0);
+  }
+}
+template <class Tail>
+__device__ __forceinline__ void ed_scalars_item(Slot e, const uint32_t sig[16], const uint32_t pk[8],
+                                                const Tail& msg, uint32_t mlen) {
+  uint32_t R[8], S[8], b[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    R[i] = sig[i];
+    S[i] = sig[8 + i];
+  }
+  HalfScalars hs;
+  ed25519_scalars(hs, b, R, S, pk, msg, mlen);
+  int nw = (hs.bits + 4) >> 2;
+  nw = nw < 1 ? 1 : (nw > 64 ? 64 : nw);
+  if ((threadIdx.x & 63u) == 0) {
+    st_words8(e + 0, hs.c0);
+    st_words8(e + 8, hs.c1);
+    st_words8(e + 16, b);
+    stg1(e.word(24), nw);
+    stg1(e.word(25), hs.c0_neg ? 1 : 0);
+  }
+}
+// [|c0|](+-A) + [c1](-R) + [b]B == O from the record (the ed25519_verify_wide
+// equation); resets the counter
+__device__ __forceinline__ bool ed_chain(Slot e, const uint16_t* bw) {
+  const Lanes L = lanes();
+  uint32_t c0[8], c1[8], b[8];
+  ld_words8(c0, e + 0);
+  ld_words8(c1, e + 8);
+  ld_words8(b, e + 16);
+  const int nw = ldg1(e.word(24));
+  const bool c0_neg = ldg1(e.word(25)) != 0;
+  const ge_p3 negA{ld_fe(e + 28), ld_fe(e + 40), ld_fe(e + 52), ld_fe(e + 64)};
+  const ge_p3 negR{ld_fe(e + 76), ld_fe(e + 88), ld_fe(e + 100), ld_fe(e + 112)};
+  const bool ok = ldg1(e.word(124)) != 0;
+  if ((threadIdx.x & 63u) == 0) stg1(e.word(125), 0);
+  const int32_t d2 = d2_wide(L);
+  TabW t1, t2;
+  tab_build(t1, pw_from_p3(c0_neg ? ge_p3_neg(negA) : negA, L), d2, L);
+  tab_build(t2, pw_from_p3(negR, L), d2, L);
+  const pw Q = pw_dsm<true, true>(t1, c0, nw, t2, c1, nw, b, bw, L);
+  return ok && pw_is_identity(Q);
 }
 
 // The tail of header i on the last core's wave: both VRFs at once (lanes

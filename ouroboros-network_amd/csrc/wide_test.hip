@@ -105,7 +105,9 @@ __global__ void __launch_bounds__(WT_BOUNDS) k_wide_selftest(uint64_t seed, int3
   }
   res[2] = ok && same_fe(fw_to_fe(sq), sq_ref);
   // 3: z^(2^252 - 3)
-  res[3] = same_fe(fw_to_fe(fw_pow22523(fe_to_fw(a, L))), fe_pow22523(a));
+  // (and z^(p - 2), the wave-wide inversion)
+  res[3] = same_fe(fw_to_fe(fw_pow22523(fe_to_fw(a, L))), fe_pow22523(a)) &&
+           same_fe(fw_to_fe(fw_invert(fe_to_fw(b, L))), fe_invert(b));
   // points: Elligator2 images
   const ge_p3 P = elligator2_h(wa), Q = elligator2_h(wb);
   const pw Pw = pw_from_p3(P, L), Qw = pw_from_p3(Q, L);
