@@ -500,7 +500,8 @@ int launch_lowlat(hipStream_t st, const ouro_tpraos_batch& b, const uint32_t* d_
   const char* skip_env = getenv("OURO_LAT_SKIP");
   const int skip = skip_env ? (int)(strtol(skip_env, nullptr, 0) & 0xff) : 0;
   hipLaunchKernelGGL(k_tpraos_cores, dim3(g1), dim3(blk), 0, st, b, d_n, res_buf, scratch,
-                     ds->btab, quad | (skip << 8) | (wmask << 16) | (fused ? 1 << 24 : 0),
+                     ds->btab, quad | (skip << 8) | (wmask << 16) | (fused ? 1 << 24 : 0) |
+                                   (getenv("OURO_LAT_STAMPS") ? 1 << 25 : 0),
                      (int)(wide_blocks * blk / 64), verdict, be, bl);
   if ((rc = launch_check())) return rc;
   if (fused) return OURO_OK;

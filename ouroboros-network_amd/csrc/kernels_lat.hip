@@ -128,13 +128,21 @@ __device__ __noinline__ void hdr_core_wide(const ouro_tpraos_batch& b, size_t i,
 // Every finished core arrives at the header's counter; the eighth runs the
 // finish (hdr_tail_wide).  skip: the timing probe's mask (cores 0..7).
 constexpr int kFusedItems = kLatCores + 2;
+// stamps (OURO_LAT_STAMPS=1, a timing probe): header 0's items print their
+// start / end times (s_memrealtime, 100 MHz) and the tail's end.
 __device__ __noinline__ void hdr_item_fused(const ouro_tpraos_batch& b, size_t i, uint32_t opts,
                                             int item, Slot res, const uint16_t* bw, uint32_t skip,
                                             uint8_t* verdict, uint8_t* beta_eta,
-                                            uint8_t* beta_leader) {
+                                            uint8_t* beta_leader, bool stamps) {
 #if defined(__HIP_DEVICE_COMPILE__)
   using namespace wide;
   const bool lead = (threadIdx.x & 63u) == 0;
+  const uint64_t t0 = stamps ? __builtin_amdgcn_s_memrealtime() : 0;
+  auto stamp = [&](const char* what) {
+    if (stamps && lead && i == 0)
+      printf("stamp %d %s %llu %llu\n", item, what, (unsigned long long)t0,
+             (unsigned long long)__builtin_amdgcn_s_memrealtime());
+  };
   if (item == kCoreOcert || item == kCoreKes || item >= kLatCores) {
     const int e = item >= kLatCores ? item - kLatCores : item;  // 0 OCERT, 1 KES
     const bool scal = item >= kLatCores;
@@ -162,7 +170,10 @@ __device__ __noinline__ void hdr_item_fused(const ouro_tpraos_batch& b, size_t i
       else
         ed_points_item(ed, sig, cur, walk_ok);
     }
-    if (!arrive_last(ed.word(125), 2)) return;
+    if (!arrive_last(ed.word(125), 2)) {
+      stamp("half");
+      return;
+    }
     int32_t flag = 0;
     if (skipped) {
       if (lead) stg1(ed.word(125), 0);
@@ -173,7 +184,11 @@ __device__ __noinline__ void hdr_item_fused(const ouro_tpraos_batch& b, size_t i
   } else if (!((skip >> item) & 1u)) {
     hdr_core_wide(b, i, opts, item, res, bw, true);
   }
-  if (arrive_last(res.word(kLatCtr))) hdr_tail_wide(b, i, opts, res, verdict, beta_eta, beta_leader);
+  stamp("core");
+  if (arrive_last(res.word(kLatCtr))) {
+    hdr_tail_wide(b, i, opts, res, verdict, beta_eta, beta_leader);
+    stamp("tail");
+  }
 #endif
 }
 
@@ -226,7 +241,7 @@ __global__ void __launch_bounds__(kBlock, OURO_WAVES) k_tpraos_cores(ouro_tpraos
     if (i < n)
       hdr_item_fused(b, i, opts, (int)(wv % kFusedItems), slot_of(res_buf, i, kLatResWords),
                      reinterpret_cast<const uint16_t*>(btab + kBTabWords), skip, verdict,
-                     beta_eta, beta_leader);
+                     beta_eta, beta_leader, ((uint32_t)mode >> 25) & 1u);
     return;
   }
   if (gtid < wide_lanes) {  // wave-uniform

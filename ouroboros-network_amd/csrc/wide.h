@@ -115,6 +115,39 @@ __device__ __forceinline__ int32_t sel4(int32_t a0, int32_t a1, int32_t a2, int3
   return L.high ? hi : lo;
 }
 
+// f * g for REPLICATED f, g (every row the same element): the sixteen steps
+// split over the four rows (row r takes steps 4r..4r+3, its operands rotated
+// into place by 4r lanes first), the rows' accumulators summed across rows
+// with permlane swaps, one carry: ~43 instructions instead of ~62 -- for the
+// exponentiation chains, whose operands are replicated.
+__device__ __forceinline__ int64_t add_rows_u64(int64_t a) {
+  const uint32_t lo = (uint32_t)a, hi = (uint32_t)((uint64_t)a >> 32);
+  const auto l1 = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+  const auto h1 = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+  const uint64_t s = ((uint64_t)h1[0] << 32 | l1[0]) + ((uint64_t)h1[1] << 32 | l1[1]);
+  const uint32_t slo = (uint32_t)s, shi = (uint32_t)(s >> 32);
+  const auto l2 = __builtin_amdgcn_permlane32_swap(slo, slo, false, false);
+  const auto h2 = __builtin_amdgcn_permlane32_swap(shi, shi, false, false);
+  return (int64_t)(((uint64_t)h2[0] << 32 | l2[0]) + ((uint64_t)h2[1] << 32 | l2[1]));
+}
+__device__ __forceinline__ int32_t fw_mul_rep(int32_t f, int32_t g, const Lanes& L) {
+  const int j = L.j;
+  // f' lane k = f_(4r + k); G lane j = g_(j - 4r) (x 38 where it wrapped)
+  const int32_t fr = sel4(f, dpp<0x12c>(f), dpp<0x128>(f), dpp<0x124>(f), L);  // ror 12 / 8 / 4
+  const int32_t g4 = s24(dpp<0x124>(g)) * (j < 4 ? 38 : 1);
+  const int32_t g8 = s24(dpp<0x128>(g)) * (j < 8 ? 38 : 1);
+  const int32_t g12 = s24(dpp<0x12c>(g)) * (j < 12 ? 38 : 1);
+  int32_t G = sel4(g, g4, g8, g12, L);
+  int64_t acc = (int64_t)bcast<0>(fr) * G;
+  G = s24(ror1(G)) * s24(L.fac);
+  acc += (int64_t)bcast<1>(fr) * G;
+  G = s24(ror1(G)) * s24(L.fac);
+  acc += (int64_t)bcast<2>(fr) * G;
+  G = s24(ror1(G)) * s24(L.fac);
+  acc += (int64_t)bcast<3>(fr) * G;
+  return fw_carry(add_rows_u64(acc), L.fac);
+}
+
 // ---- conversions -------------------------------------------------------------
 // lane-local fe (same value in every lane) -> replicated fw
 __device__ __forceinline__ int32_t fe_to_fw(const fe& f, const Lanes& L) {
@@ -163,16 +196,29 @@ __device__ __forceinline__ fe fw_to_fe(int32_t x, int row = 0) {
 
 __device__ __forceinline__ int32_t fw_one(const Lanes& L) { return L.j == 0 ? 1 : 0; }
 
-// ---- exponentiation (Elligator2's z^(2^252 - 3)), replicated operands -------
+// ---- exponentiations -------------------------------------------------------------
+#ifndef OURO_FW_REP
+#define OURO_FW_REP 1  // A/B switch: replicated chains with the row-split product
+#endif
+template <bool kRep>
+__device__ __forceinline__ int32_t fw_mul_t(int32_t f, int32_t g, const Lanes& L) {
+  return (kRep && OURO_FW_REP) ? fw_mul_rep(f, g, L) : fw_mul(f, g, L);
+}
+template <bool kRep>
 __device__ __forceinline__ int32_t fw_sqn(int32_t t, int n, const Lanes& L) {
 #pragma unroll 1
-  for (int i = 0; i < n; i++) t = fw_sq(t, L);
+  for (int i = 0; i < n; i++) t = fw_mul_t<kRep>(t, t, L);
   return t;
 }
 // z^(2^252 - 3) (mode 1: the square-root helper) or z^(p - 2) (mode 0: the
-// inversion), fe25519.h fe_pow_chain's addition chain
+// inversion), fe25519.h fe_pow_chain's addition chain.  kRep: z replicated
+// (one chain on the wave, row-split products); else each row its own chain.
+template <bool kRep>
 __device__ __noinline__ int32_t fw_pow_chain(int32_t z, int mode) {
   const Lanes L = lanes();
+#define fw_mul(a, b, l) fw_mul_t<kRep>(a, b, l)
+#define fw_sq(a, l) fw_mul_t<kRep>(a, a, l)
+#define fw_sqn fw_sqn<kRep>
   const int32_t z2 = fw_sq(z, L);
   int32_t t = fw_sqn(z2, 2, L);
   const int32_t z9 = fw_mul(t, z, L);
@@ -187,9 +233,15 @@ __device__ __noinline__ int32_t fw_pow_chain(int32_t z, int mode) {
   t = fw_mul(fw_sqn(z100, 100, L), z100, L);              // 2^200 - 1
   const int32_t z250 = fw_mul(fw_sqn(t, 50, L), z50, L);
   return fw_mul(fw_sqn(z250, mode ? 2 : 5, L), mode ? z : z11, L);  // 2^252 - 3 | 2^255 - 21
+#undef fw_mul
+#undef fw_sq
+#undef fw_sqn
 }
-__device__ __forceinline__ int32_t fw_pow22523(int32_t z) { return fw_pow_chain(z, 1); }
-__device__ __forceinline__ int32_t fw_invert(int32_t z) { return fw_pow_chain(z, 0); }
+// rows independent (e.g. two decodes at once)
+__device__ __forceinline__ int32_t fw_pow22523_rows(int32_t z) { return fw_pow_chain<false>(z, 1); }
+// z replicated in every row
+__device__ __forceinline__ int32_t fw_pow22523(int32_t z) { return fw_pow_chain<true>(z, 1); }
+__device__ __forceinline__ int32_t fw_invert(int32_t z) { return fw_pow_chain<true>(z, 0); }
 
 // ---- group operations ----------------------------------------------------------
 struct pw { int32_t X, Y, Z, T; };  // extended point, coordinates replicated

@@ -33,7 +33,7 @@ __device__ __forceinline__ void ge_decode_pair_wide(ge_p3* a, bool* oka, ge_p3* 
   DecodePre da, db;
   const fe ta = ge_decode_pre(da, sa), tb = ge_decode_pre(db, sb);
   const int32_t x = L.odd ? fe_to_fw(tb, L) : fe_to_fw(ta, L);
-  const int32_t y = fw_pow22523(x);
+  const int32_t y = fw_pow22523_rows(x);
   *oka = ge_decode_post(a, da, fw_to_fe(y, 0), sa, negate);
   *okb = ge_decode_post(b, db, fw_to_fe(y, 1), sb, negate);
 }
@@ -236,7 +236,7 @@ __device__ __forceinline__ void vrf_v_full_wide(uint32_t Henc[8], uint32_t Venc[
   fe gpow;
   const ge_p3 H = elligator2_h_with(rw, [&](const fe& z) {
     const int32_t x = L.odd ? fe_to_fw(tg, L) : fe_to_fw(z, L);
-    const int32_t y = fw_pow22523(x);
+    const int32_t y = fw_pow22523_rows(x);
     gpow = fw_to_fe(y, 1);
     return fw_to_fe(y, 0);
   });
