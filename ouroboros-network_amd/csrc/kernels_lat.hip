@@ -20,6 +20,13 @@
 
 #include "wide_cores.h"
 
+// A/B switch: 1 = the V core computes the whole V = [s]H - [c]Gamma (Gamma
+// decoded on its other rows); 0 = -[c]Gamma on the Gamma core and the second
+// of the two to arrive combines (the default: the V core is the critical item)
+#ifndef OURO_V_WHOLE
+#define OURO_V_WHOLE 0
+#endif
+
 using namespace ouro;
 
 // One core of header i on one wave (wide_cores.h): the same checks and the
@@ -76,7 +83,7 @@ __device__ __noinline__ void hdr_core_wide(const ouro_tpraos_batch& b, size_t i,
       ld_words(pi, (leader ? b.leader_proof : b.eta_proof) + 80 * i, 5);
       SeedMsg alpha;
       hdr_seed(alpha, b, i, leader, opts);
-      if (fused) {
+      if (fused && OURO_V_WHOLE) {
         uint32_t Henc[8], Venc[8];
         vrf_v_full_wide(Henc, Venc, p, pi, alpha);
         if (lead) {
@@ -86,6 +93,8 @@ __device__ __noinline__ void hdr_core_wide(const ouro_tpraos_batch& b, size_t i,
         flag = kFlagOk;
         break;
       }
+      // (fused, split V: H and [s]H to the record; vrf_combine_encode adds
+      // the Gamma core's -[c]Gamma)
       ge_p3 H;
       ge_p2 V;
       vrf_sh(H, V, p, pi, alpha);
@@ -101,10 +110,13 @@ __device__ __noinline__ void hdr_core_wide(const ouro_tpraos_batch& b, size_t i,
       ld_words(pi, (leader ? b.leader_proof : b.eta_proof) + 80 * i, 5);
       if (fused) {
         uint32_t beta[16];
-        flag = vrf_gamma_beta_wide(beta, pi);
+        ge_p2 part;
+        flag = vrf_gamma_beta_wide(beta, part, pi);
         if (lead) {
           st_words8(res + kLatBeta + 16 * (int)leader, beta);
           st_words8(res + kLatBeta + 16 * (int)leader + 8, beta + 8);
+          if (!OURO_V_WHOLE)
+            st_point_at(res + kLatPart + (leader ? kPtWords : 0), part.X, part.Y, part.Z);
         }
         break;
       }
@@ -181,8 +193,20 @@ __device__ __noinline__ void hdr_item_fused(const ouro_tpraos_batch& b, size_t i
       flag = ed_chain(ed, bw) ? kFlagOk : 0;
     }
     if (lead) stg1(res.word(kResFlags + e), flag);
-  } else if (!((skip >> item) & 1u)) {
-    hdr_core_wide(b, i, opts, item, res, bw, true);
+  } else {
+    if (!((skip >> item) & 1u)) hdr_core_wide(b, i, opts, item, res, bw, true);
+    // split V: the second of a VRF's V and Gamma cores combines and encodes
+    const bool vg = item == kCoreVe || item == kCoreVl || item == kCoreGe || item == kCoreGl;
+    if (!OURO_V_WHOLE && vg) {
+      const int which = (item == kCoreVl || item == kCoreGl) ? 1 : 0;
+      if (arrive_last(res.word(kLatCtr + 1 + which), 2)) {
+        if (((skip >> (kCoreVe + which)) | (skip >> (kCoreGe + which))) & 1u) {  // probe: reset
+          if (lead) stg1(res.word(kLatCtr + 1 + which), 0);
+        } else {
+          vrf_combine_encode(res, which);
+        }
+      }
+    }
   }
   stamp("core");
   if (arrive_last(res.word(kLatCtr))) {

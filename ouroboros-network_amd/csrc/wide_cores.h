@@ -253,21 +253,49 @@ __device__ __forceinline__ void vrf_v_full_wide(uint32_t Henc[8], uint32_t Venc[
   ge_encode_with_inv(Venc, V.X, V.Y, fe_mul(inv, H.Z));
 }
 
-// The Gamma core: acceptance checks, [8]Gamma and beta = SHA-512(suite ||
-// 0x03 || encode([8]Gamma)); returns the flag word (with kFlagGammaX0)
-__device__ __forceinline__ int32_t vrf_gamma_beta_wide(uint32_t beta[16], const uint32_t pi[20]) {
+// The Gamma core: acceptance checks, [8]Gamma, beta = SHA-512(suite || 0x03
+// || encode([8]Gamma)) and the V half -[c]Gamma (`partial`); returns the flag
+// word (with kFlagGammaX0)
+__device__ __forceinline__ int32_t vrf_gamma_beta_wide(uint32_t beta[16], ge_p2& partial,
+                                                       const uint32_t pi[20]) {
   const Lanes L = lanes();
-  uint32_t G[8];
+  uint32_t G[8], c[8];
 #pragma unroll
-  for (int i = 0; i < 8; i++) G[i] = pi[i];
+  for (int i = 0; i < 8; i++) {
+    G[i] = pi[i];
+    c[i] = i < 4 ? pi[8 + i] : 0u;
+  }
   ge_p3 Gamma;
   bool ok = ge_is_canonical(G);
   ok = ge_decode_wide(&Gamma, G, false) && ok;
-  const pw G8w = pw_dbl(pw_dbl(pw_dbl(pw_from_p3(Gamma, L), L), L), L);
+  const pw Gw = pw_from_p3(Gamma, L);
+  const pw G8w = pw_dbl(pw_dbl(pw_dbl(Gw, L), L), L);
   uint32_t enc[8];
   encode_p2(enc, pw_to_p2(G8w));
   vrf_beta(beta, enc);
+  TabW t;
+  tab_build(t, pw_from_p3(ge_p3_neg(Gamma), L), d2_wide(L), L);
+  partial = pw_to_p2(pw_dsm<false, false>(t, c, 33, t, c, 0, c, nullptr, L));
   return (ok ? kFlagOk : 0) | (fe_iszero(Gamma.X) ? kFlagGammaX0 : 0);
+}
+
+// The second of a VRF's V and Gamma cores to arrive: V = [s]H + (-[c]Gamma)
+// from the record, H and V encoded with one inversion; resets the VRF's
+// counter (kLatCtr + 1 + which)
+__device__ __forceinline__ void vrf_combine_encode(Slot res, int which) {
+  const int ptH = which ? kPtHl : kPtHe, ptV = which ? kPtVl : kPtVe;
+  const ge_p2 H = ld_point_at(res + ptH * kPtWords);
+  const ge_p2 V = ge_p2_add(ld_point_at(res + ptV * kPtWords),
+                            ld_point_at(res + kLatPart + which * kPtWords));
+  const fe inv = invert_wide(fe_mul(H.Z, V.Z));
+  uint32_t Henc[8], Venc[8];
+  ge_encode_with_inv(Henc, H.X, H.Y, fe_mul(inv, V.Z));
+  ge_encode_with_inv(Venc, V.X, V.Y, fe_mul(inv, H.Z));
+  if ((threadIdx.x & 63u) == 0) {
+    st_words8(res + kLatEnc + 8 * (3 * which + 0), Henc);
+    st_words8(res + kLatEnc + 8 * (3 * which + 2), Venc);
+    stg1(res.word(kLatCtr + 1 + which), 0);
+  }
 }
 
 // Arrival at a counter of `parties` waves: this wave's record stores are
