@@ -138,6 +138,16 @@ __global__ void k_tpraos_cores(ouro_tpraos_batch b, const uint32_t* __restrict__
                                const int32_t* __restrict__ btab, int mode, int wide_waves,
                                uint8_t* __restrict__ verdict, uint8_t* __restrict__ beta_eta,
                                uint8_t* __restrict__ beta_leader);
+__global__ void k_ed25519_wide(size_t n, const uint8_t* __restrict__ pk,
+                               const uint8_t* __restrict__ sig, const uint8_t* __restrict__ msg,
+                               const uint64_t* __restrict__ msg_off,
+                               const uint32_t* __restrict__ msg_len, uint8_t* __restrict__ verdict,
+                               const int32_t* __restrict__ btab, uint32_t byron);
+__global__ void k_vrf03_wide(size_t n, const uint8_t* __restrict__ pk,
+                             const uint8_t* __restrict__ proof, const uint8_t* __restrict__ alpha,
+                             const uint64_t* __restrict__ alpha_off,
+                             const uint32_t* __restrict__ alpha_len, uint8_t* __restrict__ beta,
+                             uint8_t* __restrict__ verdict, const int32_t* __restrict__ btab);
 __global__ void k_tpraos_finish(ouro_tpraos_batch b, const uint32_t* __restrict__ d_n,
                                 int32_t* res_buf, uint8_t* __restrict__ verdict,
                                 uint8_t* __restrict__ beta_eta, uint8_t* __restrict__ beta_leader,
@@ -367,6 +377,15 @@ int launch_check() {
   return OURO_OK;
 }
 
+// Small batches (n <= OURO_WIDE_SMALL_MAX, default 2048; 0 = never) run one
+// item per wave (kernels_lat.hip k_ed25519_wide / k_vrf03_wide): a single
+// item's latency is then one wave's chain, not one lane's.
+size_t wide_small_max() {
+  if (const char* e = getenv("OURO_WIDE_SMALL_MAX")) return (size_t)strtoull(e, nullptr, 0);
+  return 2048;
+}
+int wide_grid(size_t n) { return (int)std::min<size_t>(n, 8192); }
+
 // ---- device-pointer launches (shared by the host-buffer and device APIs) ----
 // byron = 1: ByronDSIGN acceptance (cardano-crypto)
 int launch_ed(hipStream_t st, size_t n, const uint8_t* pk, const uint8_t* sig, const uint8_t* msg,
@@ -374,6 +393,11 @@ int launch_ed(hipStream_t st, size_t n, const uint8_t* pk, const uint8_t* sig, c
   DeviceState* ds;
   int rc = device_state(&ds);
   if (rc) return rc;
+  if (n <= wide_small_max()) {
+    hipLaunchKernelGGL(k_ed25519_wide, dim3(wide_grid(n)), dim3(64), 0, st, n, pk, sig, msg, off,
+                       len, verdict, ds->btab, byron);
+    return launch_check();
+  }
   int grid;
   int32_t* scr;
   if ((rc = plan(ds, kEd, n, st, &grid, &scr))) return rc;
@@ -388,6 +412,11 @@ int launch_vrf(hipStream_t st, size_t n, const uint8_t* pk, const uint8_t* proof
   DeviceState* ds;
   int rc = device_state(&ds);
   if (rc) return rc;
+  if (n <= wide_small_max()) {
+    hipLaunchKernelGGL(k_vrf03_wide, dim3(wide_grid(n)), dim3(64), 0, st, n, pk, proof, alpha,
+                       off, len, beta, verdict, ds->btab);
+    return launch_check();
+  }
   int grid;
   int32_t* scr;
   if ((rc = plan(ds, kVrf, n, st, &grid, &scr))) return rc;

@@ -335,3 +335,51 @@ __global__ void __launch_bounds__(kBlock, OURO_WAVES) k_tpraos_finish(ouro_tprao
   }
 }
 
+// Small batches on whole waves (one item per wave, wide_cores.h): the
+// latency of a single-item call or a few items is one wave's chain instead of
+// one lane's (launch_ed / launch_vrf route n <= OURO_WIDE_SMALL_MAX here).
+// Same verdicts and outputs as k_ed25519_verify / k_vrf03_verify.
+__global__ void __launch_bounds__(64) k_ed25519_wide(size_t n, const uint8_t* __restrict__ pk,
+                                                     const uint8_t* __restrict__ sig,
+                                                     const uint8_t* __restrict__ msg,
+                                                     const uint64_t* __restrict__ msg_off,
+                                                     const uint32_t* __restrict__ msg_len,
+                                                     uint8_t* __restrict__ verdict,
+                                                     const int32_t* __restrict__ btab,
+                                                     uint32_t byron) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const uint16_t* bw = reinterpret_cast<const uint16_t*>(btab + kBTabWords);
+  for (size_t i = blockIdx.x; i < n; i += gridDim.x) {
+    uint32_t s[16], p[8];
+    load_words(s, sig + 64 * i, 4);
+    load_words(p, pk + 32 * i, 2);
+    const bool ok = wide::ed25519_verify_wide(s, p, ShaGlobalTail{msg + msg_off[i]}, msg_len[i],
+                                              bw, byron != 0);
+    if (threadIdx.x == 0) verdict[i] = ok ? 1 : 0;
+  }
+#endif
+}
+
+__global__ void __launch_bounds__(64) k_vrf03_wide(size_t n, const uint8_t* __restrict__ pk,
+                                                   const uint8_t* __restrict__ proof,
+                                                   const uint8_t* __restrict__ alpha,
+                                                   const uint64_t* __restrict__ alpha_off,
+                                                   const uint32_t* __restrict__ alpha_len,
+                                                   uint8_t* __restrict__ beta,
+                                                   uint8_t* __restrict__ verdict,
+                                                   const int32_t* __restrict__ btab) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const uint16_t* bw = reinterpret_cast<const uint16_t*>(btab + kBTabWords);
+  for (size_t i = blockIdx.x; i < n; i += gridDim.x) {
+    uint32_t p[8], pi[20], b[16];
+    load_words(p, pk + 32 * i, 2);
+    load_words(pi, proof + 80 * i, 5);
+    const bool ok = wide::vrf03_verify_wide(b, p, pi, ShaGlobalTail{alpha + alpha_off[i]},
+                                            alpha_len[i], bw);
+    if (threadIdx.x == 0) {
+      store_words(beta + 64 * i, b, 4);
+      verdict[i] = ok ? 1 : 0;
+    }
+  }
+#endif
+}

@@ -52,7 +52,7 @@ __device__ __forceinline__ ge_p2 pw_to_p2(const pw& Q) {
 template <class Tail>
 __device__ __forceinline__ bool ed25519_verify_wide(const uint32_t sig[16], const uint32_t pk[8],
                                                     const Tail& msg, uint32_t mlen,
-                                                    const uint16_t* bw) {
+                                                    const uint16_t* bw, bool byron = false) {
   const Lanes L = lanes();
   uint32_t R[8], S[8];
 #pragma unroll
@@ -60,7 +60,7 @@ __device__ __forceinline__ bool ed25519_verify_wide(const uint32_t sig[16], cons
     R[i] = sig[i];
     S[i] = sig[8 + i];
   }
-  bool ok = ed25519_precheck(R, S, pk, false);
+  bool ok = ed25519_precheck(R, S, pk, byron);
   ge_p3 negA, negR;
   bool okA, okR;
   ge_decode_pair_wide(&negA, &okA, &negR, &okR, pk, R, true);
@@ -187,6 +187,74 @@ __device__ __forceinline__ void vrf_sh(ge_p3& H, ge_p2& V, const uint32_t pk[8],
   TabW tab;
   tab_build(tab, pw_from_p3(H, L), d2_wide(L), L);
   V = pw_to_p2(pw_scalarmult(tab, s, L));
+}
+
+// ---- a whole draft-03 VRF verification on one wave (small batches) ---------------
+// verify.h vrf03_verify_lane with the wave-wide arithmetic: Y's and Gamma's
+// decodes on alternate rows at once, Elligator2, U = [s]B - [c]Y, V = [s]H -
+// [c]Gamma, [8]Gamma, one inversion for the four encodings, the challenge
+// and beta.  beta is zeroed unless the proof verifies.
+__device__ __forceinline__ fe invert_wide(const fe& z);
+template <class Tail>
+__device__ __forceinline__ bool vrf03_verify_wide(uint32_t beta[16], const uint32_t pk[8],
+                                                  const uint32_t pi[20], const Tail& alpha,
+                                                  uint32_t alen, const uint16_t* bw) {
+  const Lanes L = lanes();
+  uint32_t G[8], c[8], s_raw[8], s[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    G[i] = pi[i];
+    c[i] = i < 4 ? pi[8 + i] : 0u;
+    s_raw[i] = pi[12 + i];
+  }
+  ge_p3 Y, Gamma;
+  bool okY, okG;
+  ge_decode_pair_wide(&Y, &okY, &Gamma, &okG, pk, G, false);
+  bool ok = !ge_has_small_order(pk) && ge_is_canonical(pk) && okY;
+  ok = ge_is_canonical(G) && okG && ok;
+  sc_reduce256(s, s_raw);
+  uint32_t pre[9];
+  pre[0] = 0x04u | (0x01u << 8) | (pk[0] << 16);
+#pragma unroll
+  for (int i = 1; i < 8; i++) pre[i] = (pk[i - 1] >> 16) | (pk[i] << 16);
+  pre[8] = pk[7] >> 16;
+  uint64_t Hs[8];
+  sha512_prefixed<34>(Hs, pre, alpha, alen);
+  uint32_t rw[16];
+  sha512_digest_words(rw, Hs);
+  rw[7] &= 0x7fffffffu;
+  const ge_p3 Hp = elligator2_h_with(rw, [](const fe& z) { return pow22523_wide(z); });
+  const int32_t d2 = d2_wide(L);
+  TabW tY, tH, tG;
+  tab_build(tY, pw_from_p3(ge_p3_neg(Y), L), d2, L);
+  const ge_p2 U = pw_to_p2(pw_dsm<false, true>(tY, c, 33, tY, c, 0, s, bw, L));
+  tab_build(tH, pw_from_p3(Hp, L), d2, L);
+  const pw Gw = pw_from_p3(Gamma, L);
+  tab_build(tG, pw_from_p3(ge_p3_neg(Gamma), L), d2, L);
+  const ge_p2 V = pw_to_p2(pw_dsm<true, false>(tH, s, 64, tG, c, 33, s, nullptr, L));
+  const ge_p2 G8 = pw_to_p2(pw_dbl(pw_dbl(pw_dbl(Gw, L), L), L));
+  // one inversion for the four encodings
+  const fe a1 = fe_mul(Hp.Z, U.Z), a2 = fe_mul(a1, V.Z), a3 = fe_mul(a2, G8.Z);
+  fe inv = invert_wide(a3);
+  const fe z3 = fe_mul(inv, a2);
+  inv = fe_mul(inv, G8.Z);
+  const fe z2 = fe_mul(inv, a1);
+  inv = fe_mul(inv, V.Z);
+  const fe z1 = fe_mul(inv, Hp.Z), z0 = fe_mul(inv, U.Z);
+  uint32_t Henc[8], Uenc[8], Venc[8], G8enc[8], Genc[8], cc[4], b[16];
+  ge_encode_with_inv(Henc, Hp.X, Hp.Y, z0);
+  ge_encode_with_inv(Uenc, U.X, U.Y, z1);
+  ge_encode_with_inv(Venc, V.X, V.Y, z2);
+  ge_encode_with_inv(G8enc, G8.X, G8.Y, z3);
+#pragma unroll
+  for (int i = 0; i < 8; i++) Genc[i] = G[i];
+  if (fe_iszero(Gamma.X)) Genc[7] &= 0x7fffffffu;
+#pragma unroll
+  for (int i = 0; i < 4; i++) cc[i] = c[i];
+  ok = vrf_finish(b, Henc, Genc, Uenc, Venc, G8enc, cc) && ok;
+#pragma unroll
+  for (int i = 0; i < 16; i++) beta[i] = ok ? b[i] : 0u;
+  return ok;
 }
 
 // ---- fused mode: each core encodes the points it makes ----------------------

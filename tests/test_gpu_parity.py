@@ -28,7 +28,17 @@ def corrupt_rows(rng, arrays, frac=8):
     return idx
 
 
-def test_ed25519_batch_matches_oracle(gpu_lib):
+@pytest.fixture(params=["wave_per_item", "lane_per_item"])
+def small_path(request, monkeypatch):
+    """Batches up to OURO_WIDE_SMALL_MAX items run one item per wave
+    (wide_cores.h, the single-item latency path); 0 forces the one-lane
+    throughput kernels.  Both must agree with the oracle."""
+    if request.param == "lane_per_item":
+        monkeypatch.setenv("OURO_WIDE_SMALL_MAX", "0")
+    return request.param
+
+
+def test_ed25519_batch_matches_oracle(small_path, gpu_lib):
     from ouroboros_network_amd import Ed25519DSIGN
 
     rng = np.random.default_rng(7)
@@ -41,7 +51,7 @@ def test_ed25519_batch_matches_oracle(gpu_lib):
     np.testing.assert_array_equal(got, want)
 
 
-def test_ed25519_edge_cases(gpu_lib):
+def test_ed25519_edge_cases(small_path, gpu_lib):
     from ouroboros_network_amd import Ed25519DSIGN
 
     cases = ed25519_edge_cases()
@@ -51,7 +61,7 @@ def test_ed25519_edge_cases(gpu_lib):
     np.testing.assert_array_equal(got, want)
 
 
-def test_ed25519_variable_messages(gpu_lib):
+def test_ed25519_variable_messages(small_path, gpu_lib):
     from ouroboros_network_amd import Ed25519DSIGN
 
     rng = np.random.default_rng(3)
@@ -71,7 +81,7 @@ def test_ed25519_variable_messages(gpu_lib):
     np.testing.assert_array_equal(got, want)
 
 
-def test_vrf_batch_matches_oracle(gpu_lib):
+def test_vrf_batch_matches_oracle(small_path, gpu_lib):
     from ouroboros_network_amd import PraosVRF
 
     rng = np.random.default_rng(11)
@@ -83,7 +93,7 @@ def test_vrf_batch_matches_oracle(gpu_lib):
     np.testing.assert_array_equal(beta, wbeta)
 
 
-def test_vrf_draft03_vectors(gpu_lib, kats):
+def test_vrf_draft03_vectors(small_path, gpu_lib, kats):
     from ouroboros_network_amd import PraosVRF
 
     vs = kats["vrf_draft03"]
@@ -97,7 +107,7 @@ def test_vrf_draft03_vectors(gpu_lib, kats):
         assert PraosVRF.output_from_proof(bytes.fromhex(v["pi"])).hex() == v["beta"]
 
 
-def test_vrf_edge_cases(gpu_lib):
+def test_vrf_edge_cases(small_path, gpu_lib):
     from ouroboros_network_amd import PraosVRF
 
     cases = vrf_edge_cases()
@@ -386,7 +396,7 @@ def test_plan_submit_wait_windows_in_flight(gpu_lib, kats):
 
 # ---- ByronDSIGN ------------------------------
 
-def test_byron_golden_header(gpu_lib, kats):
+def test_byron_golden_header(small_path, gpu_lib, kats):
     from ouroboros_network_amd import ByronDSIGN, parse_byron_header, verify_byron_headers
 
     b = kats["byron"]
@@ -400,7 +410,7 @@ def test_byron_golden_header(gpu_lib, kats):
     assert verify_byron_headers([h, h]).tolist() == [True, True]
 
 
-def test_byron_batch_matches_oracle(gpu_lib):
+def test_byron_batch_matches_oracle(small_path, gpu_lib):
     """Synthetic signatures with 1/8 corrupted, the Ed25519 edge-case set and
     the Byron-specific corners (S + L < 2^253 accepted, top bits of S set):
     verdicts bit-exact with the oracle's donna-style rule."""
