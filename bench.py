@@ -217,12 +217,16 @@ class DeviceHeaders:
 
 
 def source_hash() -> str:
-    """sha256 over the product's device/host sources (csrc/, include/): ties a
-    committed PMC traffic figure to the code it was measured on."""
+    """sha256 over the sources the header kernel k_tpraos_verify is built from
+    (csrc/ and include/ headers, kernels.hip): ties a committed PMC traffic
+    figure to the code it was measured on.  The latency-mode translation unit
+    (kernels_lat.hip, wide*.h) and the test/synthesis sources do not enter
+    that kernel and are left out."""
     h = hashlib.sha256()
     for d in (os.path.join(ROOT, "ouroboros-network_amd", "csrc"), os.path.join(ROOT, "include")):
         for name in sorted(os.listdir(d)):
-            if name.endswith((".h", ".hip")) and not name.startswith(("devhost", "synth")):
+            if (name.endswith((".h", ".hip"))
+                    and not name.startswith(("devhost", "synth", "wide", "kernels_lat"))):
                 with open(os.path.join(d, name), "rb") as f:
                     h.update(name.encode() + b"\0" + f.read())
     return h.hexdigest()[:16]

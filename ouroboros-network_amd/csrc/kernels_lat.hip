@@ -140,8 +140,13 @@ __device__ __noinline__ void hdr_core_wide(const ouro_tpraos_batch& b, size_t i,
 // Every finished core arrives at the header's counter; the eighth runs the
 // finish (hdr_tail_wide).  skip: the timing probe's mask (cores 0..7).
 constexpr int kFusedItems = kLatCores + 2;
-// stamps (OURO_LAT_STAMPS=1, a timing probe): header 0's items print their
-// start / end times (s_memrealtime, 100 MHz) and the tail's end.
+// stamps (a timing probe, tools/lat_stamps.py: a build with
+// -DOURO_LAT_STAMPS=1, run with OURO_LAT_STAMPS set): header 0's items print
+// their start / end times (s_memrealtime, 100 MHz) and the tail's end.  The
+// product build has no printf.
+#ifndef OURO_LAT_STAMPS
+#define OURO_LAT_STAMPS 0
+#endif
 __device__ __noinline__ void hdr_item_fused(const ouro_tpraos_batch& b, size_t i, uint32_t opts,
                                             int item, Slot res, const uint16_t* bw, uint32_t skip,
                                             uint8_t* verdict, uint8_t* beta_eta,
@@ -151,9 +156,14 @@ __device__ __noinline__ void hdr_item_fused(const ouro_tpraos_batch& b, size_t i
   const bool lead = (threadIdx.x & 63u) == 0;
   const uint64_t t0 = stamps ? __builtin_amdgcn_s_memrealtime() : 0;
   auto stamp = [&](const char* what) {
+#if OURO_LAT_STAMPS
     if (stamps && lead && i == 0)
       printf("stamp %d %s %llu %llu\n", item, what, (unsigned long long)t0,
              (unsigned long long)__builtin_amdgcn_s_memrealtime());
+#else
+    (void)what;
+    (void)t0;
+#endif
   };
   if (item == kCoreOcert || item == kCoreKes || item >= kLatCores) {
     const int e = item >= kLatCores ? item - kLatCores : item;  // 0 OCERT, 1 KES

@@ -1,11 +1,13 @@
 #!/usr/bin/env python3
-"""Timing probe of the fused configs[4] launch: with OURO_LAT_STAMPS=1 the
-kernel prints header 0's item start/end times (s_memrealtime, 100 MHz); this
-runs a 64-header plan R times and prints, per item, the median start and end
-in us relative to the earliest start of each launch.  Items: 0/8 OCERT points/
+"""Timing probe of the fused configs[4] launch: a library built with
+-DOURO_LAT_STAMPS=1 (tools/build_variant.sh stamps -DOURO_LAT_STAMPS=1), run
+with OURO_LAT_STAMPS set, prints header 0's item start/end times
+(s_memrealtime, 100 MHz); this runs a 64-header plan R times on that library
+(OURO_VERIFY_LIB) and prints, per item, the median start and end in us
+relative to the earliest start of each launch.  Items: 0/8 OCERT points/
 scalars, 1/9 KES points/scalars, 2/3 U eta/leader, 4/5 V, 6/7 Gamma.
 
-  python tools/lat_stamps.py [--runs R] > stamps.txt   (reads its own stdout)
+  python tools/lat_stamps.py [--runs R] [--lib PATH]
 """
 import os
 import subprocess
@@ -37,7 +39,9 @@ plan.close()
 
 def main():
     runs = int(sys.argv[sys.argv.index("--runs") + 1]) if "--runs" in sys.argv else 20
-    env = dict(os.environ, OURO_LAT_STAMPS="1")
+    lib = sys.argv[sys.argv.index("--lib") + 1] if "--lib" in sys.argv else os.path.join(
+        ROOT, "ouroboros-network_amd", "lib", "variants", "stamps.so")
+    env = dict(os.environ, OURO_LAT_STAMPS="1", OURO_VERIFY_LIB=os.path.abspath(lib))
     p = subprocess.run([sys.executable, "-c", CHILD % (ROOT, runs)], env=env, capture_output=True,
                        text=True, timeout=600)
     if p.returncode:
