@@ -118,6 +118,7 @@ __device__ __noinline__ void hdr_core_wide(const ouro_tpraos_batch& b, size_t i,
           if (!OURO_V_WHOLE)
             st_point_at(res + kLatPart + (leader ? kPtWords : 0), part.X, part.Y, part.Z);
         }
+        if (!leader && (opts & kOptEtaNonce)) eta_nonce_candidates(b, i, opts, res, beta);
         break;
       }
       ge_p2 part;

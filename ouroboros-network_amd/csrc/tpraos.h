@@ -40,7 +40,11 @@ constexpr int kLatCtr = kLatBeta + 32;
 // (wide_cores.h): its scalars, decoded points and arrival counter
 constexpr int kLatEd = kLatCtr + 4;                   // Ed record e at kLatEd + kEdWords e
 constexpr int kEdWords = 128;
-constexpr int kLatResWords = kLatEd + 2 * kEdWords;   // 708 words (16-B multiple)
+// fused mode: the eta nonce's two candidates, Blake2b-256 of the output it
+// hashes if the eta VRF verifies (the claimed one when given) and of 64 zero
+// bytes (a failed proof), hashed by the eta Gamma core off the critical path
+constexpr int kLatNonce = kLatEd + 2 * kEdWords;
+constexpr int kLatResWords = kLatNonce + 16;          // 724 words (16-B multiple)
 enum HdrCore { kCoreOcert = 0, kCoreKes, kCoreUe, kCoreUl, kCoreVe, kCoreVl, kHdrCores,
                // latency mode splits each V = [s]H - [c]Gamma over two lanes: the V
                // cores do [s]H (252-bit chain), these do -[c]Gamma (128-bit chain)

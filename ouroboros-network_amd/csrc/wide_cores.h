@@ -450,6 +450,27 @@ __device__ __forceinline__ bool ed_chain(Slot e, const uint16_t* bw) {
   return ok && pw_is_identity(Q);
 }
 
+// The eta nonce's candidates (tpraos.h hdr_eta_nonce): Blake2b-256 of the
+// claimed eta output when the batch carries it, else of this core's beta --
+// the nonce if the VRF verifies -- and of 64 zero bytes (if it does not).
+// Lanes 0 / 1 hash one each; stored for the tail to pick.
+__device__ __forceinline__ void eta_nonce_candidates(const ouro_tpraos_batch& b, size_t i,
+                                                     uint32_t opts, Slot res,
+                                                     const uint32_t beta[16]) {
+  const uint32_t lane = threadIdx.x & 63u;
+  uint32_t in[16], h[8];
+  if (opts & kOptEtaClaim) {
+    ld_words(in, b.eta_output + 64 * i, 4);
+  } else {
+#pragma unroll
+    for (int k = 0; k < 16; k++) in[k] = beta[k];
+  }
+#pragma unroll
+  for (int k = 0; k < 16; k++) in[k] = lane == 1 ? 0u : in[k];
+  blake2b256_64(h, in);
+  if (lane < 2) st_words8(res + kLatNonce + 8 * (int)lane, h);
+}
+
 // The tail of header i on the last core's wave: both VRFs at once (lanes
 // 0..31 the eta VRF, 32..63 the leader VRF) -- challenge check from the
 // record's encodings, beta, claimed-output bits, the eta nonce -- and the
@@ -483,7 +504,14 @@ __device__ __forceinline__ void hdr_tail_wide(const ouro_tpraos_batch& b, size_t
   bit |= hdr_claim_bit(b, i, opts, which, ok, beta);
   uint8_t* dst = which ? beta_leader : beta_eta;
   if ((lane & 31u) == 0 && dst) st_words(dst + 64 * i, beta, 4);
-  if (lane == 0) hdr_eta_nonce(b, i, opts, beta);
+  // the eta nonce: the candidate the eta Gamma core hashed (claimed output, or
+  // beta when the proof verified; Blake2b of zeros when it did not)
+  if (lane == 0 && (opts & kOptEtaNonce)) {
+    const bool pick0 = (opts & kOptEtaClaim) || ok;
+    uint32_t h[8];
+    ld_words8(h, res + kLatNonce + (pick0 ? 0 : 8));
+    st_words(b.eta_nonce + 32 * i, h, 2);
+  }
   const uint32_t other = (uint32_t)__builtin_amdgcn_readlane((int)bit, 32);
   if (lane == 0) {
     uint32_t v = bit | other;

@@ -26,6 +26,8 @@ def main():
     ap.add_argument("--batch", type=int, default=64)
     ap.add_argument("--var", default="OURO_LAT_BLOCK")
     ap.add_argument("--values", default="256,128,64")
+    ap.add_argument("--nonce", action="store_true",
+                    help="(--libs) request the eta nonce output as a node would")
     ap.add_argument("--libs", nargs="*", default=None,
                     help="A/B build variants of libouro_verify.so instead of an env variable")
     args = ap.parse_args()
@@ -89,7 +91,8 @@ def lib_variants(args, hb, body):
         assert plan, path
         plans[os.path.basename(path)] = (lib, plan)
     n = len(hb)
-    s = hb.c_struct()
+    en = np.zeros((n, 32), np.uint8)
+    s = hb.c_struct(eta_nonce=en) if args.nonce else hb.c_struct()
     outs = {k: (np.zeros(n, np.uint8), np.zeros((n, 64), np.uint8), np.zeros((n, 64), np.uint8))
             for k in plans}
     ptr = lambda a: a.ctypes.data_as(P)  # noqa: E731
