@@ -220,6 +220,7 @@ __device__ __noinline__ void hdr_item_fused(const ouro_tpraos_batch& b, size_t i
     }
   }
   stamp("core");
+  if (stamps) vstamp_print();
   if (arrive_last(res.word(kLatCtr))) {
     hdr_tail_wide(b, i, opts, res, verdict, beta_eta, beta_leader);
     stamp("tail");

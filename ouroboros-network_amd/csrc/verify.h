@@ -582,8 +582,10 @@ OURO_HD inline bool ed25519_verify_lane(const uint32_t sig[16], const uint32_t p
 // square; tools/check_elligator_exceptions.py), so no inverse of zero can
 // occur where libsodium would have computed one.
 // pow22523: z -> z^(2^252 - 3); the latency mode's wave-wide item passes the
-// wide exponentiation (wide.h), everything else fe_pow22523.
-template <class Pow>
+// wide exponentiation (wide.h), everything else fe_pow22523.  kMul8 = false
+// returns the Elligator2 point before the cofactor clearing (the wave-wide
+// item doubles it three times on the wave).
+template <class Pow, bool kMul8 = true>
 OURO_HD inline ge_p3 elligator2_h_with(const uint32_t r[8], Pow pow22523) {
   const fe A = fe_mont_a();
   fe rr = fe_from_words(r);
@@ -612,6 +614,7 @@ OURO_HD inline ge_p3 elligator2_h_with(const uint32_t r[8], Pow pow22523) {
   fe n = fe_sub(Xn, D), m = fe_add(Xn, D);
   const fe nc = fe_carry(n);
   ge_p3 P{fe_mul(x, m), nc, m, fe_mul(x, nc)};
+  if constexpr (!kMul8) return P;
   return ge_mul8(P);
 }
 OURO_HD inline ge_p3 elligator2_h(const uint32_t r[8]) {

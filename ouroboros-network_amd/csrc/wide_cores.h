@@ -13,6 +13,31 @@ namespace ouro {
 #if defined(__HIP_DEVICE_COMPILE__)
 namespace wide {
 
+// timing probe (a build with -DOURO_LAT_STAMPS=1, tools/lat_stamps.py): the
+// eta V item of header 0 in a fused launch (block 4) prints phase times
+#ifndef OURO_LAT_STAMPS
+#define OURO_LAT_STAMPS 0
+#endif
+#if OURO_LAT_STAMPS
+__device__ unsigned long long g_vstamps[8];
+#endif
+// phase k of that item (0 start, 1 sha, 2 elligator, 3 table, 4 chain,
+// 5 combine-add, 6 encoded), kept in device memory: printed once at the end
+__device__ __forceinline__ void vstamp(int k) {
+#if OURO_LAT_STAMPS
+  if (blockIdx.x == 4 && threadIdx.x == 0) g_vstamps[k] = __builtin_amdgcn_s_memrealtime();
+#else
+  (void)k;
+#endif
+}
+__device__ __forceinline__ void vstamp_print() {
+#if OURO_LAT_STAMPS
+  if (blockIdx.x == 4 && threadIdx.x == 0)
+    printf("vstamp %llu %llu %llu %llu %llu %llu %llu\n", g_vstamps[0], g_vstamps[1],
+           g_vstamps[2], g_vstamps[3], g_vstamps[4], g_vstamps[5], g_vstamps[6]);
+#endif
+}
+
 // z^(2^252 - 3) of a lane-local element on the wave
 __device__ __forceinline__ fe pow22523_wide(const fe& z) {
   return fw_to_fe(fw_pow22523(fe_to_fw(z, lanes())));
@@ -179,14 +204,23 @@ __device__ __forceinline__ void vrf_sh(ge_p3& H, ge_p2& V, const uint32_t pk[8],
   for (int k = 1; k < 8; k++) pre[k] = (pk[k - 1] >> 16) | (pk[k] << 16);
   pre[8] = pk[7] >> 16;
   uint64_t Hs[8];
+  vstamp(0);
   sha512_prefixed<34>(Hs, pre, alpha, 32);
   uint32_t rw[16];
   sha512_digest_words(rw, Hs);
   rw[7] &= 0x7fffffffu;
-  H = elligator2_h_with(rw, [](const fe& z) { return pow22523_wide(z); });
+  vstamp(1);
+  // the Elligator2 point, its cofactor cleared by three doublings on the wave
+  auto pw22523 = [](const fe& z) { return pow22523_wide(z); };
+  const ge_p3 P = elligator2_h_with<decltype(pw22523), false>(rw, pw22523);
+  const pw Hw = pw_dbl(pw_dbl(pw_dbl(pw_from_p3(P, L), L), L), L);
+  H = ge_p3{fw_to_fe(Hw.X), fw_to_fe(Hw.Y), fw_to_fe(Hw.Z), fw_to_fe(Hw.T)};
+  vstamp(2);
   TabW tab;
-  tab_build(tab, pw_from_p3(H, L), d2_wide(L), L);
+  tab_build(tab, Hw, d2_wide(L), L);
+  vstamp(3);
   V = pw_to_p2(pw_scalarmult(tab, s, L));
+  vstamp(4);
 }
 
 // ---- a whole draft-03 VRF verification on one wave (small batches) ---------------
@@ -355,10 +389,12 @@ __device__ __forceinline__ void vrf_combine_encode(Slot res, int which) {
   const ge_p2 H = ld_point_at(res + ptH * kPtWords);
   const ge_p2 V = ge_p2_add(ld_point_at(res + ptV * kPtWords),
                             ld_point_at(res + kLatPart + which * kPtWords));
+  vstamp(5);
   const fe inv = invert_wide(fe_mul(H.Z, V.Z));
   uint32_t Henc[8], Venc[8];
   ge_encode_with_inv(Henc, H.X, H.Y, fe_mul(inv, V.Z));
   ge_encode_with_inv(Venc, V.X, V.Y, fe_mul(inv, H.Z));
+  vstamp(6);
   if ((threadIdx.x & 63u) == 0) {
     st_words8(res + kLatEnc + 8 * (3 * which + 0), Henc);
     st_words8(res + kLatEnc + 8 * (3 * which + 2), Venc);

@@ -46,8 +46,12 @@ def main():
                        text=True, timeout=600)
     if p.returncode:
         sys.exit(p.stderr[-2000:])
-    launches, cur = [], []
+    launches, cur, vst = [], [], {}
     for line in p.stdout.splitlines():
+        if line.startswith("vstamp "):
+            ts = [int(x) for x in line.split()[1:]]
+            tags = ["start", "sha", "elligator", "table", "chain", "combine-add", "encoded"]
+            vst.setdefault(len(launches), []).extend(zip(tags, ts))
         if line.startswith("stamp "):
             _, item, what, t0, t1 = line.split()
             cur.append((int(item), what, int(t0), int(t1)))
@@ -63,6 +67,18 @@ def main():
     for (item, what), v in sorted(rows.items(), key=lambda kv: np.median([e for _, e in kv[1]])):
         a = np.array(v)
         print(f"item {item:2d} {what:5s} start {np.median(a[:, 0]):7.1f}  end {np.median(a[:, 1]):7.1f}")
+    # phases of header 0's eta V item (vstamp), relative to its start
+    phases = {}
+    for k, st in vst.items():
+        if k < 2:
+            continue
+        t0 = dict(st).get("start")
+        for tag, t in st:
+            if t0 is not None:
+                phases.setdefault(tag, []).append((t - t0) / 100.0)
+    if phases:
+        print("eta V item phases (us after its start):",
+              ", ".join(f"{k} {np.median(v):.1f}" for k, v in phases.items()))
 
 
 if __name__ == "__main__":
