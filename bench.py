@@ -4,9 +4,12 @@
 Workload (BASELINE.json configs[3]): full TPraos header batches -- per header
 the opcert Ed25519, Sum6KES (6 Blake2b Merkle levels + Ed25519 leaf over the
 544-byte body) and the eta + leader draft-03 VRF verifies with their outputs.
-Each rank verifies its own contiguous shard of 1,048,576 synthetic headers per
-step (weak scaling; no data-path collective); for N > 1 the step ends with the
-one RCCL all-gather of verdicts and VRF outputs the north star names.
+At N = 1 one GPU verifies a batch of 1,048,576 synthetic headers per step.  At
+N > 1 the default is configs[3] as written -- ONE batch of 1,048,576 headers
+per step cut into N/G contiguous shards (strong scaling; no data-path
+collective) -- and the step ends with the one RCCL all-gather of verdicts and
+VRF outputs the north star names; the weak-scaling figure (1,048,576 headers
+per GPU) is reported beside it as `weak`.  --weak makes weak scaling the line.
 
 Inputs are synthesised on the device (lib/libouro_synth.so, deterministic
 seeds) and are resident in HBM before timing starts.  The
@@ -48,7 +51,8 @@ def body_template() -> bytes:
     return H.parse_header(bytes.fromhex(kats["headers"][0]["raw"])).body
 
 
-def synth_headers(n: int, npools: int, device, first: int = 0, keep_nodes: bool = False):
+def synth_headers(n: int, npools: int, device, first: int = 0, keep_nodes: bool = False,
+                  keep_pool: bool = False):
     """Device-resident SoA header batch (torch uint8 tensors)."""
     import torch
 
@@ -83,7 +87,35 @@ def synth_headers(n: int, npools: int, device, first: int = 0, keep_nodes: bool 
     torch.cuda.synchronize()
     if keep_nodes:
         return t, blen, nodes
+    if keep_pool:
+        return t, blen, pool
     return t, blen
+
+
+def synth_node_config(t, n: int, npools: int, pool, eta0: bytes, device, slot0: int = 4_492_800):
+    """Turn a synth_headers batch into the node's configuration:
+    slots (slot0 + i), VRF proofs re-made over mkSeed seedEta / seedL slot eta0
+    (the device then derives the alphas itself), and the headers' claimed
+    outputs.  Adds "slot", "epoch_nonce", "eta_output", "leader_output"."""
+    import torch
+
+    lib = ctypes.CDLL(SYNTH_SO)
+    u8 = dict(dtype=torch.uint8, device=device)
+    t["slot"] = torch.empty(n * 8, **u8)
+    t["epoch_nonce"] = torch.frombuffer(bytearray(eta0), dtype=torch.uint8).to(device)
+    t["eta_output"] = torch.empty(n * 64, **u8)
+    t["leader_output"] = torch.empty(n * 64, **u8)
+    P = ctypes.c_void_p
+    fn = lib.ouro_synth_seeded
+    fn.restype = ctypes.c_int
+    fn.argtypes = [ctypes.c_size_t, ctypes.c_uint64, ctypes.c_int, P, ctypes.c_uint64] + [P] * 8
+    rc = fn(n, 0, npools, pool.data_ptr(), slot0, t["epoch_nonce"].data_ptr(),
+            *[t[k].data_ptr() for k in ("slot", "eta_alpha", "leader_alpha", "eta_proof",
+                                        "leader_proof", "eta_output", "leader_output")])
+    if rc != 0:
+        raise RuntimeError(f"ouro_synth_seeded failed: {rc}")
+    torch.cuda.synchronize()
+    return t
 
 
 RAW_OFFSET_NAMES = ["body", "body_len", "slot", "prev", "issuer", "vrf", "eta_out", "eta_proof",
@@ -205,7 +237,12 @@ class DeviceHeaders:
 
         blen = int(h("body_len", np.uint32)[0])
         body = self.t["body"][: m * blen].cpu().numpy()
-        return HeaderBatch(
+        opt = {}
+        if "slot" in self.t:  # the node configuration (synth_node_config)
+            opt = dict(slot=h("slot", np.uint64), epoch_nonce=self.t["epoch_nonce"].cpu().numpy(),
+                       eta_output=h("eta_output", np.uint8, 64),
+                       leader_output=h("leader_output", np.uint8, 64))
+        return HeaderBatch(**opt,
             issuer_vk=h("issuer_vk", np.uint8, 32), vrf_vk=h("vrf_vk", np.uint8, 32),
             eta_proof=h("eta_proof", np.uint8, 80), leader_proof=h("leader_proof", np.uint8, 80),
             eta_alpha=h("eta_alpha", np.uint8, 32), leader_alpha=h("leader_alpha", np.uint8, 32),
@@ -464,24 +501,18 @@ def cpu_baseline(hb, threads: int):
     return len(hb) / dt, dt, res
 
 
-def latency_leg(hdr, batch: int, iters: int, cpu_threads: int, cpu_iters: int):
-    """configs[4]: ChainSync small-batch path.  `batch` headers from host
-    memory through the captured hipGraph plan (H2D, the six-lanes-per-header
-    core kernel, the finish kernel, D2H), wall-clock per call; next to the CPU
-    oracle on the same batch on 1 core and on `cpu_threads` cores."""
-    sys.path.insert(0, os.path.join(ROOT, "tests"))
-    import oracle_ffi as O
+def _plan_latency(hb, iters: int, nonce: bool):
+    """Wall-clock latency of ouro_tpraos_plan_run on one batch, timed at the C
+    ABI as an FFI caller drives it (a prepared batch struct; the Python
+    wrapper's per-call marshalling, ~tens of us, is not the product's
+    latency).  Returns (latencies s, outputs)."""
     from ouroboros_network_amd.tpraos import HeaderPlan
 
-    hb = hdr.host_sample(batch)
     body_bytes = int(hb.body_len.astype(np.int64).sum())
-    plan = HeaderPlan(batch, body_bytes)
+    plan = HeaderPlan(len(hb), body_bytes)
     try:
-        out = plan.run(hb)
-        # timed at the C ABI, as an FFI caller drives it (ouro_tpraos_plan_run
-        # on a prepared batch struct); the Python wrapper's per-call struct
-        # marshalling (~tens of us) is not the product's latency
-        s = hb.c_struct()
+        out = plan.run(hb, nonce=nonce)
+        s = hb.c_struct(out[3] if nonce else None)
         P = lambda a: a.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
         run = plan._lib.ouro_tpraos_plan_run
         args = (plan._p, ctypes.byref(s), P(out[0]), P(out[1]), P(out[2]))
@@ -495,6 +526,30 @@ def latency_leg(hdr, batch: int, iters: int, cpu_threads: int, cpu_iters: int):
             assert rc == 0
     finally:
         plan.close()
+    return lat, out
+
+
+def _pcts(lat):
+    ms = lambda q: round(float(np.percentile(lat, q)) * 1e3, 4)  # noqa: E731
+    return {"p50_ms": ms(50), "p99_ms": ms(99), "p99_9_ms": ms(99.9), "max_ms": ms(100)}
+
+
+def latency_leg(hdr, batch: int, iters: int, cpu_threads: int, cpu_iters: int, node=None):
+    """configs[4]: ChainSync small-batch path.  `batch` headers from host
+    memory through the captured hipGraph plan (H2D, the fused latency kernel,
+    D2H), wall-clock per call over `iters` windows (p50 / p99 / p99.9); next to
+    the CPU oracle on the same batch on 1 core and on `cpu_threads` cores.
+    `node` (a DeviceHeaders in the node's configuration, synth_node_config):
+    the same timing with claimed outputs, (slot, eta0) seeds derived on the
+    device and the eta nonce requested -- the configuration a node runs --
+    beside the minimal one (caller-supplied alphas, no claims, no nonce)."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_ffi as O
+    from ouroboros_network_amd.tpraos import HDR_ALL_OK, HDR_STRICT_OK, HeaderPlan
+
+    hb = hdr.host_sample(batch)
+    body_bytes = int(hb.body_len.astype(np.int64).sum())
+    lat, out = _plan_latency(hb, iters, nonce=False)
     # windows in flight: 4 plans (e.g. 4 ChainSync peers) submitted round-robin,
     # each waited for just before its next submit
     plans = [HeaderPlan(batch, body_bytes) for _ in range(4)]
@@ -527,14 +582,28 @@ def latency_leg(hdr, batch: int, iters: int, cpu_threads: int, cpu_iters: int):
 
     c1, cn = cpu_lat(1), cpu_lat(cpu_threads)
     ms = lambda a, q: round(float(np.percentile(a, q)) * 1e3, 3)  # noqa: E731
-    return {"workload": f"configs[4]: {batch}-header batches from host memory, hipGraph plan",
-            "iters": iters, "p50_ms": ms(lat, 50), "p99_ms": ms(lat, 99),
-            "headers_per_s_at_p50": round(batch / (np.percentile(lat, 50)), 1),
-            "in_flight_4_plans_headers_per_s": round(batch * (4 * rounds + 4) / inflight_s, 1),
-            "all_valid": bool((out[0] == 15).all()), "gpu_equals_cpu": same,
-            "cpu_1core": {"p50_ms": ms(c1, 50), "p99_ms": ms(c1, 99), "iters": cpu_iters},
-            "cpu_ncores": {"cores": cpu_threads, "p50_ms": ms(cn, 50), "p99_ms": ms(cn, 99),
-                           "iters": cpu_iters}}
+    res = {"workload": f"configs[4]: {batch}-header batches from host memory, hipGraph plan "
+                       "(minimal configuration: caller alphas, no claimed outputs, no nonce)",
+           "iters": iters, **_pcts(lat),
+           "headers_per_s_at_p50": round(batch / (np.percentile(lat, 50)), 1),
+           "in_flight_4_plans_headers_per_s": round(batch * (4 * rounds + 4) / inflight_s, 1),
+           "all_valid": bool((out[0] == HDR_ALL_OK).all()), "gpu_equals_cpu": same,
+           "cpu_1core": {"p50_ms": ms(c1, 50), "p99_ms": ms(c1, 99), "iters": cpu_iters},
+           "cpu_ncores": {"cores": cpu_threads, "p50_ms": ms(cn, 50), "p99_ms": ms(cn, 99),
+                          "iters": cpu_iters}}
+    if node is not None:
+        nb = node.host_sample(batch)
+        nlat, nout = _plan_latency(nb, iters, nonce=True)
+        wv, wbe, wbl, wen = O.tpraos_verify_batch_nonce(nb, threads=1)
+        res["node"] = {
+            "workload": f"{batch}-header windows as a node runs them: claimed outputs checked "
+                        "(*_CLAIM_OK), VRF inputs from (slot, eta0) by mkSeed on the device, "
+                        "eta nonce output requested",
+            "iters": iters, **_pcts(nlat),
+            "all_strict_ok": bool((nout[0] == HDR_STRICT_OK).all()),
+            "gpu_equals_cpu": bool((nout[0] == wv).all() and (nout[1] == wbe).all()
+                                   and (nout[2] == wbl).all() and (nout[3] == wen).all())}
+    return res
 
 
 def e2e_leg(hdr, n: int, reps: int = 3):
@@ -807,11 +876,18 @@ def single_item_leg(ed, hdr, iters: int = 300):
         return {"p50_us": round(float(np.percentile(t, 50)) * 1e6, 1),
                 "p99_us": round(float(np.percentile(t, 99)) * 1e6, 1)}
 
+    shim = _native.load_shim()
     res = {"workload": f"{iters} single-item calls, valid synthetic items, one thread",
+           "routing": "each single-item symbol is one GPU round trip (H2D, one wave, D2H); "
+                      "include/ouro_verify.h routes per-item callers (n = 1) to "
+                      "libsodium / the fork and windows of >= 64 headers to plans",
            "ouro_ed25519_verify": lat(lambda i: lib.ouro_ed25519_verify(
                items[i][0], items[i][1], 32, items[i][2])),
-           "crypto_vrf_ietfdraft03_verify": lat(lambda i: lib.crypto_vrf_ietfdraft03_verify(
-               out, vitems[i][0], vitems[i][1], vitems[i][2], 32))}
+           "ouro_vrf03_verify": lat(lambda i: lib.ouro_vrf03_verify(
+               out, vitems[i][0], vitems[i][1], vitems[i][2], 32)),
+           "crypto_vrf_ietfdraft03_verify (opt-in shim)": lat(
+               lambda i: shim.crypto_vrf_ietfdraft03_verify(out, vitems[i][0], vitems[i][1],
+                                                            vitems[i][2], 32))}
     if os.path.exists(SODIUM_SO):
         so = ctypes.CDLL(SODIUM_SO)
         so.sodium_init()
@@ -823,16 +899,37 @@ def single_item_leg(ed, hdr, iters: int = 300):
     return res
 
 
+def step_shards(world: int, rank: int, headers: int, global_headers: int, weak: bool):
+    """This rank's share of a step: (strong, n, first, n_global).  N = 1: one
+    batch of `headers`.  N > 1: configs[3] as written by default -- ONE batch
+    of 1,048,576 (or global_headers) headers cut into N/G contiguous shards
+     -- or, with `weak` / global_headers = 0, `headers`
+    per rank (global headers [rank*n, (rank+1)*n))."""
+    from ouroboros_network_amd.shard import shard_range
+
+    if global_headers < 0:
+        global_headers = 0 if (world == 1 or weak) else (1 << 20)
+    if global_headers > 0:
+        lo, hi = shard_range(global_headers, world, rank)
+        if hi == lo:
+            raise SystemExit("more ranks than headers")
+        return True, hi - lo, lo, global_headers
+    return False, headers, rank * headers, headers * world
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--headers", type=int, default=1 << 20,
-                    help="headers per GPU per step (weak scaling)")
-    ap.add_argument("--global-headers", type=int, default=0,
+                    help="headers per GPU per step (weak scaling; the N = 1 batch)")
+    ap.add_argument("--global-headers", type=int, default=-1,
                     help="strong scaling: ONE batch of this many headers per step, cut into "
-                         "N/G contiguous shards (configs[3] as written: 1,048,576 over G GPUs)")
+                         "N/G contiguous shards (default for N > 1: 1,048,576, configs[3] as "
+                         "written; 0 = weak scaling)")
+    ap.add_argument("--weak", action="store_true",
+                    help="N > 1: weak scaling (--headers per GPU) as the line")
     ap.add_argument("--pools", type=int, default=1024)
     ap.add_argument("--cpu-sample", type=int, default=65536)
     ap.add_argument("--no-cpu", action="store_true")
@@ -840,9 +937,13 @@ def main():
     ap.add_argument("--no-latency", action="store_true")
     ap.add_argument("--no-e2e", action="store_true",
                     help="skip the host-buffer (PCIe-inclusive) end-to-end leg")
-    ap.add_argument("--lat-iters", type=int, default=2000,
-                    help="configs[4] 64-header plan launches timed for p50/p99")
+    ap.add_argument("--lat-iters", type=int, default=10000,
+                    help="configs[4] 64-header plan launches timed for p50/p99/p99.9 "
+                         "(SURVEY.md §8(d) C5: >= 10,000)")
     ap.add_argument("--lat-cpu-iters", type=int, default=50)
+    ap.add_argument("--components-only", action="store_true",
+                    help="time only the standalone Ed25519 / VRF / Sum6KES kernels over --headers "
+                         "items (the profiling run of tools/profile_components.sh)")
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (RCCL over xGMI, the real path) or gloo (rehearsal of the "
                          "multi-rank path on fewer GPUs: ranks share devices, gather via host)")
@@ -870,23 +971,25 @@ def main():
         else:
             dist.init_process_group(args.dist_backend)
 
-    from ouroboros_network_amd.shard import all_gather_results, pack_results, shard_range
+    from ouroboros_network_amd.shard import all_gather_results, pack_results
 
-    strong = args.global_headers > 0
-    if strong:
-        # one global batch, N/G contiguous headers per rank
-        lo, hi = shard_range(args.global_headers, world, rank)
-        n, first, n_global = hi - lo, lo, args.global_headers
-        if n == 0:
-            raise SystemExit("more ranks than headers")
-    else:
-        # each rank its own shard of n: global headers [rank*n, (rank+1)*n)
-        n, first, n_global = args.headers, rank * args.headers, args.headers * world
+    strong, n, first, n_global = step_shards(world, rank, args.headers, args.global_headers,
+                                             args.weak)
     t_syn = time.perf_counter()
     tensors, blen = synth_headers(n, args.pools, device, first=first)
     syn_s = time.perf_counter() - t_syn
     hdr = DeviceHeaders(tensors, n, device)
     stream = torch.cuda.current_stream()
+    if args.components_only:
+        # one header launch (the VRF leg compares its outputs), then each
+        # standalone kernel: 1 warm + --steps timed launches over n items
+        hdr.launch(stream)
+        torch.cuda.synchronize()
+        out = {"components_only": True, "n": n, "steps": args.steps, "source_hash": source_hash()}
+        out["ed25519"], _ = ed25519_rate(device, n, args.steps)
+        out.update(component_rates(hdr, n, args.steps))
+        print(json.dumps(out))
+        return
 
     def gather():
         # the one collective of the path: every rank receives all verdicts and
@@ -962,6 +1065,37 @@ def main():
     total = n_global * args.steps
     value = total / elapsed
     ms_per_step = elapsed / args.steps * 1e3
+    dist_info = None
+    if world > 1:
+        # what the process group itself reports, and every rank's kernel time
+        per_rank = [None] * world
+        dist.all_gather_object(per_rank, {"rank": rank, "device": gpu, "headers": n,
+                                          "kernel_ms": round(kern_ms, 3)})
+        dist_info = {"world_size_seen": dist.get_world_size(), "backend": dist.get_backend(),
+                     "per_rank": per_rank}
+        if strong:
+            # the weak-scaling figure beside the strong line: each rank
+            # re-verifies its N/G shard G times per step (1,048,576 headers of
+            # kernel work per GPU per step when G divides it), then gathers
+            torch.cuda.synchronize()
+            dist.barrier()
+            tw = time.perf_counter()
+            for k in range(args.steps):
+                hdr.use(0)
+                for _ in range(world):
+                    hdr.launch(stream)
+                gather()
+            torch.cuda.synchronize()
+            dist.barrier()
+            ew = time.perf_counter() - tw
+            red_dev = device if args.dist_backend == "nccl" else torch.device("cpu")
+            tt = torch.tensor([ew], dtype=torch.float64, device=red_dev)
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            ew = float(tt.item())
+            dist_info["weak"] = {
+                "value": round(n * world * world * args.steps / ew, 1), "unit": "headers/s",
+                "headers_per_gpu_per_step": n * world, "ms_per_step": round(ew / args.steps * 1e3, 3),
+                "how": "each rank verifies its N/G shard G times per step, then the all-gather"}
 
     if rank == 0:
         peak = None
@@ -1007,6 +1141,8 @@ def main():
             "synth_s": round(syn_s, 2),
             "roofline": roof,
         }
+        if dist_info:
+            out["distributed"] = dist_info
         cpu = host_cpu_info()
         sys.path.insert(0, os.path.join(ROOT, "tests"))
         import oracle_ffi as O
@@ -1047,8 +1183,11 @@ def main():
                 out["raw_cbor"] = {"error": str(e)}
         if not args.no_latency and world == 1:
             try:
+                nt, _, npool = synth_headers(64, args.pools, device, keep_pool=True)
+                synth_node_config(nt, 64, args.pools, npool, bytes(range(7, 39)), device)
+                node = DeviceHeaders(nt, 64, device)
                 out["latency"] = latency_leg(hdr, 64, args.lat_iters, cpu["usable"],
-                                             args.lat_cpu_iters)
+                                             args.lat_cpu_iters, node=node)
             except Exception as e:  # noqa: BLE001
                 out["latency"] = {"error": str(e)}
         if not args.no_cpu and world == 1:
@@ -1069,6 +1208,9 @@ def main():
                 "one_core": round(rate1, 1), "one_core_sample": m1,
                 "thread_scaling": round(rate / rate1, 2),
                 "host": cpu,
+                "cores_note": (f"{threads} = the CPUs this job may use: the cgroup quota "
+                               f"({cpu['cgroup_cpu_quota']}) / affinity of a {cpu['nproc']}-CPU "
+                               "host -- a container limit, not the box's core count"),
                 "why_port": "the reference's VRF C (cardano-crypto-praos) is not in the image; "
                             "the oracle restates it and is pinned to libsodium 1.0.18 + golden "
                             "vectors (DESIGN.md §2)",

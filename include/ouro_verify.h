@@ -15,7 +15,9 @@
  *     untouched and the call returns OURO_EDEVICE.
  *   - The caller owns every buffer; nothing is retained after return.
  *   - All calls are thread-safe and reentrant: each calling thread gets its own
- *     HIP stream and staging buffers on the current device.
+ *     HIP stream and staging buffers on the current device, borrowed from a
+ *     per-device pool and returned when the thread exits (threads that come
+ *     and go reuse them; nothing leaks per thread).
  *   - Byte layouts are the raw encodings of cardano-crypto-class:
  *     VerKeyDSIGN/VerKeyVRF/VerKeyKES 32 B, SigDSIGN 64 B, CertVRF (proof) 80 B,
  *     OutputVRF 64 B, SigKES (Sum6KES Ed25519DSIGN Blake2b_256) 448 B.
@@ -53,6 +55,17 @@ extern "C" {
 #define OURO_HDR_LEADER_CLAIM_OK 0x20u
 #define OURO_HDR_ALL_OK 0x0fu    /* ref2020: every proof / signature valid    */
 #define OURO_HDR_STRICT_OK 0x3fu /* strict: and both claimed outputs correct  */
+/* The VRF proof's s is NOT below L (set from the proof bytes alone, whatever
+ * the verdict).  Draft-03 leaves s's range to the implementation; this
+ * library, like the libsodium fork as SURVEY.md App. B.3 recalls it, reduces
+ * s mod L and accepts (the default; parity of that choice is unpinned: no
+ * reference fixture has s >= L).  A caller that must reject unreduced s
+ * ("strict s") requires these bits CLEAR:
+ *   valid_strict_s(v) = (v & (OURO_HDR_ALL_OK | OURO_HDR_S_UNREDUCED))
+ *                       == OURO_HDR_ALL_OK */
+#define OURO_HDR_ETA_S_UNREDUCED 0x40u
+#define OURO_HDR_LEADER_S_UNREDUCED 0x80u
+#define OURO_HDR_S_UNREDUCED 0xc0u
 
 /* ------------------------------------------------------------------ setup */
 
@@ -141,6 +154,14 @@ int ouro_vrf03_verify_batch(size_t n, const uint8_t *pk /* n x 32 */,
                             const uint8_t *proof /* n x 80 */, const uint8_t *alpha,
                             const uint64_t *alpha_off, const uint32_t *alpha_len,
                             uint8_t *beta /* n x 64 */, uint8_t *verdict);
+/* The same with option flags: OURO_VRF_STRICT_S rejects a proof whose s is
+ * not below L (verdict 0, beta zeroed) instead of reducing it (the default,
+ * see OURO_HDR_S_UNREDUCED). */
+#define OURO_VRF_STRICT_S 0x1u
+int ouro_vrf03_verify_batch_flags(size_t n, const uint8_t *pk, const uint8_t *proof,
+                                  const uint8_t *alpha, const uint64_t *alpha_off,
+                                  const uint32_t *alpha_len, uint8_t *beta, uint8_t *verdict,
+                                  uint32_t flags);
 
 int ouro_sum6kes_verify_batch(size_t n, const uint8_t *vk /* n x 32 */,
                               const uint32_t *t, const uint8_t *msg, const uint64_t *msg_off,
@@ -307,6 +328,20 @@ int ouro_tpraos_plan_submit(ouro_tpraos_plan *plan, const ouro_tpraos_batch *b);
 int ouro_tpraos_plan_wait(ouro_tpraos_plan *plan, uint8_t *verdict, uint8_t *beta_eta,
                           uint8_t *beta_leader);
 
+/* A plan's latency kernel counts each header's finished checks in per-header
+ * arrival counters tagged with the launch's generation (a new one per
+ * submit), so a counter an earlier launch left mid-count (one that never
+ * completed) is never counted again.  TEST HOOK: leaves every counter of the
+ * plan as its last launch would have left them had it been cut off one
+ * arrival short of each finish (tests/test_gpu_claims.py). */
+int ouro_tpraos_plan_debug_poison(ouro_tpraos_plan *plan);
+
+/* Diagnostics: per-thread contexts (stream, scratch, staging) are pooled per
+ * device; a thread borrows one on its first call and returns it when it
+ * exits.  created = contexts made so far on `device`, idle = returned ones
+ * waiting in the pool.  Host-only. */
+int ouro_debug_contexts(int device, size_t *created, size_t *idle);
+
 /* ---------------------------------------------- leader threshold ----- */
 /* ledger-specs checkLeaderValue (shelley-spec-ledger BlockChain.hs), called by
  * meetsLeaderThreshold, ouroboros-consensus-shelley/src/Ouroboros/Consensus/
@@ -345,6 +380,10 @@ int ouro_vrf03_verify_batch_device(void *stream, size_t n, const uint8_t *pk,
                                    const uint8_t *proof, const uint8_t *alpha,
                                    const uint64_t *alpha_off, const uint32_t *alpha_len,
                                    uint8_t *beta, uint8_t *verdict);
+int ouro_vrf03_verify_batch_device_flags(void *stream, size_t n, const uint8_t *pk,
+                                         const uint8_t *proof, const uint8_t *alpha,
+                                         const uint64_t *alpha_off, const uint32_t *alpha_len,
+                                         uint8_t *beta, uint8_t *verdict, uint32_t flags);
 int ouro_sum6kes_verify_batch_device(void *stream, size_t n, const uint8_t *vk,
                                      const uint32_t *t, const uint8_t *msg,
                                      const uint64_t *msg_off, const uint32_t *msg_len,

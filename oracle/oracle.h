@@ -54,6 +54,9 @@ int orc_ed25519_verify_byron(const uint8_t sig[64], const uint8_t *m, size_t mle
 
 /* ---- ECVRF-ED25519-SHA512-Elligator2, IETF draft-03 ---- */
 void orc_elligator2_from_uniform(uint8_t out[32], const uint8_t r[32]);
+/* strict_s = 1: also reject a proof whose s is not below L */
+int orc_vrf03_verify_mode(uint8_t out[64], const uint8_t pk[32], const uint8_t pi[80],
+                          const uint8_t *m, size_t mlen, int strict_s);
 int orc_vrf03_verify(uint8_t out[64], const uint8_t pk[32], const uint8_t proof[80],
                      const uint8_t *m, size_t mlen);
 int orc_vrf03_proof_to_hash(uint8_t out[64], const uint8_t proof[80]);
@@ -105,6 +108,11 @@ typedef struct orc_tpraos_batch {
 #define ORC_HDR_ALL_OK 15u
 #define ORC_HDR_ETA_CLAIM_OK 16u
 #define ORC_HDR_LEADER_CLAIM_OK 32u
+/* the proof's s is not reduced (s >= L): draft-03's decode_proof as
+ * libsodium's fork reduces it (accepted); a strict-s caller rejects it
+ * (parity of the default unpinned) */
+#define ORC_HDR_ETA_S_UNREDUCED 64u
+#define ORC_HDR_LEADER_S_UNREDUCED 128u
 
 /* ledger-specs mkNonceFromNumber: Blake2b-256(BE64(k)) (a Nonce hash) */
 void orc_mk_nonce_from_number(uint8_t out[32], uint64_t k);

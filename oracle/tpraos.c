@@ -83,5 +83,8 @@ void orc_tpraos_verify_one(const orc_tpraos_batch *b, size_t i, uint8_t *verdict
    * of the computed one */
   if (b->eta_nonce)
     orc_blake2b_256(b->eta_nonce + 32 * i, b->eta_output ? b->eta_output + 64 * i : beta_eta, 64);
+  /* App. B.3 flag: s not reduced mod L, whatever the verdict */
+  if (!sc_is_canonical(b->eta_proof + 80 * i + 48)) v |= ORC_HDR_ETA_S_UNREDUCED;
+  if (!sc_is_canonical(b->leader_proof + 80 * i + 48)) v |= ORC_HDR_LEADER_S_UNREDUCED;
   *verdict = v;
 }

@@ -124,6 +124,15 @@ int orc_vrf03_proof_to_hash(uint8_t beta[64], const uint8_t pi[80]) {
   return 0;
 }
 
+/* draft-03 leaves the range of s to the implementation: the fork's
+ * decode_proof reduces it mod L (recalled, unpinned);
+ * strict_s selects the other reading, s >= L rejected. */
+int orc_vrf03_verify_mode(uint8_t out[64], const uint8_t pk[32], const uint8_t pi[80],
+                          const uint8_t *m, size_t mlen, int strict_s) {
+  if (strict_s && !sc_is_canonical(pi + 48)) return -1;
+  return orc_vrf03_verify(out, pk, pi, m, mlen);
+}
+
 int orc_vrf03_verify(uint8_t out[64], const uint8_t pk[32], const uint8_t pi[80],
                      const uint8_t *m, size_t mlen) {
   ge Y, G, H, negY, negG, U, V;

@@ -29,6 +29,10 @@ HDR_ETA_CLAIM_OK = 0x10
 HDR_LEADER_CLAIM_OK = 0x20
 HDR_ALL_OK = 0x0F      # ref2020: every proof and signature valid
 HDR_STRICT_OK = 0x3F   # strict: and both claimed outputs equal the computed ones
+HDR_ETA_S_UNREDUCED = 0x40     # the proof's s is not below L
+HDR_LEADER_S_UNREDUCED = 0x80
+HDR_S_UNREDUCED = 0xC0
+VRF_STRICT_S = 0x1             # ouro_vrf03_verify_batch_flags: reject s >= L
 
 LEADER_NO = 0
 LEADER_YES = 1
@@ -88,6 +92,11 @@ SIGNATURES = {
     "ouro_ed25519_verify_batch": (_I, [_SZ, _P, _P, _P, _P, _P, _P]),
     "ouro_byron_ed25519_verify_batch": (_I, [_SZ, _P, _P, _P, _P, _P, _P]),
     "ouro_vrf03_verify_batch": (_I, [_SZ, _P, _P, _P, _P, _P, _P, _P]),
+    "ouro_vrf03_verify_batch_flags": (_I, [_SZ, _P, _P, _P, _P, _P, _P, _P, ctypes.c_uint32]),
+    "ouro_vrf03_verify_batch_device_flags": (_I, [_P, _SZ, _P, _P, _P, _P, _P, _P, _P,
+                                                  ctypes.c_uint32]),
+    "ouro_tpraos_plan_debug_poison": (_I, [_P]),
+    "ouro_debug_contexts": (_I, [_I, _P, _P]),
     "ouro_sum6kes_verify_batch": (_I, [_SZ, _P, _P, _P, _P, _P, _P, _P]),
     "ouro_tpraos_verify_batch": (_I, [ctypes.POINTER(TPraosBatch), _P, _P, _P]),
     "ouro_ed25519_verify_batch_device": (_I, [_P, _SZ, _P, _P, _P, _P, _P, _P]),
@@ -114,7 +123,9 @@ SIGNATURES = {
                                           ctypes.POINTER(TPraosBatch), _P, _P, _P]),
 }
 
-# the cardano-crypto-praos names the library also exports (include/ouro_verify.h)
+# the cardano-crypto-praos names the OPT-IN shim exports (lib/libouro_vrf_shim.so,
+# csrc/vrf_shim.cpp); the product library itself does not
+SHIM_PATH = os.path.join(_HERE, "lib", "libouro_vrf_shim.so")
 VRF_ALIASES = {
     "crypto_vrf_ietfdraft03_verify": (_I, [_P, _P, _P, _P, _ULL]),
     "crypto_vrf_ietfdraft03_proof_to_hash": (_I, [_P, _P]),
@@ -149,12 +160,32 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
             lib = ctypes.CDLL(path)
         except OSError as e:  # pragma: no cover - depends on the image
             raise NativeUnavailable(f"cannot load {path}: {e}") from e
-        for name, (res, args) in list(SIGNATURES.items()) + list(VRF_ALIASES.items()):
+        for name, (res, args) in SIGNATURES.items():
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args
         _lib = lib
         return lib
+
+
+_shim = None
+
+
+def load_shim(path: str = SHIM_PATH) -> ctypes.CDLL:
+    """The opt-in crypto_vrf_* link shim (loads the product library first)."""
+    global _shim
+    load()
+    with _lock:
+        if _shim is None:
+            if not os.path.exists(path):
+                raise NativeUnavailable(f"{path} is not built")
+            lib = ctypes.CDLL(path)
+            for name, (res, args) in VRF_ALIASES.items():
+                fn = getattr(lib, name)
+                fn.restype = res
+                fn.argtypes = args
+            _shim = lib
+        return _shim
 
 
 def check(rc: int, what: str) -> int:

@@ -218,23 +218,32 @@ OURO_HD inline uint32_t kes_t_of(uint64_t slot, uint64_t spkp, uint64_t c0) {
   return t > 0xffffffffull ? 0xffffffffu : (uint32_t)t;
 }
 
+// CBOR-in-CBOR as the reference decodes it
+// (ouroboros-network/src/Ouroboros/Network/Block.hs:509-514, decodeWrapped):
+// the tag-24 byte string must be definite and lie inside the header's span,
+// the [header_body, kes_sig] item is parsed from its payload ALONE and must
+// end exactly where the payload ends ("trailing bytes in CBOR-in-CBOR"), and
+// nothing may follow the header inside its span.
 OURO_HD inline uint8_t pack_one(const uint8_t* raw, uint64_t base, uint32_t len, uint64_t spkp, const Out& o,
                  size_t i) {
-  const Cur c{raw + base, len};
+  const Cur outer{raw + base, len};
   int mt;
   uint64_t arg, j, pos = 0, era = 1;
   bool ind;
-  if (!head(c, 0, &mt, &arg, &j, &ind)) return OURO_PACK_ECBOR;
+  if (!head(outer, 0, &mt, &arg, &j, &ind)) return OURO_PACK_ECBOR;
   if (mt == 4 && !ind && arg == 2) {  // [era, wrapped]
-    if (!uint_at(c, j, &era)) return OURO_PACK_ESHAPE;
+    if (!uint_at(outer, j, &era)) return OURO_PACK_ESHAPE;
     if (era == 0) return OURO_PACK_EBYRON;
-    if (!skip(c, j, &pos)) return OURO_PACK_ECBOR;
+    if (!skip(outer, j, &pos)) return OURO_PACK_ECBOR;
   }
-  if (!head(c, pos, &mt, &arg, &j, &ind)) return OURO_PACK_ECBOR;
+  if (!head(outer, pos, &mt, &arg, &j, &ind)) return OURO_PACK_ECBOR;
   if (mt != 6 || ind || arg != 24) return OURO_PACK_ESHAPE;
   uint64_t k;
-  if (!head(c, j, &mt, &arg, &k, &ind)) return OURO_PACK_ECBOR;
-  if (mt != 2) return OURO_PACK_ESHAPE;
+  if (!head(outer, j, &mt, &arg, &k, &ind)) return OURO_PACK_ECBOR;
+  if (mt != 2 || ind) return OURO_PACK_ESHAPE;
+  if (outer.n - k < arg) return OURO_PACK_ECBOR;       // payload past the span
+  if (k + arg != outer.n) return OURO_PACK_ECBOR;      // bytes after the header
+  const Cur c{raw + base, k + arg};                    // the payload's end bounds the parse
   // [header_body, kes_sig]: the body's fields are walked once (the last
   // field's end is the body's end), then the signature
   uint64_t ts[2], te[2], fs[15], fe[15];
@@ -247,6 +256,7 @@ OURO_HD inline uint8_t pack_one(const uint8_t* raw, uint64_t base, uint32_t len,
   if (cnt != 15) return OURO_PACK_ESHAPE;
   te[0] = ts[1] = fe[14];
   if (!skip(c, ts[1], &te[1])) return OURO_PACK_ECBOR;
+  if (te[1] != c.n) return OURO_PACK_ECBOR;            // trailing bytes in CBOR-in-CBOR
   uint64_t es[2], ee[2], ls[2], le[2];
   int ce, cl;
   if (!array_items(c, fs[5], es, ee, 2, &ce) || !array_items(c, fs[6], ls, le, 2, &cl))

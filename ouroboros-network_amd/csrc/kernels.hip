@@ -48,7 +48,8 @@ __global__ void __launch_bounds__(kBlock, OURO_WAVES) k_vrf03_verify(
     size_t n, const uint8_t* __restrict__ pk, const uint8_t* __restrict__ proof,
     const uint8_t* __restrict__ alpha, const uint64_t* __restrict__ alpha_off,
     const uint32_t* __restrict__ alpha_len, uint8_t* __restrict__ beta,
-    uint8_t* __restrict__ verdict, int32_t* scratch, const int32_t* __restrict__ btab) {
+    uint8_t* __restrict__ verdict, int32_t* scratch, const int32_t* __restrict__ btab,
+    uint32_t flags) {
   const size_t tid = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   const size_t nth = (size_t)gridDim.x * blockDim.x;
   const Slot lane = slot_of(scratch, tid, kSlotWords);
@@ -56,7 +57,10 @@ __global__ void __launch_bounds__(kBlock, OURO_WAVES) k_vrf03_verify(
     uint32_t p[8], pi[20], b[16];
     load_words(p, pk + 32 * i, 2);
     load_words(pi, proof + 80 * i, 5);
-    const bool ok = vrf03_verify_lane(b, p, pi, ShaGlobalTail{alpha + alpha_off[i]}, alpha_len[i], lane, btab);
+    bool ok = vrf03_verify_lane(b, p, pi, ShaGlobalTail{alpha + alpha_off[i]}, alpha_len[i], lane, btab);
+    if ((flags & OURO_VRF_STRICT_S) && !sc_is_canonical(pi + 12)) ok = false;  // App. B.3
+#pragma unroll
+    for (int k = 0; k < 16; k++) b[k] = ok ? b[k] : 0u;
     store_words(beta + 64 * i, b, 4);
     verdict[i] = ok ? 1 : 0;
   }
@@ -147,7 +151,8 @@ __global__ void k_vrf03_wide(size_t n, const uint8_t* __restrict__ pk,
                              const uint8_t* __restrict__ proof, const uint8_t* __restrict__ alpha,
                              const uint64_t* __restrict__ alpha_off,
                              const uint32_t* __restrict__ alpha_len, uint8_t* __restrict__ beta,
-                             uint8_t* __restrict__ verdict, const int32_t* __restrict__ btab);
+                             uint8_t* __restrict__ verdict, const int32_t* __restrict__ btab,
+                             uint32_t flags);
 __global__ void k_tpraos_finish(ouro_tpraos_batch b, const uint32_t* __restrict__ d_n,
                                 int32_t* res_buf, uint8_t* __restrict__ verdict,
                                 uint8_t* __restrict__ beta_eta, uint8_t* __restrict__ beta_leader,
@@ -319,19 +324,103 @@ struct Buf {
   void* p = nullptr;
   size_t cap = 0;
 };
+
+// The bytes a batch addresses by (offset, length) pairs: the window
+// [lo, hi) over the items with length > 0, and the offsets rebased to lo, so
+// only that window is uploaded (a slice or shard of a larger batch with
+// absolute offsets does not drag the bytes before it along).
+struct Window {
+  uint64_t lo = 0, hi = 0;
+  std::vector<uint64_t> off;  // rebased; alive until the upload has completed
+  size_t span() const { return (size_t)(hi - lo); }
+};
+
+// rows [lo, lo + m) of a host batch on the device: `d` points at the copies
+// (optional members only when given), ver/be/bl/nonce at the result buffers
+struct StagedHdr {
+  ouro_tpraos_batch d{};
+  uint8_t *ver = nullptr, *be = nullptr, *bl = nullptr, *nonce = nullptr;
+  Window body;
+};
+
+// ---- pipelined host-buffer header batches (state) ----
+// A large batch from pageable host memory is cut into chunks of one full grid
+// of lanes.  Two slots (stream, device buffers, pinned result staging) take
+// turns: while chunk c's kernel runs on one stream, the host uploads chunk
+// c + 1 on the other and copies chunk c - 1's results out, so PCIe and the
+// host copies hide behind the kernel instead of adding to it.
+constexpr size_t kOutRow = 1 + 64 + 64 + 32;  // verdict | beta_eta | beta_leader | eta_nonce
+struct PipeSlot {
+  hipStream_t st = nullptr;
+  hipEvent_t done = nullptr;
+  Buf in[28];
+  uint8_t* h_out = nullptr;  // pinned: verdict (m) | beta_eta (64 m) | beta_leader (64 m) | eta_nonce (32 m)
+  size_t h_cap = 0;
+  StagedHdr staged;  // its rebased body offsets stay alive for the async upload
+  size_t lo = 0, m = 0;
+  bool busy = false;
+};
+struct Pipe {
+  bool ready = false;
+  PipeSlot s[2];
+};
+
+// Everything a calling thread needs on one device: its stream, the scratch
+// slots of each stream it launches on, staging buffers and the two-slot
+// pipeline.  Contexts are POOLED per device ("a per-thread
+// or pooled stream"): a thread borrows one on its first call for a device and
+// its thread-exit guard (Lease) hands it back, so the node's churning FFI
+// worker threads reuse a few contexts instead of leaking one each.  A
+// returned context has nothing in flight: host-buffer calls synchronise
+// before returning, and device-API launches on a caller stream only use the
+// scratch keyed by that stream (work later enqueued on the same stream is
+// ordered after them).  Only the pool itself outlives the process (never
+// freed: the HIP runtime may be gone at teardown).
 struct ThreadCtx {
   hipStream_t stream = nullptr;
   std::map<hipStream_t, Buf> scratch;  // per stream: concurrent launches never share slots
   Buf in[32];  // staging slots; a header batch uses up to 24
+  Pipe pipe;
 };
-// process teardown: the runtime may already be gone; the contexts leak rather
-// than free into it
-thread_local std::map<int, ThreadCtx>* t_ctx = nullptr;
+struct CtxPool {
+  std::mutex mu;
+  std::map<int, std::vector<ThreadCtx*>> free;  // per device
+  std::map<int, size_t> created;
+};
+CtxPool& ctx_pool() {
+  static CtxPool* p = new CtxPool;  // leaked on purpose (see above)
+  return *p;
+}
+struct Lease {
+  std::map<int, ThreadCtx*> held;  // device -> the context this thread borrowed
+  ~Lease() {
+    if (held.empty()) return;
+    CtxPool& P = ctx_pool();
+    std::lock_guard<std::mutex> g(P.mu);
+    for (auto& kv : held) P.free[kv.first].push_back(kv.second);
+  }
+};
+thread_local Lease t_lease;
 
 // the calling thread's context on device `dev`
 ThreadCtx& ctx_of(int dev) {
-  if (!t_ctx) t_ctx = new std::map<int, ThreadCtx>;
-  return (*t_ctx)[dev];
+  auto it = t_lease.held.find(dev);
+  if (it != t_lease.held.end()) return *it->second;
+  ThreadCtx* c = nullptr;
+  {
+    CtxPool& P = ctx_pool();
+    std::lock_guard<std::mutex> g(P.mu);
+    std::vector<ThreadCtx*>& v = P.free[dev];
+    if (!v.empty()) {
+      c = v.back();
+      v.pop_back();
+    } else {
+      c = new ThreadCtx;
+      P.created[dev]++;
+    }
+  }
+  t_lease.held[dev] = c;
+  return *c;
 }
 // ... on its current device (valid after current_device())
 ThreadCtx& ctx() { return ctx_of(t_device); }
@@ -408,20 +497,20 @@ int launch_ed(hipStream_t st, size_t n, const uint8_t* pk, const uint8_t* sig, c
 
 int launch_vrf(hipStream_t st, size_t n, const uint8_t* pk, const uint8_t* proof,
                const uint8_t* alpha, const uint64_t* off, const uint32_t* len, uint8_t* beta,
-               uint8_t* verdict) {
+               uint8_t* verdict, uint32_t flags = 0) {
   DeviceState* ds;
   int rc = device_state(&ds);
   if (rc) return rc;
   if (n <= wide_small_max()) {
     hipLaunchKernelGGL(k_vrf03_wide, dim3(wide_grid(n)), dim3(64), 0, st, n, pk, proof, alpha,
-                       off, len, beta, verdict, ds->btab);
+                       off, len, beta, verdict, ds->btab, flags);
     return launch_check();
   }
   int grid;
   int32_t* scr;
   if ((rc = plan(ds, kVrf, n, st, &grid, &scr))) return rc;
   hipLaunchKernelGGL(k_vrf03_verify, dim3(grid), dim3(kBlock), 0, st, n, pk, proof, alpha, off,
-                     len, beta, verdict, scr, ds->btab);
+                     len, beta, verdict, scr, ds->btab, flags);
   return launch_check();
 }
 
@@ -581,16 +670,8 @@ struct Stager {
   }
 };
 
-// The bytes a batch addresses by (offset, length) pairs: the window
-// [lo, hi) over the items with length > 0, and the offsets rebased to lo, so
-// only that window is uploaded (a slice or shard of a larger batch with
-// absolute offsets does not drag the bytes before it along).  EINVAL when an
-// offset + length overflows.
-struct Window {
-  uint64_t lo = 0, hi = 0;
-  std::vector<uint64_t> off;  // rebased; alive until the upload has completed
-  size_t span() const { return (size_t)(hi - lo); }
-};
+// Window of a batch (see struct Window); EINVAL when an offset + length
+// overflows.
 int window_of(size_t n, const uint64_t* off, const uint32_t* len, Window* w) {
   uint64_t lo = ~0ull, hi = 0;
   for (size_t i = 0; i < n; i++) {
@@ -630,14 +711,6 @@ int check_hdr_batch(const ouro_tpraos_batch* b) {
     return fail(OURO_EINVAL, "null alpha (and no slots to derive it from)");
   return OURO_OK;
 }
-
-// rows [lo, lo + m) of a host batch on the device: `d` points at the copies
-// (optional members only when given), ver/be/bl/nonce at the result buffers
-struct StagedHdr {
-  ouro_tpraos_batch d{};
-  uint8_t *ver = nullptr, *be = nullptr, *bl = nullptr, *nonce = nullptr;
-  Window body;
-};
 
 int stage_hdr(Stager& sg, const ouro_tpraos_batch* b, size_t lo, size_t m, StagedHdr* s) {
   int rc = window_of(m, b->body_off + lo, b->body_len + lo, &s->body);
@@ -738,7 +811,15 @@ int ouro_byron_ed25519_verify_batch(size_t n, const uint8_t* pk, const uint8_t* 
 int ouro_vrf03_verify_batch(size_t n, const uint8_t* pk, const uint8_t* proof, const uint8_t* alpha,
                             const uint64_t* alpha_off, const uint32_t* alpha_len, uint8_t* beta,
                             uint8_t* verdict) {
+  return ouro_vrf03_verify_batch_flags(n, pk, proof, alpha, alpha_off, alpha_len, beta, verdict, 0);
+}
+
+int ouro_vrf03_verify_batch_flags(size_t n, const uint8_t* pk, const uint8_t* proof,
+                                  const uint8_t* alpha, const uint64_t* alpha_off,
+                                  const uint32_t* alpha_len, uint8_t* beta, uint8_t* verdict,
+                                  uint32_t flags) {
   if (n == 0) return OURO_OK;
+  if (flags & ~OURO_VRF_STRICT_S) return fail(OURO_EINVAL, "unknown VRF flags");
   if (!pk || !proof || !alpha_off || !alpha_len || !verdict) return fail(OURO_EINVAL, "null argument");
   hipStream_t st;
   int rc = thread_stream(&st);
@@ -755,7 +836,7 @@ int ouro_vrf03_verify_batch(size_t n, const uint8_t* pk, const uint8_t* proof, c
   auto dbeta = sg.out<uint8_t>(64 * n);
   auto dver = sg.out<uint8_t>(n);
   if (sg.rc) return sg.rc;
-  if ((rc = launch_vrf(st, n, dpk, dpi, dal, doff, dlen, dbeta, dver))) return rc;
+  if ((rc = launch_vrf(st, n, dpk, dpi, dal, doff, dlen, dbeta, dver, flags))) return rc;
   std::vector<uint8_t> tv(n), tb(beta ? 64 * n : 0);
   if ((rc = download(st, tv.data(), dver, n))) return rc;
   if (beta && (rc = download(st, tb.data(), dbeta, 64 * n))) return rc;
@@ -796,32 +877,9 @@ int ouro_sum6kes_verify_batch(size_t n, const uint8_t* vk, const uint32_t* t, co
 }  // extern "C"
 
 namespace {
-// ---- pipelined host-buffer header batches ----
-// A large batch from pageable host memory is cut into chunks of one full grid
-// of lanes.  Two slots (stream, device buffers, pinned result staging) take
-// turns: while chunk c's kernel runs on one stream, the host uploads chunk
-// c + 1 on the other and copies chunk c - 1's results out, so PCIe and the
-// host copies hide behind the kernel instead of adding to it.
-constexpr size_t kOutRow = 1 + 64 + 64 + 32;  // verdict | beta_eta | beta_leader | eta_nonce
-struct PipeSlot {
-  hipStream_t st = nullptr;
-  hipEvent_t done = nullptr;
-  Buf in[28];
-  uint8_t* h_out = nullptr;  // pinned: verdict (m) | beta_eta (64 m) | beta_leader (64 m) | eta_nonce (32 m)
-  size_t h_cap = 0;
-  StagedHdr staged;  // its rebased body offsets stay alive for the async upload
-  size_t lo = 0, m = 0;
-  bool busy = false;
-};
-struct Pipe {
-  bool ready = false;
-  PipeSlot s[2];
-};
-thread_local std::map<int, Pipe>* t_pipe = nullptr;  // per device, like t_ctx
-
+// ---- pipelined host-buffer header batches (PipeSlot / Pipe above) ----
 int pipe_of(int dev, Pipe** out) {
-  if (!t_pipe) t_pipe = new std::map<int, Pipe>;
-  Pipe& p = (*t_pipe)[dev];
+  Pipe& p = ctx_of(dev).pipe;
   if (!p.ready) {
     for (PipeSlot& q : p.s) {
       if (!q.st) OURO_HIP(hipStreamCreateWithFlags(&q.st, hipStreamNonBlocking));
@@ -921,7 +979,8 @@ int hdr_batch_once(const ouro_tpraos_batch* b, const HdrOut& o, bool lowlat) {
   StagedHdr s;
   if ((rc = stage_hdr(sg, b, 0, n, &s))) return rc;
   if (lowlat) {
-    const uint32_t nw[4] = {(uint32_t)n, batch_opts(s.d), 0u, 0u};
+    // {n, option bits, generation (arrive_last; res is zeroed below), 0}
+    const uint32_t nw[4] = {(uint32_t)n, batch_opts(s.d), 1u, 0u};
     const uint32_t* d_n = sg.up(nw, 4);
     int32_t* res = sg.out<int32_t>(slot_region_words(n, kLatResWords));
     int32_t* scr = sg.out<int32_t>(lowlat_scratch_words(ds, n));
@@ -1100,24 +1159,8 @@ int ouro_vrf03_proof_to_hash(unsigned char* output, const unsigned char* proof) 
   return OURO_OK;
 }
 
-// The cardano-crypto-praos names (PraosVRF's foreign imports), so the shim can
-// satisfy them by link order; the version-less names are the fork's aliases
-// of draft-03.
-int crypto_vrf_ietfdraft03_verify(unsigned char* output, const unsigned char* pk,
-                                  const unsigned char* proof, const unsigned char* m,
-                                  unsigned long long mlen) {
-  return ouro_vrf03_verify(output, pk, proof, m, mlen);
-}
-int crypto_vrf_ietfdraft03_proof_to_hash(unsigned char* output, const unsigned char* proof) {
-  return ouro_vrf03_proof_to_hash(output, proof);
-}
-int crypto_vrf_verify(unsigned char* output, const unsigned char* pk, const unsigned char* proof,
-                      const unsigned char* m, unsigned long long mlen) {
-  return ouro_vrf03_verify(output, pk, proof, m, mlen);
-}
-int crypto_vrf_proof_to_hash(unsigned char* output, const unsigned char* proof) {
-  return ouro_vrf03_proof_to_hash(output, proof);
-}
+// (The cardano-crypto-praos names are NOT exported here: the opt-in
+// lib/libouro_vrf_shim.so, csrc/vrf_shim.cpp, provides them.)
 
 int ouro_sum6kes_verify(const unsigned char* vk, unsigned int t, const unsigned char* m,
                         unsigned long long mlen, const unsigned char* sig) {
@@ -1157,6 +1200,16 @@ int ouro_vrf03_verify_batch_device(void* stream, size_t n, const uint8_t* pk, co
   if (n == 0) return OURO_OK;
   hipStream_t st = static_cast<hipStream_t>(stream);  // NULL = HIP's default stream
   return launch_vrf(st, n, pk, proof, alpha, alpha_off, alpha_len, beta, verdict);
+}
+
+int ouro_vrf03_verify_batch_device_flags(void* stream, size_t n, const uint8_t* pk,
+                                         const uint8_t* proof, const uint8_t* alpha,
+                                         const uint64_t* alpha_off, const uint32_t* alpha_len,
+                                         uint8_t* beta, uint8_t* verdict, uint32_t flags) {
+  if (n == 0) return OURO_OK;
+  if (flags & ~OURO_VRF_STRICT_S) return fail(OURO_EINVAL, "unknown VRF flags");
+  hipStream_t st = static_cast<hipStream_t>(stream);  // NULL = HIP's default stream
+  return launch_vrf(st, n, pk, proof, alpha, alpha_off, alpha_len, beta, verdict, flags);
 }
 
 int ouro_sum6kes_verify_batch_device(void* stream, size_t n, const uint8_t* vk, const uint32_t* t,
@@ -1214,7 +1267,8 @@ int ouro_leader_check_batch_device(void* stream, size_t n, const uint8_t* beta,
 }  // extern "C"
 
 // ---- captured plans: pinned staging + hipGraph (H2D, 2 kernels, D2H) --------
-// The packed input block: 16 bytes {n, option bits (tpraos.h kOpt*)}, then
+// The packed input block: 16 bytes {n, option bits (tpraos.h kOpt*), the
+// launch's generation (wide_cores.h arrive_last), 0}, then
 // every member of ouro_tpraos_batch in order, each 16-byte aligned at
 // capacity size; the output block: verdict | beta_eta | beta_leader | eta_nonce.
 namespace {
@@ -1238,6 +1292,7 @@ struct ouro_tpraos_plan {
   int32_t *res = nullptr, *scratch = nullptr;
   size_t off[kPlanFields] = {0};  // byte offsets of the members in the packed input block
   ouro_tpraos_batch dev_batch{};
+  uint32_t gen = 0;             // generation of the last launch (arrive_last), 1..2^28-1
   size_t pending = 0;           // headers of the batch in flight (submit .. wait)
   uint8_t* nonce_dst = nullptr;  // that batch's eta_nonce (written by wait)
   bool inflight = false;
@@ -1375,7 +1430,10 @@ int ouro_tpraos_plan_submit(ouro_tpraos_plan* p, const ouro_tpraos_batch* b) {
                                             : (kFieldBytes[f] == 0 ? w.span() : 32);
     if (bytes && src[f]) memcpy(p->h_in + p->off[f], src[f], bytes);
   }
-  const uint32_t nw[2] = {(uint32_t)n, batch_opts(*b)};
+  // every launch a new generation, so no counter an earlier launch left
+  // behind (one that never completed) is ever counted again
+  p->gen = p->gen % 0x0fffffffu + 1u;
+  const uint32_t nw[3] = {(uint32_t)n, batch_opts(*b), p->gen};
   memcpy(p->h_in, nw, sizeof nw);
   OURO_HIP(hipSetDevice(p->dev));
   OURO_HIP(hipGraphLaunch(p->exec, p->st));
@@ -1414,6 +1472,40 @@ int ouro_tpraos_plan_run(ouro_tpraos_plan* p, const ouro_tpraos_batch* b, uint8_
 }
 
 void ouro_tpraos_plan_destroy(ouro_tpraos_plan* p) { plan_free(p); }
+
+// TEST HOOK (tests/test_gpu_claims.py::test_plan_counters_from_cut_off_launch):
+// leaves every arrival counter of the plan's records as a launch of its last
+// generation would have left them had it been cut off one arrival short of
+// each finish, so a test can show the next launch ignores them.
+int ouro_tpraos_plan_debug_poison(ouro_tpraos_plan* p) {
+  if (!p) return fail(OURO_EINVAL, "null plan");
+  if (p->inflight) return fail(OURO_EINVAL, "the plan has a batch in flight");
+  OURO_HIP(hipSetDevice(p->dev));
+  const size_t words = slot_region_words(p->cap, kLatResWords);
+  std::vector<int32_t> h(words);
+  OURO_HIP(hipMemcpy(h.data(), p->res, sizeof(int32_t) * words, hipMemcpyDeviceToHost));
+  const int32_t tag = (int32_t)((p->gen & 0x0fffffffu) << 4);
+  for (size_t i = 0; i < p->cap; i++) {
+    const Slot r = slot_of(h.data(), i, kLatResWords);
+    *r.word(kLatCtr) = tag | (kLatCores - 1);     // the header's tail one arrival away
+    *r.word(kLatCtr + 1) = tag | 1;                // each V / Gamma pair, one of two in
+    *r.word(kLatCtr + 2) = tag | 1;
+    *r.word(kLatEd + 125) = tag | 1;               // each Ed25519 points / scalars pair
+    *r.word(kLatEd + kEdWords + 125) = tag | 1;
+  }
+  OURO_HIP(hipMemcpy(p->res, h.data(), sizeof(int32_t) * words, hipMemcpyHostToDevice));
+  return OURO_OK;
+}
+
+// Contexts of the per-thread pool on `device` (kernels.hip ThreadCtx):
+// created so far and idle (returned by exited threads).
+int ouro_debug_contexts(int device, size_t* created, size_t* idle) {
+  CtxPool& P = ctx_pool();
+  std::lock_guard<std::mutex> g(P.mu);
+  if (created) *created = P.created[device];
+  if (idle) *idle = P.free[device].size();
+  return OURO_OK;
+}
 
 }  // extern "C"
 

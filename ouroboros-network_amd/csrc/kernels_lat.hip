@@ -150,6 +150,7 @@ constexpr int kFusedItems = kLatCores + 2;
 #endif
 __device__ __noinline__ void hdr_item_fused(const ouro_tpraos_batch& b, size_t i, uint32_t opts,
                                             int item, Slot res, const uint16_t* bw, uint32_t skip,
+                                            uint32_t gen,
                                             uint8_t* verdict, uint8_t* beta_eta,
                                             uint8_t* beta_leader, bool stamps) {
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -193,16 +194,11 @@ __device__ __noinline__ void hdr_item_fused(const ouro_tpraos_batch& b, size_t i
       else
         ed_points_item(ed, sig, cur, walk_ok);
     }
-    if (!arrive_last(ed.word(125), 2)) {
+    if (!arrive_last(ed.word(125), gen, 2)) {
       stamp("half");
       return;
     }
-    int32_t flag = 0;
-    if (skipped) {
-      if (lead) stg1(ed.word(125), 0);
-    } else {
-      flag = ed_chain(ed, bw) ? kFlagOk : 0;
-    }
+    const int32_t flag = (!skipped && ed_chain(ed, bw)) ? kFlagOk : 0;
     if (lead) stg1(res.word(kResFlags + e), flag);
   } else {
     if (!((skip >> item) & 1u)) hdr_core_wide(b, i, opts, item, res, bw, true);
@@ -210,18 +206,14 @@ __device__ __noinline__ void hdr_item_fused(const ouro_tpraos_batch& b, size_t i
     const bool vg = item == kCoreVe || item == kCoreVl || item == kCoreGe || item == kCoreGl;
     if (!OURO_V_WHOLE && vg) {
       const int which = (item == kCoreVl || item == kCoreGl) ? 1 : 0;
-      if (arrive_last(res.word(kLatCtr + 1 + which), 2)) {
-        if (((skip >> (kCoreVe + which)) | (skip >> (kCoreGe + which))) & 1u) {  // probe: reset
-          if (lead) stg1(res.word(kLatCtr + 1 + which), 0);
-        } else {
-          vrf_combine_encode(res, which);
-        }
-      }
+      if (arrive_last(res.word(kLatCtr + 1 + which), gen, 2) &&
+          !(((skip >> (kCoreVe + which)) | (skip >> (kCoreGe + which))) & 1u))
+        vrf_combine_encode(res, which);
     }
   }
   stamp("core");
   if (stamps) vstamp_print();
-  if (arrive_last(res.word(kLatCtr))) {
+  if (arrive_last(res.word(kLatCtr), gen)) {
     hdr_tail_wide(b, i, opts, res, verdict, beta_eta, beta_leader);
     stamp("tail");
   }
@@ -265,6 +257,7 @@ __global__ void __launch_bounds__(kBlock, OURO_WAVES) k_tpraos_cores(ouro_tpraos
                                                             uint8_t* __restrict__ beta_leader) {
   const size_t n = d_n[0];
   const uint32_t opts = d_n[1];
+  const uint32_t gen = d_n[2];  // the launch's generation (arrive_last), never 0
   const int quad = mode & 1;
   const uint32_t skip = ((uint32_t)mode >> 8) & 0xffu;
   const uint32_t wmask = ((uint32_t)mode >> 16) & 0xffu;
@@ -276,7 +269,7 @@ __global__ void __launch_bounds__(kBlock, OURO_WAVES) k_tpraos_cores(ouro_tpraos
     const size_t wv = gtid >> 6, i = wv / kFusedItems;
     if (i < n)
       hdr_item_fused(b, i, opts, (int)(wv % kFusedItems), slot_of(res_buf, i, kLatResWords),
-                     reinterpret_cast<const uint16_t*>(btab + kBTabWords), skip, verdict,
+                     reinterpret_cast<const uint16_t*>(btab + kBTabWords), skip, gen, verdict,
                      beta_eta, beta_leader, ((uint32_t)mode >> 25) & 1u);
     return;
   }
@@ -333,6 +326,7 @@ __global__ void __launch_bounds__(kBlock, OURO_WAVES) k_tpraos_finish(ouro_tprao
     load_words(pi, (which ? b.leader_proof : b.eta_proof) + 80 * i, 5);
     uint32_t bit = vrf_finish_split(res, which, pi, beta);
     bit |= hdr_claim_bit(b, i, opts, which, bit != 0, beta);
+    if (!sc_is_canonical(pi + 12)) bit |= which ? OURO_HDR_LEADER_S_UNREDUCED : OURO_HDR_ETA_S_UNREDUCED;
     if (q == 0) hdr_eta_nonce(b, i, opts, beta);
     // quad position 0 takes position 2's (the leader VRF's) bits
     const uint32_t other = (uint32_t)__builtin_amdgcn_mov_dpp((int)bit, 0x0a, 0xf, 0xf, true);
@@ -379,15 +373,19 @@ __global__ void __launch_bounds__(64) k_vrf03_wide(size_t n, const uint8_t* __re
                                                    const uint32_t* __restrict__ alpha_len,
                                                    uint8_t* __restrict__ beta,
                                                    uint8_t* __restrict__ verdict,
-                                                   const int32_t* __restrict__ btab) {
+                                                   const int32_t* __restrict__ btab,
+                                                   uint32_t flags) {
 #if defined(__HIP_DEVICE_COMPILE__)
   const uint16_t* bw = reinterpret_cast<const uint16_t*>(btab + kBTabWords);
   for (size_t i = blockIdx.x; i < n; i += gridDim.x) {
     uint32_t p[8], pi[20], b[16];
     load_words(p, pk + 32 * i, 2);
     load_words(pi, proof + 80 * i, 5);
-    const bool ok = wide::vrf03_verify_wide(b, p, pi, ShaGlobalTail{alpha + alpha_off[i]},
-                                            alpha_len[i], bw);
+    bool ok = wide::vrf03_verify_wide(b, p, pi, ShaGlobalTail{alpha + alpha_off[i]},
+                                      alpha_len[i], bw);
+    if ((flags & OURO_VRF_STRICT_S) && !sc_is_canonical(pi + 12)) ok = false;  // App. B.3
+#pragma unroll
+    for (int k = 0; k < 16; k++) b[k] = ok ? b[k] : 0u;
     if (threadIdx.x == 0) {
       store_words(beta + 64 * i, b, 4);
       verdict[i] = ok ? 1 : 0;

@@ -263,6 +263,68 @@ __global__ void __launch_bounds__(kBlock) k_synth_headers(
   }
 }
 
+// The node's configuration of a batch made by k_synth_headers (ADVICE r02:
+// the bench's "node" latency leg): slot_i = slot0 + i, VRF inputs derived
+// as the OVERLAY rule does -- mkSeed seedEta / seedL slot eta0 -- and both
+// proofs re-made over them with the pool's VRF key; the claimed outputs are
+// the proofs' outputs (proof_to_hash).  eta0 = NULL: NeutralNonce.
+__device__ void vrf_output_of(uint8_t* out, const uint32_t pi[20]) {
+  uint32_t G[8];
+  for (int k = 0; k < 8; k++) G[k] = pi[k];
+  ge_p3 Gamma;
+  ge_decode(&Gamma, G, false);
+  const ge_p3 G8 = ge_mul8(Gamma);
+  uint32_t enc[8], bp[9], w[16];
+  ge_encode_with_inv(enc, G8.X, G8.Y, fe_invert(G8.Z));
+  bp[0] = 0x04u | (0x03u << 8) | (enc[0] << 16);
+  for (int k = 1; k < 8; k++) bp[k] = (enc[k - 1] >> 16) | (enc[k] << 16);
+  bp[8] = enc[7] >> 16;
+  uint64_t H[8];
+  sha512_prefixed<34>(H, bp, ShaNoTail{}, 0);
+  sha512_digest_words(w, H);
+  st_n(out, w, 4);
+}
+
+__global__ void __launch_bounds__(kBlock) k_synth_seeded(
+    size_t n, uint64_t first, int npools, const uint32_t* pool, uint64_t slot0,
+    const uint8_t* eta0, uint64_t* slot, uint8_t* eta_alpha, uint8_t* leader_alpha,
+    uint8_t* eta_proof, uint8_t* leader_proof, uint8_t* eta_out, uint8_t* lead_out,
+    int32_t* scratch, const int32_t* btab) {
+  const size_t tid = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const size_t nth = (size_t)gridDim.x * blockDim.x;
+  const Slot lane = slot_of(scratch, tid, kLaneWords);
+  uint32_t e0[8];
+  if (eta0)
+    for (int k = 0; k < 8; k++)
+      e0[k] = (uint32_t)eta0[4 * k] | ((uint32_t)eta0[4 * k + 1] << 8) |
+              ((uint32_t)eta0[4 * k + 2] << 16) | ((uint32_t)eta0[4 * k + 3] << 24);
+  for (size_t i = tid; i < n; i += nth) {
+    const int j = (int)((first + i) % (uint64_t)npools);
+    const uint32_t* rec = pool + (size_t)j * 56;
+    ExpandedKey vrf;
+    for (int w = 0; w < 8; w++) {
+      vrf.a[w] = rec[8 + w];
+      vrf.prefix[w] = rec[16 + w];
+      vrf.pk[w] = rec[24 + w];
+    }
+    const uint64_t s = slot0 + i;
+    slot[i] = s;
+    uint32_t h[8], ae[8], al[8], pe[20], pl[20];
+    mkseed_hash(h, s, eta0 ? e0 : nullptr);
+    for (int k = 0; k < 8; k++) {
+      ae[k] = h[k] ^ kSeedEta[k];
+      al[k] = h[k] ^ kSeedL[k];
+    }
+    vrf03_prove_lane(pe, vrf, ae, lane, btab);
+    vrf03_prove_lane(pl, vrf, al, lane, btab);
+    st_n(eta_alpha + 32 * i, ae, 2);
+    st_n(leader_alpha + 32 * i, al, 2);
+    st_n(eta_proof + 80 * i, pe, 5);
+    st_n(leader_proof + 80 * i, pl, 5);
+    vrf_output_of(eta_out + 64 * i, pe);
+    vrf_output_of(lead_out + 64 * i, pl);
+  }
+}
 
 // Raw wire headers (#6.24(bytes .cbor [header_body, kes_sig])) consistent with
 // a synthesised SoA batch, for the raw-CBOR -> verdict bench leg and tests:
@@ -464,6 +526,20 @@ int ouro_synth_headers(size_t n, uint64_t first, int npools, const uint8_t* body
                      nodes, body_tmpl, body_len, issuer_vk, vrf_vk, eta_proof, leader_proof,
                      eta_alpha, leader_alpha, hot_vk, counter, c0, sigma, kes_t, kes_sig, body,
                      body_off, body_lens, g_ctx.scratch, g_ctx.btab);
+  return done();
+}
+
+// the node configuration (k_synth_seeded) of a batch ouro_synth_headers made
+// with the same n, first, npools, pool; eta0 a device pointer or NULL
+int ouro_synth_seeded(size_t n, uint64_t first, int npools, const uint32_t* pool, uint64_t slot0,
+                      const uint8_t* eta0, uint64_t* slot, uint8_t* eta_alpha,
+                      uint8_t* leader_alpha, uint8_t* eta_proof, uint8_t* leader_proof,
+                      uint8_t* eta_out, uint8_t* lead_out) {
+  if (npools <= 0) return -3;
+  if (prepare(n)) return -2;
+  hipLaunchKernelGGL(k_synth_seeded, dim3(grid_for(n)), dim3(kBlock), 0, 0, n, first, npools,
+                     pool, slot0, eta0, slot, eta_alpha, leader_alpha, eta_proof, leader_proof,
+                     eta_out, lead_out, g_ctx.scratch, g_ctx.btab);
   return done();
 }
 

@@ -386,6 +386,13 @@ OURO_HD inline uint32_t vrf_finish_split(Slot res, int which, const uint32_t pi[
   return ok ? (which ? 0x08u : 0x04u) : 0u;
 }
 
+// The App. B.3 flag bits of a header (include/ouro_verify.h
+// OURO_HDR_*_S_UNREDUCED): s = pi[48..80) not below L, from the bytes alone
+OURO_FI uint32_t hdr_s_bits(const uint32_t pie[20], const uint32_t pil[20]) {
+  return (sc_is_canonical(pie + 12) ? 0u : OURO_HDR_ETA_S_UNREDUCED) |
+         (sc_is_canonical(pil + 12) ? 0u : OURO_HDR_LEADER_S_UNREDUCED);
+}
+
 // ---- per-header drivers (the kernels' bodies; host-testable) -------------
 OURO_FI void ld_words(uint32_t* w, const uint8_t* p, int n16) {
 #pragma unroll
@@ -540,6 +547,7 @@ OURO_HD inline void hdr_finish_item_split(const ouro_tpraos_batch& b, size_t i, 
   for (int which = 0; which < 2; which++) {
     uint32_t pi[20], beta[16];
     ld_words(pi, (which ? b.leader_proof : b.eta_proof) + 80 * i, 5);
+    if (!sc_is_canonical(pi + 12)) v |= which ? OURO_HDR_LEADER_S_UNREDUCED : OURO_HDR_ETA_S_UNREDUCED;
     const uint32_t bit = vrf_finish_split(res, which, pi, beta);
     v |= bit | hdr_claim_bit(b, i, opts, which, bit != 0, beta);
     if (!which) hdr_eta_nonce(b, i, opts, beta);
@@ -555,7 +563,7 @@ OURO_HD inline void hdr_finish_item(const ouro_tpraos_batch& b, size_t i, uint32
   uint32_t pie[20], pil[20], be[16], bl[16];
   ld_words(pie, b.eta_proof + 80 * i, 5);
   ld_words(pil, b.leader_proof + 80 * i, 5);
-  const uint32_t v = hdr_finish(res, tmp, pie, pil, be, bl);
+  const uint32_t v = hdr_finish(res, tmp, pie, pil, be, bl) | hdr_s_bits(pie, pil);
   if (beta_eta) st_words(beta_eta + 64 * i, be, 4);
   if (beta_leader) st_words(beta_leader + 64 * i, bl, 4);
   verdict[i] = (uint8_t)v;

@@ -382,8 +382,7 @@ __device__ __forceinline__ int32_t vrf_gamma_beta_wide(uint32_t beta[16], ge_p2&
 }
 
 // The second of a VRF's V and Gamma cores to arrive: V = [s]H + (-[c]Gamma)
-// from the record, H and V encoded with one inversion; resets the VRF's
-// counter (kLatCtr + 1 + which)
+// from the record, H and V encoded with one inversion
 __device__ __forceinline__ void vrf_combine_encode(Slot res, int which) {
   const int ptH = which ? kPtHl : kPtHe, ptV = which ? kPtVl : kPtVe;
   const ge_p2 H = ld_point_at(res + ptH * kPtWords);
@@ -398,18 +397,37 @@ __device__ __forceinline__ void vrf_combine_encode(Slot res, int which) {
   if ((threadIdx.x & 63u) == 0) {
     st_words8(res + kLatEnc + 8 * (3 * which + 0), Henc);
     st_words8(res + kLatEnc + 8 * (3 * which + 2), Venc);
-    stg1(res.word(kLatCtr + 1 + which), 0);
   }
 }
 
 // Arrival at a counter of `parties` waves: this wave's record stores are
 // released, the counter bumped; true for the last party (then acquired).
-__device__ __forceinline__ bool arrive_last(int32_t* ctr, uint32_t parties = kLatCores) {
+// The counter word is tagged with the launch's generation (gen, 28 bits,
+// never 0: bits 4..31; the arrivals in bits 0..3): an arrival that finds
+// another generation's tag starts the count afresh, so a counter left
+// mid-count by an earlier launch that never completed (or a zeroed one) can
+// never make a header finish early with that launch's record contents --
+// every core rewrites its record fields before it arrives.
+__device__ __forceinline__ bool arrive_last(int32_t* ctr, uint32_t gen,
+                                            uint32_t parties = kLatCores) {
   __threadfence();
-  uint32_t old = 0;
-  if ((threadIdx.x & 63u) == 0) old = atomicAdd(reinterpret_cast<unsigned int*>(ctr), 1u);
-  old = (uint32_t)__builtin_amdgcn_readlane((int)old, 0);
-  if (old != parties - 1) return false;
+  uint32_t mine = 0;
+  if ((threadIdx.x & 63u) == 0) {
+    unsigned int* c = reinterpret_cast<unsigned int*>(ctr);
+    const uint32_t tag = (gen & 0x0fffffffu) << 4;
+    uint32_t cur = __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (;;) {
+      const uint32_t want = (cur & ~0xfu) == tag ? cur + 1u : (tag | 1u);
+      const uint32_t prev = atomicCAS(c, cur, want);
+      if (prev == cur) {
+        mine = want & 0xfu;
+        break;
+      }
+      cur = prev;
+    }
+  }
+  mine = (uint32_t)__builtin_amdgcn_readlane((int)mine, 0);
+  if (mine != parties) return false;
   __threadfence();
   return true;
 }
@@ -465,7 +483,7 @@ __device__ __forceinline__ void ed_scalars_item(Slot e, const uint32_t sig[16], 
   }
 }
 // [|c0|](+-A) + [c1](-R) + [b]B == O from the record (the ed25519_verify_wide
-// equation); resets the counter
+// equation)
 __device__ __forceinline__ bool ed_chain(Slot e, const uint16_t* bw) {
   const Lanes L = lanes();
   uint32_t c0[8], c1[8], b[8];
@@ -477,7 +495,6 @@ __device__ __forceinline__ bool ed_chain(Slot e, const uint16_t* bw) {
   const ge_p3 negA{ld_fe(e + 28), ld_fe(e + 40), ld_fe(e + 52), ld_fe(e + 64)};
   const ge_p3 negR{ld_fe(e + 76), ld_fe(e + 88), ld_fe(e + 100), ld_fe(e + 112)};
   const bool ok = ldg1(e.word(124)) != 0;
-  if ((threadIdx.x & 63u) == 0) stg1(e.word(125), 0);
   const int32_t d2 = d2_wide(L);
   TabW t1, t2;
   tab_build(t1, pw_from_p3(c0_neg ? ge_p3_neg(negA) : negA, L), d2, L);
@@ -510,7 +527,7 @@ __device__ __forceinline__ void eta_nonce_candidates(const ouro_tpraos_batch& b,
 // The tail of header i on the last core's wave: both VRFs at once (lanes
 // 0..31 the eta VRF, 32..63 the leader VRF) -- challenge check from the
 // record's encodings, beta, claimed-output bits, the eta nonce -- and the
-// verdict; the counter is reset for the next launch.  Same bits and outputs
+// verdict.  Same bits and outputs
 // as k_tpraos_finish (tpraos.h vrf_finish_split).
 __device__ __forceinline__ void hdr_tail_wide(const ouro_tpraos_batch& b, size_t i, uint32_t opts,
                                               Slot res, uint8_t* verdict, uint8_t* beta_eta,
@@ -538,6 +555,7 @@ __device__ __forceinline__ void hdr_tail_wide(const ouro_tpraos_batch& b, size_t
   for (int k = 0; k < 16; k++) beta[k] = ok ? beta[k] : 0u;
   uint32_t bit = ok ? (which ? 0x08u : 0x04u) : 0u;
   bit |= hdr_claim_bit(b, i, opts, which, ok, beta);
+  if (!sc_is_canonical(pi + 12)) bit |= which ? OURO_HDR_LEADER_S_UNREDUCED : OURO_HDR_ETA_S_UNREDUCED;
   uint8_t* dst = which ? beta_leader : beta_eta;
   if ((lane & 31u) == 0 && dst) st_words(dst + 64 * i, beta, 4);
   // the eta nonce: the candidate the eta Gamma core hashed (claimed output, or
@@ -554,7 +572,6 @@ __device__ __forceinline__ void hdr_tail_wide(const ouro_tpraos_batch& b, size_t
     if (fl(kCoreOcert) & kFlagOk) v |= 0x01u;
     if (fl(kCoreKes) & kFlagOk) v |= 0x02u;
     verdict[i] = (uint8_t)v;
-    stg1(res.word(kLatCtr), 0);
   }
 }
 

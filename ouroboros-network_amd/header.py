@@ -128,7 +128,12 @@ class ShelleyHeader:
 
 
 def parse_header(raw: bytes) -> ShelleyHeader:
-    """Parse an N2N (v1: tag-24 wrapped) or Cardano HFC-wrapped Shelley-era header."""
+    """Parse an N2N (v1: tag-24 wrapped) or Cardano HFC-wrapped Shelley-era header.
+
+    CBOR-in-CBOR as the reference decodes it (ouroboros-network/src/Ouroboros/
+    Network/Block.hs:509-514): the tag-24 byte string is definite and inside
+    `raw`; [header_body, kes_sig] is parsed from its payload alone and must end
+    where the payload ends; nothing may follow the header."""
     buf = bytes(raw)
     era, i = 1, 0
     mt, arg, j = _head(buf, 0)
@@ -141,13 +146,20 @@ def parse_header(raw: bytes) -> ShelleyHeader:
     if mt != 6 or arg != 24:
         raise CBORError("expected #6.24 wrapped header")
     mt, arg, k = _head(buf, j)
-    if mt != 2:
-        raise CBORError("expected CBOR-in-bytes")
+    if mt != 2 or arg < 0:
+        raise CBORError("expected definite CBOR-in-bytes")
+    if k + arg > len(buf):
+        raise CBORError("truncated")
+    if k + arg != len(buf):
+        raise CBORError("trailing bytes after the header")
+    buf = buf[:k + arg]  # (the same length: the payload bounds every parse below)
     inner_start = k
     top = array_items(buf, inner_start)
     if len(top) != 2:
         raise CBORError("header must be [body, sig]")
-    (b0, b1), (s0, _s1) = top
+    (b0, b1), (s0, s1) = top
+    if s1 != k + arg:
+        raise CBORError("trailing bytes in CBOR-in-CBOR")
     f = array_items(buf, b0)
     if len(f) != 15:
         raise CBORError(f"header body must have 15 fields, got {len(f)}")

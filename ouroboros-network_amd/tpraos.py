@@ -28,6 +28,9 @@ HDR_ETA_CLAIM_OK = _native.HDR_ETA_CLAIM_OK
 HDR_LEADER_CLAIM_OK = _native.HDR_LEADER_CLAIM_OK
 HDR_ALL_OK = _native.HDR_ALL_OK
 HDR_STRICT_OK = _native.HDR_STRICT_OK
+HDR_ETA_S_UNREDUCED = _native.HDR_ETA_S_UNREDUCED
+HDR_LEADER_S_UNREDUCED = _native.HDR_LEADER_S_UNREDUCED
+HDR_S_UNREDUCED = _native.HDR_S_UNREDUCED
 
 # field name -> (dtype, row width or None for scalars)
 LAYOUT = {
@@ -264,6 +267,12 @@ class HeaderPlan:
         nonce, self._nonce = getattr(self, "_nonce", None), None
         return tuple(out) + (nonce,) if nonce is not None else out
 
+    def debug_poison(self) -> None:
+        """TEST HOOK (ouro_tpraos_plan_debug_poison): leave the plan's arrival
+        counters as a launch cut off one arrival short of each finish would."""
+        _native.check(self._lib.ouro_tpraos_plan_debug_poison(self._p),
+                      "ouro_tpraos_plan_debug_poison")
+
     def close(self):
         if self._p:
             self._lib.ouro_tpraos_plan_destroy(self._p)
@@ -276,10 +285,12 @@ class HeaderPlan:
             pass
 
 
-def first_invalid(verdict: np.ndarray, required: int = HDR_ALL_OK) -> Optional[int]:
+def first_invalid(verdict: np.ndarray, required: int = HDR_ALL_OK,
+                  s_mode: str = "reduce") -> Optional[int]:
     """Index of the first header failing any required CRYPTO check (HDR_ALL_OK
     for the reference's ref2020 semantics, HDR_STRICT_OK to also demand the
-    claimed VRF outputs) -- where the reference's sequential
+    claimed VRF outputs; s_mode="strict" also rejects a VRF proof whose s is
+    not below L, the HDR_*_S_UNREDUCED bits) -- where the reference's sequential
     HeaderStateHistory fold stops as far as the crypto goes.
 
     The verdict bits cover the signatures and proofs only.  The host fold must
@@ -288,7 +299,12 @@ def first_invalid(verdict: np.ndarray, required: int = HDR_ALL_OK) -> Optional[i
     Integrity.hs:38-44), the operational-certificate counter, the VRF key hash
     against the pool's registration, and the leader threshold
     (leader.check_leader_value on the CLAIMED leader output)."""
-    bad = np.nonzero((verdict & required) != required)[0]
+    if s_mode not in ("reduce", "strict"):
+        raise ValueError("s_mode: reduce or strict")
+    bad = (verdict & required) != required
+    if s_mode == "strict":
+        bad |= (verdict & HDR_S_UNREDUCED) != 0
+    bad = np.nonzero(bad)[0]
     return int(bad[0]) if bad.size else None
 
 

@@ -11,6 +11,11 @@ Claimed-output semantics: ``verify_vrf`` in mode
 ``"ref2020"`` (default, as recalled for cardano-base@4251c0bb) checks the proof
 only; ``"strict"`` additionally requires the claimed output to equal the
 proof's output.  ``output_from_proof`` is ``crypto_vrf_ietfdraft03_proof_to_hash``.
+
+The range of the proof's s: ``s_mode="reduce"`` (default,
+the fork as recalled: s reduced mod L) or ``"strict"`` (s >= L rejected,
+OURO_VRF_STRICT_S).  Which one cardano-crypto-praos uses is unpinned -- no
+reference fixture has s >= L -- so both are offered.
 """
 from __future__ import annotations
 
@@ -26,12 +31,24 @@ SIZE_PROOF = 80
 SIZE_OUTPUT = 64
 
 
+S_MODES = {"reduce": 0, "strict": _native.VRF_STRICT_S}
+
+
+def _s_flags(s_mode: str) -> int:
+    if s_mode not in S_MODES:
+        raise ValueError(f"s_mode: one of {sorted(S_MODES)}")
+    return S_MODES[s_mode]
+
+
 class PraosVRF:
     @staticmethod
-    def verify(vk: bytes, msg: bytes, proof: bytes):
+    def verify(vk: bytes, msg: bytes, proof: bytes, s_mode: str = "reduce"):
         """crypto_vrf_ietfdraft03_verify: the 64-byte output, or None."""
         if len(vk) != SIZE_VERKEY or len(proof) != SIZE_PROOF:
             return None
+        if _s_flags(s_mode):
+            ok, beta = PraosVRF.verify_batch([vk], [msg], [proof], s_mode=s_mode)
+            return bytes(beta[0]) if ok[0] else None
         out = ctypes.create_string_buffer(SIZE_OUTPUT)
         rc = _native.load().ouro_vrf03_verify(out, vk, proof, msg, len(msg))
         if rc == _native.OURO_OK:
@@ -42,10 +59,11 @@ class PraosVRF:
         return None
 
     @staticmethod
-    def verify_vrf(ctx, vk: bytes, msg: bytes, certified, mode: str = "ref2020") -> bool:
+    def verify_vrf(ctx, vk: bytes, msg: bytes, certified, mode: str = "ref2020",
+                   s_mode: str = "reduce") -> bool:
         """``verifyVRF () vk msg (output, proof)``."""
         output, proof = certified
-        beta = PraosVRF.verify(vk, msg, proof)
+        beta = PraosVRF.verify(vk, msg, proof, s_mode=s_mode)
         if beta is None:
             return False
         return True if mode == "ref2020" else bytes(output) == beta
@@ -66,8 +84,9 @@ class PraosVRF:
         return None
 
     @staticmethod
-    def verify_batch(vks, alphas, proofs):
+    def verify_batch(vks, alphas, proofs, s_mode: str = "reduce"):
         """Returns (valid bool array, outputs (n, 64) uint8; zero rows where invalid)."""
+        flags = _s_flags(s_mode)
         vk = as_rows(vks, SIZE_VERKEY, "vk")
         pf = as_rows(proofs, SIZE_PROOF, "proof")
         buf, off, ln = msgs_arg(alphas)
@@ -77,9 +96,9 @@ class PraosVRF:
         ver = np.zeros(n, dtype=np.uint8)
         beta = np.zeros((n, SIZE_OUTPUT), dtype=np.uint8)
         if n:
-            rc = _native.load().ouro_vrf03_verify_batch(
-                n, ptr(vk), ptr(pf), ptr(buf), ptr(off), ptr(ln), ptr(beta), ptr(ver))
-            _native.check(rc, "ouro_vrf03_verify_batch")
+            rc = _native.load().ouro_vrf03_verify_batch_flags(
+                n, ptr(vk), ptr(pf), ptr(buf), ptr(off), ptr(ln), ptr(beta), ptr(ver), flags)
+            _native.check(rc, "ouro_vrf03_verify_batch_flags")
         return ver.astype(bool), beta
 
 

@@ -4,11 +4,17 @@
  * ChainSync client thread per peer plus ChainDB's chain-selection thread
  * (ouroboros-consensus/src/Ouroboros/Consensus/Network/NodeToNode.hs:173-176),
  * so T threads here interleave single-item calls (the libsodium /
- * cardano-crypto-praos ABI and its crypto_vrf_* aliases) with batch calls on
- * their own data, each result checked against the CPU oracle computed up
- * front.  Test infrastructure: links the product library and the oracle.
+ * cardano-crypto-praos ABI, the crypto_vrf_* names through the opt-in shim
+ * lib/libouro_vrf_shim.so) with batch calls on their own data, each result
+ * checked against the CPU oracle computed up front.  Then CHURN short-lived
+ * threads, one after another, each make one batch call (GHC's FFI worker
+ * pool grows and shrinks like this): the per-thread context pool must hand
+ * each the context the previous one returned at its exit, so the contexts
+ * created grow by at most one.  Test infrastructure: links the product
+ * library, the shim and the oracle.
  *
- * usage: concurrency THREADS ROUNDS   -> prints "ok <calls>" or "FAIL ..."
+ * usage: concurrency THREADS ROUNDS [CHURN]
+ *        -> prints "ok <calls> <contexts created by the churn>" or "FAIL ..."
  */
 #include <pthread.h>
 #include <stdio.h>
@@ -50,6 +56,22 @@ static uint64_t rnd(uint64_t *s) {
       return NULL;                        \
     }                                     \
   } while (0)
+
+/* one Ed25519 batch call, then the thread exits (returning its context) */
+static void *short_lived(void *arg) {
+  const int lo = (int)(long)arg % (NED - 64);
+  uint64_t off[64];
+  uint32_t len[64];
+  uint8_t v[64];
+  for (int k = 0; k < 64; k++) {
+    off[k] = 32ull * (uint64_t)(lo + k);
+    len[k] = 32;
+  }
+  CHECK(ouro_ed25519_verify_batch(64, ed_pk[lo], ed_sig[lo], &ed_msg[0][0], off, len, v) == 0,
+        "short-lived batch rc\n");
+  for (int k = 0; k < 64; k++) CHECK(v[k] == ed_ok[lo + k], "short-lived %d\n", lo + k);
+  return NULL;
+}
 
 static void *worker(void *arg) {
   const int id = (int)(long)arg;
@@ -160,10 +182,19 @@ int main(int argc, char **argv) {
     pthread_join(th[t], NULL);
     total += g_calls[t];
   }
+  const int churn = argc > 3 ? atoi(argv[3]) : 0;
+  size_t before = 0, after = 0, idle = 0;
+  ouro_debug_contexts(0, &before, &idle);
+  for (int t = 0; t < churn && !g_fail; t++) {
+    pthread_t one;
+    pthread_create(&one, NULL, short_lived, (void *)(long)(7 * t));
+    pthread_join(one, NULL);
+  }
+  ouro_debug_contexts(0, &after, &idle);
   if (g_fail) {
     printf("FAIL %d\n", g_fail);
     return 1;
   }
-  printf("ok %ld\n", total);
+  printf("ok %ld %zu\n", total, after - before);
   return 0;
 }

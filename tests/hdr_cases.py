@@ -18,9 +18,18 @@ import oracle_ffi as O
 from ouroboros_network_amd import header as H
 
 GOLDEN_VRF_SEED = b"\x01" * 32
+L = 2**252 + 27742317777372353535851937790883648493
 
 
-def golden_variants(kats, stride=1, claimed=True):
+def with_s_plus_l(proof: bytes) -> bytes:
+    """The same proof with s replaced by s + L: draft-03 as the fork reads it
+    (s reduced mod L) still verifies it; a strict-s reading rejects it
+    (the OURO_HDR_*_S_UNREDUCED bits)."""
+    s = int.from_bytes(proof[48:80], "little")
+    return proof[:48] + (s + L).to_bytes(32, "little")
+
+
+def golden_variants(kats, stride=1, claimed=True, s_rows=True):
     hs = kats["headers"]
     parsed = [H.parse_header(bytes.fromhex(h["raw"])) for h in hs]
     ea = [bytes.fromhex(h["eta_alpha"]) for h in hs]
@@ -35,7 +44,40 @@ def golden_variants(kats, stride=1, claimed=True):
             continue  # no longer decodes: the reference rejects before crypto
         ea.append(ea[0])
         la.append(la[0])
-    return H.pack(parsed, ea, la, slots_per_kes_period=100, claimed=claimed)
+    batch = H.pack(parsed, ea, la, slots_per_kes_period=100, claimed=claimed)
+    if not s_rows:
+        return batch
+    # the first golden header three more times: the eta proof's s, the
+    # leader proof's s, both, replaced by s + L
+    rows = batch.rows([0, 0, 0])
+    ep, lp = rows.eta_proof.copy(), rows.leader_proof.copy()
+    for r, (e, l) in enumerate(((1, 0), (0, 1), (1, 1))):
+        if e:
+            ep[r] = np.frombuffer(with_s_plus_l(ep[r].tobytes()), np.uint8)
+        if l:
+            lp[r] = np.frombuffer(with_s_plus_l(lp[r].tobytes()), np.uint8)
+    extra = rows.with_(eta_proof=ep, leader_proof=lp)
+    return concat(batch, extra)
+
+
+def concat(a, b):
+    """Rows of a then rows of b (b's body offsets rebased past a's body)."""
+    from dataclasses import fields
+
+    kw = {}
+    for f in fields(a):
+        x, y = getattr(a, f.name), getattr(b, f.name)
+        if f.name == "body":
+            kw[f.name] = np.concatenate([x, y])
+        elif f.name == "body_off":
+            kw[f.name] = np.concatenate([x, y + np.uint64(a.body.size)])
+        elif f.name == "epoch_nonce":
+            kw[f.name] = x
+        elif x is None:
+            kw[f.name] = None
+        else:
+            kw[f.name] = np.concatenate([x, y])
+    return type(a)(**kw)
 
 
 def forge_claims(batch, rng, frac=4):

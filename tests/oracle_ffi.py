@@ -45,6 +45,7 @@ def lib(path: str = None) -> ctypes.CDLL:
             "orc_ed25519_verify_byron": (I, [P, P, SZ, P]),
             "orc_elligator2_from_uniform": (None, [P, P]),
             "orc_vrf03_verify": (I, [P, P, P, P, SZ]),
+            "orc_vrf03_verify_mode": (I, [P, P, P, P, SZ, I]),
             "orc_vrf03_proof_to_hash": (I, [P, P]),
             "orc_vrf03_keypair": (None, [P, P, P]),
             "orc_vrf03_prove": (I, [P, P, P, SZ]),
@@ -224,6 +225,25 @@ def tpraos_verify_batch(hb, threads: int = 8):
     bl = np.zeros((n, 64), np.uint8)
     lib().orc_tpraos_verify_batch(ctypes.addressof(s), p(verdict), p(be), p(bl), threads)
     return verdict, be, bl
+
+
+def tpraos_verify_batch_nonce(hb, threads: int = 8):
+    """tpraos_verify_batch plus the eta_nonce rows (n, 32)."""
+    n = len(hb)
+    en = np.zeros((n, 32), np.uint8)
+    s = hb.c_struct(en)
+    verdict = np.zeros(n, np.uint8)
+    be = np.zeros((n, 64), np.uint8)
+    bl = np.zeros((n, 64), np.uint8)
+    lib().orc_tpraos_verify_batch(ctypes.addressof(s), p(verdict), p(be), p(bl), threads)
+    return verdict, be, bl, en
+
+
+def vrf_verify_mode(pk: bytes, proof: bytes, alpha: bytes, strict_s: bool):
+    """orc_vrf03_verify_mode: the output, or None (strict_s: s >= L rejected)."""
+    out = ctypes.create_string_buffer(64)
+    rc = lib().orc_vrf03_verify_mode(out, pk, proof, alpha, len(alpha), int(strict_s))
+    return out.raw if rc == 0 else None
 
 
 def sodium():

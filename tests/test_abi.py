@@ -84,18 +84,63 @@ def test_struct_offsets_match_the_c_compiler(tmp_path):
         assert getattr(_native.TPraosBatch, name).offset == c_off == orc_off, name
 
 
-def test_library_exports_the_vrf_aliases():
+SHIM = os.path.join(ROOT, "ouroboros-network_amd", "lib", "libouro_vrf_shim.so")
+
+
+def test_vrf_names_only_in_the_opt_in_shim():
     """crypto_vrf_ietfdraft03_{verify,proof_to_hash} and crypto_vrf_{verify,
-    proof_to_hash}: the cardano-crypto-praos names PraosVRF binds, exported so
-    a link-order drop-in needs no Haskell edit."""
+    proof_to_hash} -- the cardano-crypto-praos names PraosVRF binds -- come
+    from the separate lib/libouro_vrf_shim.so a maintainer links on purpose
+    (INTEGRATION.md §1), never from the product library, so linking the
+    product cannot take over the fork's symbols by accident."""
+    import subprocess
+
     from ouroboros_network_amd import _native
 
-    lib = ctypes.CDLL(LIB)
+    syms = subprocess.run(["nm", "-D", "--defined-only", LIB], check=True, capture_output=True,
+                          text=True).stdout
+    shim = subprocess.run(["nm", "-D", "--defined-only", SHIM], check=True, capture_output=True,
+                          text=True).stdout
     for name in _native.VRF_ALIASES:
-        assert hasattr(lib, name), name
+        assert f" {name}\n" not in syms, name
+        assert f" T {name}\n" in shim, name
     text = open(os.path.join(ROOT, "include", "ouro_verify.h")).read()
     for name in _native.VRF_ALIASES:
         assert name in text
+
+
+_SHIM_CALL = """
+import ctypes, sys
+ctypes.CDLL(sys.argv[1], mode=ctypes.RTLD_GLOBAL)
+shim = ctypes.CDLL(sys.argv[2])
+out = ctypes.create_string_buffer(64)
+print(shim.crypto_vrf_ietfdraft03_verify(out, bytes(32), bytes(80), b"x", 1), flush=True)
+"""
+
+
+@pytest.mark.parametrize("mode", ["default", "invalid"])
+def test_shim_never_reports_a_device_error_as_an_invalid_proof(mode):
+    """PraosVRF reads any nonzero as 'invalid proof'.  With no device the
+    product returns an error code; the shim must abort (default) rather than
+    pass it on, or return -1 only when OURO_SHIM_ON_ERROR=invalid says so."""
+    import subprocess
+    import sys
+
+    import torch
+
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is present")
+    env = dict(os.environ)
+    env.pop("OURO_SHIM_ON_ERROR", None)
+    if mode == "invalid":
+        env["OURO_SHIM_ON_ERROR"] = "invalid"
+    r = subprocess.run([sys.executable, "-c", _SHIM_CALL, LIB, SHIM], capture_output=True,
+                       text=True, env=env, timeout=120)
+    if mode == "default":
+        assert r.returncode == -6, (r.returncode, r.stdout, r.stderr)  # SIGABRT
+        assert "aborting rather than reporting a valid proof as invalid" in r.stderr
+    else:
+        assert r.returncode == 0 and r.stdout.strip() == "-1", (r.stdout, r.stderr)
 
 
 def test_no_device_is_an_error_not_an_accept():

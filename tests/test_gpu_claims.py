@@ -127,3 +127,33 @@ def test_nonce_fold_from_device_outputs(gpu_lib, kats):
     for fsne in (int(slots[len(slots) // 2]) + 10, 2**63):
         got = nonce_fold(en, slots, fsne, 7, None, b"\x11" * 32)
         assert got == ON.fold(None, b"\x11" * 32, [bytes(r) for r in en], slots, fsne, 7)
+
+
+def test_plan_counters_from_cut_off_launch(gpu_lib, kats):
+    """A plan whose arrival counters were left mid-count by an earlier launch
+    that never completed (simulated: ouro_tpraos_plan_debug_poison leaves every
+    counter one arrival short of its finish, tagged with the last launch's
+    generation) must still give the oracle's verdicts and outputs on the next
+    window: each launch counts in its own generation (wide_cores.h
+    arrive_last), so no header finishes early on the stale counts -- and no
+    verdict carries an earlier window's result.  The second window holds other
+    headers than the first, so a stale record would show."""
+    from ouroboros_network_amd.tpraos import HeaderPlan
+
+    rng = np.random.default_rng(41)
+    forged, _ = HC.forge_claims(HC.golden_variants(kats, stride=3), rng)
+    first, second = forged.slice(0, 64), forged.slice(64, 128)
+    w1, w2 = _oracle(first), _oracle(second)
+    plan = HeaderPlan(64, 64 * 1400)
+    try:
+        _check(plan.run(first, nonce=True), w1)
+        for _ in range(3):
+            plan.debug_poison()
+            _check(plan.run(second, nonce=True), w2)
+            plan.debug_poison()
+            _check(plan.run(first, nonce=True), w1)
+        # and a partial window after a poisoned full one
+        plan.debug_poison()
+        _check(plan.run(second.slice(5, 17), nonce=True), tuple(a[5:17] for a in w2))
+    finally:
+        plan.close()

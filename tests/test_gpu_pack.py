@@ -178,6 +178,11 @@ def test_device_slicer_matches_host_slicer(gpu_lib, kats):
                 m[pos] ^= x
                 raws.append(bytes(m))
         raws += [g[:k] for k in range(0, len(g), 7)]
+    # CBOR-in-CBOR bounds: rejected alike on host and device
+    import test_pack as TP
+
+    for g in (golden[0], golden[3]):
+        raws += list(TP._cbor_in_cbor_cases(g).values()) + [TP._short_eta_proof(g)]
     ln = np.array([len(r) for r in raws], np.uint32)
     off = np.zeros(len(raws), np.uint64)
     off[1:] = np.cumsum(ln[:-1], dtype=np.uint64)

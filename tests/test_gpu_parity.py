@@ -107,17 +107,28 @@ def test_vrf_draft03_vectors(small_path, gpu_lib, kats):
         assert PraosVRF.output_from_proof(bytes.fromhex(v["pi"])).hex() == v["beta"]
 
 
-def test_vrf_edge_cases(small_path, gpu_lib):
+@pytest.mark.parametrize("s_mode", ["reduce", "strict"])
+def test_vrf_edge_cases(small_path, gpu_lib, s_mode):
+    """Both readings of the proof's s: reduced mod L (the
+    default) and strict (s >= L rejected, OURO_VRF_STRICT_S); the s + L cases
+    split them."""
     from ouroboros_network_amd import PraosVRF
 
     cases = vrf_edge_cases()
     ok, beta = PraosVRF.verify_batch([c[0] for c in cases], [c[2] for c in cases],
-                                     [c[1] for c in cases])
+                                     [c[1] for c in cases], s_mode=s_mode)
+    split = 0
     for (pk, pi, a), o, b in zip(cases, ok, beta):
-        w = O.vrf_verify(pk, pi, a)
+        w = O.vrf_verify_mode(pk, pi, a, strict_s=s_mode == "strict")
         assert o == (w is not None)
-        if w is not None:
-            assert bytes(b) == w
+        assert bytes(b) == (w if w is not None else bytes(64))
+        split += (O.vrf_verify_mode(pk, pi, a, False) is not None) != \
+            (O.vrf_verify_mode(pk, pi, a, True) is not None)
+    assert split >= 4  # the s + L rows of the four valid proofs
+    # the single-item form agrees
+    pk, pi, a = next(c for c in cases if int.from_bytes(c[1][48:], "little") >= HC.L)
+    got = PraosVRF.verify(pk, a, pi, s_mode=s_mode)
+    assert got == O.vrf_verify_mode(pk, pi, a, strict_s=s_mode == "strict")
 
 
 def test_kes_batch_matches_oracle(gpu_lib):

@@ -83,7 +83,11 @@ def test_every_byte_corruption_matches_python(golden):
     assert_same(raws, py, pk)
     # the corruptions exercise both outcomes and several rejection classes
     assert 0 < int((pk.status == H.PACK_OK).sum()) < len(raws)
-    assert {H.PACK_ECBOR, H.PACK_ESHAPE, H.PACK_ESIZE} <= set(pk.status.tolist())
+    # (a single byte can no longer give ESIZE: a field of another length moves
+    # the end of [header_body, kes_sig] off the payload's end, which the
+    # reference rejects as CBOR first; test_cbor_in_cbor_bounds_as_the_reference
+    # makes a consistent one)
+    assert {H.PACK_ECBOR, H.PACK_ESHAPE} <= set(pk.status.tolist())
 
 
 def test_every_truncation_rejected(golden):
@@ -92,6 +96,60 @@ def test_every_truncation_rejected(golden):
         pk = c_pack(raws)
         assert (pk.status != H.PACK_OK).all()
         assert_same(raws, py_pack(raws), pk)
+
+
+def _cbor_in_cbor_cases(g):
+    """Headers the reference's CBOR-in-CBOR decoding rejects
+    (ouroboros-network/src/Ouroboros/Network/Block.hs:509-514): payload
+    length not matching [header_body, kes_sig], trailing bytes inside the
+    payload or after the header, an indefinite byte string."""
+    at = g.index(bytes.fromhex("d81859")) + 3      # the 2-byte payload length
+    ln = int.from_bytes(g[at:at + 2], "big")
+    pre, payload = g[:at], g[at + 2:]
+    assert len(payload) == ln
+    enc = lambda n: n.to_bytes(2, "big")  # noqa: E731
+    out = {
+        "length_minus_1": pre + enc(ln - 1) + payload,
+        "length_plus_1": pre + enc(ln + 1) + payload,
+        "trailing_in_payload": pre + enc(ln + 1) + payload + b"\x00",
+        "trailing_after_header": g + b"\x00",
+        "trailing_after_header_ff": g + b"\xff\xff",
+        # the payload as an indefinite byte string of one chunk
+        "indefinite_bytes": pre[:-1] + b"\x5f" + b"\x59" + enc(ln) + payload + b"\xff",
+    }
+    return out
+
+
+def _short_eta_proof(g):
+    """A well-formed header whose eta proof has 79 bytes (the payload length
+    adjusted): CBOR fine, a crypto field of the wrong size (ESIZE)."""
+    at = g.index(bytes.fromhex("d81859")) + 3
+    ln = int.from_bytes(g[at:at + 2], "big")
+    payload = g[at + 2:]
+    e = payload.index(b"\x58\x40")          # the eta certificate's output
+    q = e + 2 + 64                           # its proof's head
+    assert payload[q:q + 2] == b"\x58\x50"
+    payload = payload[:q] + b"\x58\x4f" + payload[q + 2:q + 2 + 79] + payload[q + 2 + 80:]
+    return g[:at] + (ln - 1).to_bytes(2, "big") + payload
+
+
+def test_cbor_in_cbor_bounds_as_the_reference(golden):
+    """the slicers parse the tag-24 payload alone and reject what
+    the reference's decoder rejects -- Python, host C and (tests/test_gpu_pack)
+    device C alike."""
+    for g in (golden[0], golden[3]):  # unwrapped, HFC-wrapped
+        cases = _cbor_in_cbor_cases(g)
+        raws = list(cases.values())
+        py = py_pack(raws)
+        for name, p in zip(cases, py):
+            assert p is None, f"Python accepts {name}"
+        pk = c_pack(raws)
+        for name, st in zip(cases, pk.status):
+            assert st != H.PACK_OK, f"C accepts {name}"
+        assert_same(raws, py, pk)
+        short = _short_eta_proof(g)
+        assert py_pack([short]) == [None]
+        assert c_pack([short]).status[0] == H.PACK_ESIZE
 
 
 def test_byron_era_and_wrappers(golden):

@@ -32,6 +32,27 @@ def test_shard_range_covers_exactly():
                 assert b == c and a <= b
 
 
+def test_bench_step_shards_is_configs3_strong_by_default():
+    """bench.py --gpus N > 1 measures configs[3] as written: ONE batch of
+    1,048,576 headers per step cut into N/G contiguous shards (SURVEY.md
+    §8(d)); --weak keeps 1,048,576 per GPU; N = 1 is the plain 1M batch."""
+    import bench
+
+    for world in (2, 4, 8):
+        spans = [bench.step_shards(world, r, 1 << 20, -1, False) for r in range(world)]
+        assert all(s[0] for s in spans)                       # strong
+        assert all(s[3] == 1 << 20 for s in spans)            # global batch
+        assert [s[1] for s in spans] == [(1 << 20) // world] * world
+        assert [s[2] for s in spans] == [r * (1 << 20) // world for r in range(world)]
+        weak = [bench.step_shards(world, r, 1 << 20, -1, True) for r in range(world)]
+        assert all(not s[0] and s[1] == 1 << 20 and s[3] == world << 20 for s in weak)
+        assert [s[2] for s in weak] == [r << 20 for r in range(world)]
+    assert bench.step_shards(1, 0, 1 << 20, -1, False) == (False, 1 << 20, 0, 1 << 20)
+    # an explicit global batch that does not divide evenly: ceil(N/G), contiguous
+    spans = [bench.step_shards(3, r, 0, 1000, False) for r in range(3)]
+    assert [(s[1], s[2]) for s in spans] == [(334, 0), (334, 334), (332, 668)]
+
+
 def _worker(rank, world, port, out_dir, use_gpu=False):
     import sys
 

@@ -11,7 +11,7 @@ for attempt in 1 2 3 4; do
   tail -3 /tmp/gpurun_last.out
   st=$(python3 -c "import json; d=json.load(open('gpurun_out/.last_call.json')); print(d.get('status'), d.get('run_s'))" 2>/dev/null)
   case "$st" in
-    transient*) sleep $((30 * attempt)); continue ;;
+    "transient 0"|"transient 0.0"|"transient None") sleep $((30 * attempt)); continue ;;
   esac
   exit $rc
 done
