@@ -845,6 +845,23 @@ def load_pmc_traffic():
         "traffic_matches_source": d.get("source_hash") == source_hash()}
 
 
+def load_component_traffic():
+    """HBM bytes per item of the standalone kernels from the committed
+    component PMC run (profiles/pmc_traffic_components.json,
+    tools/collect_components.py), with whether it measured THIS source."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic_components.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+    except (OSError, ValueError):
+        return {}
+    meta = {"traffic_tag": d.get("tag"), "traffic_source_hash": d.get("source_hash"),
+            "traffic_matches_source": d.get("source_hash") == source_hash()}
+    return {leg: {"traffic_per_item": round(v["hbm_bytes_per_item"], 1), "traffic_kernel": v["kernel"],
+                  **meta}
+            for leg, v in d.items() if isinstance(v, dict) and "hbm_bytes_per_item" in v}
+
+
 def single_item_leg(ed, hdr, iters: int = 300):
     """Per-call wall latency of the ABI-identical single-item symbols (each a
     one-item GPU batch: H2D, launch, D2H) next to the reference's own
@@ -1166,6 +1183,12 @@ def main():
                     out[k] = val
             except Exception as e:  # noqa: BLE001
                 out["components_error"] = str(e)
+            # each standalone kernel's HBM traffic per item from its committed
+            # rocprofv3 PMC run (profiles/r03*/components), stamped with the
+            # source hash it measured
+            for leg, tr in load_component_traffic().items():
+                if leg in out and isinstance(out[leg], dict) and "error" not in out[leg]:
+                    out[leg]["traffic"] = tr
             if ed is not None and world == 1:
                 try:
                     out["single_item"] = single_item_leg(ed, hdr)

@@ -110,20 +110,34 @@ int ouro_vrf03_verify(unsigned char *output, const unsigned char *pk,
  * Shelley/Ledger/TPraos.hs:40).  Does not verify the proof. */
 int ouro_vrf03_proof_to_hash(unsigned char *output, const unsigned char *proof);
 
-/* The library also exports the cardano-crypto-praos names themselves, with
- * these exact signatures, so a maintainer can satisfy PraosVRF's
- * `foreign import ccall "crypto_vrf_ietfdraft03_verify"` (and the
- * version-less crypto_vrf_* names, which the fork maps to draft-03) by link
- * order instead of editing the Haskell:
- *   int crypto_vrf_ietfdraft03_verify(unsigned char *output, const unsigned char *pk,
- *                                     const unsigned char *proof, const unsigned char *m,
- *                                     unsigned long long mlen);
- *   int crypto_vrf_ietfdraft03_proof_to_hash(unsigned char *output,
- *                                            const unsigned char *proof);
- *   int crypto_vrf_verify(...);         same as crypto_vrf_ietfdraft03_verify
- *   int crypto_vrf_proof_to_hash(...);  same as crypto_vrf_ietfdraft03_proof_to_hash
- * Ed25519 is NOT exported under libsodium's name (libsodium itself is still
- * linked for key generation); use --defsym for it if wanted. */
+/* Routing of single items.  Each single-item call above is ONE GPU round
+ * trip (H2D, one wave, D2H): about 220 us for Ed25519 and 420 us for a VRF
+ * proof on MI355X, against about 32 us for libsodium on one host core
+ * (bench.py "single_item").  A caller with one item at a time -- the
+ * reference's per-header OCERT / OVERLAY calls as they are today -- should
+ * keep libsodium / the cardano-crypto-praos fork for n = 1; windows of
+ * headers (ChainSync's 64-300, ouro_tpraos_plan_*) and bulk batches
+ * (ouro_*_batch) are what the GPU path is for.  The names the reference's
+ * Haskell binds are therefore NOT exported by this library; two OPT-IN link
+ * shims provide them, with these exact signatures, for a maintainer who
+ * wants the drop-in by link order instead of a Haskell edit:
+ *   lib/libouro_vrf_shim.so (PraosVRF's foreign imports; the version-less
+ *   names are the fork's aliases of draft-03):
+ *     int crypto_vrf_ietfdraft03_verify(unsigned char *output, const unsigned char *pk,
+ *                                       const unsigned char *proof, const unsigned char *m,
+ *                                       unsigned long long mlen);
+ *     int crypto_vrf_ietfdraft03_proof_to_hash(unsigned char *output,
+ *                                              const unsigned char *proof);
+ *     int crypto_vrf_verify(...);         same as crypto_vrf_ietfdraft03_verify
+ *     int crypto_vrf_proof_to_hash(...);  same as crypto_vrf_ietfdraft03_proof_to_hash
+ *   lib/libouro_sodium_shim.so (Ed25519DSIGN.verifyDSIGN's libsodium symbol):
+ *     int crypto_sign_ed25519_verify_detached(const unsigned char *sig,
+ *                                             const unsigned char *m,
+ *                                             unsigned long long mlen,
+ *                                             const unsigned char *pk);
+ * Those names follow libsodium's convention (any nonzero = invalid), so a
+ * device error must not be passed through: the shims abort with the error on
+ * stderr by default, or return -1 with OURO_SHIM_ON_ERROR=invalid. */
 
 /* Replaces SumKES.verifyKES (Sum6KES Ed25519DSIGN Blake2b_256), called via
  * SL.verifySignedKES at ouroboros-consensus-shelley/src/Ouroboros/Consensus/

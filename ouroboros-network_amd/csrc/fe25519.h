@@ -656,8 +656,73 @@ OURO_FI fe fe_sq_scan(const fe& f) {
   }
   return scan_finish(h, c);
 }
+// The same squaring in two interleaved chains (columns 0..4 and 5..9, joined
+// like fe_mul_scan's): a chain's dependent multiply-adds then alternate with
+// the other chain's instead of waiting a cycle each (the one-chain form needs
+// an s_nop between consecutive v_mad_u64_u32 of its chain).
+#ifndef OURO_SQ_CHAINS
+#define OURO_SQ_CHAINS 1
+#endif
+template <int kScale>
+OURO_FI fe fe_sq_scan2(const fe& f) {
+  uint32_t fs[10], f2s[10], f4s[10], f19[10];
+#pragma unroll
+  for (int i = 0; i < 10; i++) {
+    fs[i] = kScale * f.v[i];
+    f2s[i] = 2u * kScale * f.v[i];
+    f4s[i] = 4u * kScale * f.v[i];
+    f19[i] = 19u * f.v[i];
+  }
+  uint32_t h[10];
+  uint64_t cA = 0, cB = 0;
+#pragma unroll
+  for (int s = 0; s < 5; s++) {
+    uint64_t t[2] = {cA, cB};
+    // the terms of column s (chain 0) and s + 5 (chain 1), alternated
+    int ti[2][6], tj[2][6], nt[2] = {0, 0};
+#pragma unroll
+    for (int half = 0; half < 2; half++) {
+      const int k = s + 5 * half;
+#pragma unroll
+      for (int i = 0; i < 10; i++)
+#pragma unroll
+        for (int j = i; j < 10; j++)
+          if ((i + j) % 10 == k) {
+            ti[half][nt[half]] = i;
+            tj[half][nt[half]] = j;
+            nt[half]++;
+          }
+    }
+#pragma unroll
+    for (int q = 0; q < 6; q++) {
+#pragma unroll
+      for (int half = 0; half < 2; half++) {
+        if (q >= nt[half]) continue;
+        const int i = ti[half][q], j = tj[half][q];
+        uint32_t a, b;
+        if (i == j) {
+          a = (i & 1) ? f2s[i] : fs[i];
+          b = (2 * i >= 10) ? f19[i] : f.v[i];
+        } else {
+          a = ((i & 1) && (j & 1)) ? f4s[i] : f2s[i];
+          b = (i + j >= 10) ? f19[j] : f.v[j];
+        }
+        t[half] = mad_acc(a, b, t[half]);
+      }
+    }
+    h[s] = (uint32_t)t[0] & limb_mask(s);
+    cA = t[0] >> limb_bits(s);
+    h[s + 5] = (uint32_t)t[1] & limb_mask(s + 5);
+    cB = t[1] >> limb_bits(s + 5);
+  }
+  const uint64_t t5 = (uint64_t)h[5] + cA;
+  h[5] = (uint32_t)t5 & limb_mask(5);
+  h[6] += (uint32_t)(t5 >> 25);
+  return scan_finish(h, cB);
+}
+
 #if defined(OURO_TRACK_BOUNDS)
-inline void trk_sq_scan(fe& h, const fe& f, unsigned scale) {
+inline void trk_sq_scan(fe& h, const fe& f, unsigned scale, int nchains = 1) {
   unsigned __int128 T[10] = {0};
   for (int i = 0; i < 10; i++) {
     trk_check(((i & 1) ? 4 : 2) * scale * f.b[i] < (1ull << 32));
@@ -670,15 +735,15 @@ inline void trk_sq_scan(fe& h, const fe& f, unsigned scale) {
       T[k % 10] += x * scale;
     }
   }
-  trk_scan(h, T, 1);
+  trk_scan(h, T, nchains);
 }
 #endif
 
 OURO_FI fe fe_sq(const fe& f) {
 #if OURO_FE_SCAN
   OURO_COUNT_SQ();
-  fe h = fe_sq_scan<1>(f);
-  OURO_TRK(trk_sq_scan(h, f, 1));
+  fe h = OURO_SQ_CHAINS == 2 ? fe_sq_scan2<1>(f) : fe_sq_scan<1>(f);
+  OURO_TRK(trk_sq_scan(h, f, 1, OURO_SQ_CHAINS));
   return h;
 #else
   uint64_t t[10];
@@ -689,12 +754,70 @@ OURO_FI fe fe_sq(const fe& f) {
 #endif
 }
 
+// Two independent squarings scanned in lockstep: one chain each, their
+// multiply-adds alternating, so neither waits on its own previous result
+// (the paired exponentiations below).
+OURO_FI void fe_sq_x2(fe& f, fe& g) {
+#if OURO_FE_SCAN
+  OURO_COUNT_SQ();
+  OURO_COUNT_SQ();
+  const fe* in[2] = {&f, &g};
+  uint32_t fs[2][10], f2s[2][10], f4s[2][10], f19[2][10];
+#pragma unroll
+  for (int e = 0; e < 2; e++)
+#pragma unroll
+    for (int i = 0; i < 10; i++) {
+      fs[e][i] = in[e]->v[i];
+      f2s[e][i] = 2u * in[e]->v[i];
+      f4s[e][i] = 4u * in[e]->v[i];
+      f19[e][i] = 19u * in[e]->v[i];
+    }
+  uint32_t h[2][10];
+  uint64_t c[2] = {0, 0};
+#pragma unroll
+  for (int k = 0; k < 10; k++) {
+    uint64_t t[2] = {c[0], c[1]};
+#pragma unroll
+    for (int i = 0; i < 10; i++) {
+#pragma unroll
+      for (int j = i; j < 10; j++) {
+        if ((i + j) % 10 != k) continue;
+#pragma unroll
+        for (int e = 0; e < 2; e++) {
+          uint32_t a, b;
+          if (i == j) {
+            a = (i & 1) ? f2s[e][i] : fs[e][i];
+            b = (2 * i >= 10) ? f19[e][i] : fs[e][i];
+          } else {
+            a = ((i & 1) && (j & 1)) ? f4s[e][i] : f2s[e][i];
+            b = (i + j >= 10) ? f19[e][j] : fs[e][j];
+          }
+          t[e] = mad_acc(a, b, t[e]);
+        }
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < 2; e++) {
+      h[e][k] = (uint32_t)t[e] & limb_mask(k);
+      c[e] = t[e] >> limb_bits(k);
+    }
+  }
+  fe rf = scan_finish(h[0], c[0]), rg = scan_finish(h[1], c[1]);
+  OURO_TRK(trk_sq_scan(rf, f, 1); trk_sq_scan(rg, g, 1);)
+  f = rf;
+  g = rg;
+#else
+  f = fe_sq(f);
+  g = fe_sq(g);
+#endif
+}
+
 // 2 f^2
 OURO_FI fe fe_sq2(const fe& f) {
 #if OURO_FE_SCAN
   OURO_COUNT_SQ();
-  fe h = fe_sq_scan<2>(f);
-  OURO_TRK(trk_sq_scan(h, f, 2));
+  fe h = OURO_SQ_CHAINS == 2 ? fe_sq_scan2<2>(f) : fe_sq_scan<2>(f);
+  OURO_TRK(trk_sq_scan(h, f, 2, OURO_SQ_CHAINS));
   return h;
 #else
   uint64_t t[10];
@@ -815,5 +938,59 @@ OURO_NI fe fe_pow_chain(fe z, int mode) {
 
 OURO_FI fe fe_invert(const fe& z) { return fe_pow_chain(z, 0); }
 OURO_FI fe fe_pow22523(const fe& z) { return fe_pow_chain(z, 1); }
+
+// Two independent z^(2^252 - 3) at once: the same addition chain on both,
+// every squaring of the pair scanned in lockstep (fe_sq_x2), so the two
+// dependency chains fill each other's wait states -- the decodes of an
+// Ed25519 check (A, R), of a VRF's key and Gamma, and Gamma's decode beside
+// Elligator2's root.
+struct fe_pair {
+  fe a, b;
+};
+OURO_FI void fe_sqn_x2(fe& a, fe& b, int n) {
+#pragma unroll 1
+  for (int i = 0; i < n; i++) fe_sq_x2(a, b);
+}
+OURO_NI fe_pair fe_pow22523_x2(fe za, fe zb) {
+  fe a = za, b = zb;
+  fe_sq_x2(a, b);                      // z^2
+  fe a2 = a, b2 = b;
+  fe_sqn_x2(a, b, 2);                  // z^8
+  fe a9 = fe_mul(a, za), b9 = fe_mul(b, zb);
+  fe a11 = fe_mul(a9, a2), b11 = fe_mul(b9, b2);
+  a = a11;
+  b = b11;
+  fe_sq_x2(a, b);
+  fe a5 = fe_mul(a, a9), b5 = fe_mul(b, b9);  // 2^5 - 1
+  a = a5;
+  b = b5;
+  fe_sqn_x2(a, b, 5);
+  fe a10 = fe_mul(a, a5), b10 = fe_mul(b, b5);  // 2^10 - 1
+  a = a10;
+  b = b10;
+  fe_sqn_x2(a, b, 10);
+  fe a20 = fe_mul(a, a10), b20 = fe_mul(b, b10);
+  a = a20;
+  b = b20;
+  fe_sqn_x2(a, b, 20);
+  a = fe_mul(a, a20);                  // 2^40 - 1
+  b = fe_mul(b, b20);
+  fe_sqn_x2(a, b, 10);
+  fe a50 = fe_mul(a, a10), b50 = fe_mul(b, b10);
+  a = a50;
+  b = b50;
+  fe_sqn_x2(a, b, 50);
+  fe a100 = fe_mul(a, a50), b100 = fe_mul(b, b50);
+  a = a100;
+  b = b100;
+  fe_sqn_x2(a, b, 100);
+  a = fe_mul(a, a100);                 // 2^200 - 1
+  b = fe_mul(b, b100);
+  fe_sqn_x2(a, b, 50);
+  a = fe_mul(a, a50);                  // 2^250 - 1
+  b = fe_mul(b, b50);
+  fe_sqn_x2(a, b, 2);
+  return fe_pair{fe_mul(a, za), fe_mul(b, zb)};  // 2^252 - 3
+}
 
 }  // namespace ouro

@@ -83,8 +83,12 @@ __global__ void __launch_bounds__(kBlock, OURO_WAVES) k_sum6kes_verify(
   }
 }
 
+// The six cores from one run-time-dispatched copy of the dispatch (1, the
+// default since round 3) or six inlined calls (0): the same time (r01h 73.76
+// vs 73.62 ms; r03e 70.92 vs 70.90 ms) with the kernel's VGPR spills
+// 107 -> 48 and its scratch 3,904 -> 3,760 B/lane.
 #ifndef OURO_HDR_LOOP
-#define OURO_HDR_LOOP 0
+#define OURO_HDR_LOOP 1
 #endif
 #ifndef OURO_HDR_FINISH_NI
 #define OURO_HDR_FINISH_NI 0
@@ -114,7 +118,7 @@ __global__ void __launch_bounds__(kBlock, OURO_WAVES) k_tpraos_verify(ouro_tprao
   const uint32_t opts = batch_opts(b);
   for (size_t i = tid; i < b.n; i += nth) {
 #if OURO_HDR_LOOP
-    // A/B: one copy of the core dispatch, the core chosen at run time
+    // one copy of the core dispatch, the core chosen at run time
 #pragma unroll 1
     for (int c = kCoreOcert; c <= kCoreVl; c++) hdr_core(b, i, opts, c, lane, res, btab);
 #else

@@ -185,20 +185,27 @@ __device__ __noinline__ void hdr_item_fused(const ouro_tpraos_batch& b, size_t i
         ed_points_item(ed, s, p, true);
       }
     } else if (!skipped) {
+      kstamp(0);
       uint32_t hv[8], cur[8], sig[16];
       ld_words(hv, b.hot_vk + 32 * i, 2);
       const uint32_t* sw = reinterpret_cast<const uint32_t*>(b.kes_sig + 448 * i);
       const bool walk_ok = sum6kes_walk_wide(cur, sig, hv, b.kes_t[i], sw);
+      kstamp(1);
       if (scal)
         ed_scalars_item(ed, sig, cur, ShaGlobalTail{b.body + b.body_off[i]}, b.body_len[i]);
       else
         ed_points_item(ed, sig, cur, walk_ok);
+      kstamp(2);
     }
     if (!arrive_last(ed.word(125), gen, 2)) {
+      if (stamps && e == 1) kstamp_print();
       stamp("half");
       return;
     }
+    kstamp(3);
     const int32_t flag = (!skipped && ed_chain(ed, bw)) ? kFlagOk : 0;
+    kstamp(4);
+    if (stamps && e == 1) kstamp_print();
     if (lead) stg1(res.word(kResFlags + e), flag);
   } else {
     if (!((skip >> item) & 1u)) hdr_core_wide(b, i, opts, item, res, bw, true);

@@ -137,6 +137,15 @@ OURO_FI i288 i288_8L() {
   return r;
 }
 
+// Inner loop of the half Euclid on the leading 64 bits: 1 = one full
+// quotient per step (q = floor(x / y) estimated in double precision and
+// corrected exactly: one Euclid step each, ~0.6 steps per bit); 0 = binary
+// subtract-and-shift steps (one per quotient bit, the round-2 form).  Both
+// produce the exact remainder sequence while the matrix stays below 2^31.
+#ifndef OURO_LATTICE_QUOT
+#define OURO_LATTICE_QUOT 1
+#endif
+
 struct HalfScalars {
   uint32_t c0[8];  // |c0|
   uint32_t c1[8];  // c1 > 0, odd
@@ -167,6 +176,35 @@ OURO_HD inline void ed25519_half_scalars(HalfScalars& out, const uint32_t h[8]) 
     // 2^128 (y < 2^(128 - sh)), so that u stays the last remainder above it
     // (sh >= 65 here: r_u > r_v > 2^128)
     const int ybits = 128 - sh > 32 ? 128 - sh : 32;
+#if OURO_LATTICE_QUOT
+#pragma unroll 1
+    for (int it = 0; it < 96; it++) {
+      if (y < (1ull << ybits)) break;
+      // q = floor(x / y) >= 1 (x >= y): the double quotient scaled down by
+      // 2^-48 never exceeds it (x, y rounded to 53 bits: relative error
+      // < 2^-51 in the ratio), and is at most 1 short -- fixed exactly below
+      uint64_t q = (uint64_t)((double)x / (double)y * (1.0 - 0x1p-48));
+      if (q == 0) q = 1;
+      uint64_t r = x - q * y;  // q y <= x: no wrap
+      if (r >= y) {
+        q++;
+        r -= y;
+      }
+      // keep |m| < 2^31: the modified row grows to |m0| + q |m1|
+      if (q >= (1ull << 31)) break;
+      const int64_t a10 = m10 < 0 ? -m10 : m10, a11 = m11 < 0 ? -m11 : m11;
+      const int64_t a00 = m00 < 0 ? -m00 : m00, a01 = m01 < 0 ? -m01 : m01;
+      if (a00 + (int64_t)q * a10 >= (1ll << 31) || a01 + (int64_t)q * a11 >= (1ll << 31)) break;
+      m00 -= (int64_t)q * m10;
+      m01 -= (int64_t)q * m11;
+      moved = true;
+      // r < y: swap the rows
+      x = y;
+      y = r;
+      int64_t t = m00; m00 = m10; m10 = t;
+      t = m01; m01 = m11; m11 = t;
+    }
+#else
 #pragma unroll 1
     for (int it = 0; it < 96; it++) {
       if (y < (1ull << ybits)) break;
@@ -186,6 +224,7 @@ OURO_HD inline void ed25519_half_scalars(HalfScalars& out, const uint32_t h[8]) 
         q = m01; m01 = m11; m11 = q;
       }
     }
+#endif
     if (!moved) break;
     i288 nu = i288_add(i288_mul_s32(ru, (int32_t)m00), i288_mul_s32(rv, (int32_t)m01));
     i288 nv = i288_add(i288_mul_s32(ru, (int32_t)m10), i288_mul_s32(rv, (int32_t)m11));

@@ -163,9 +163,15 @@ OURO_HD inline int32_t vrf_v_core(const uint32_t pk[8], const uint32_t pi[20], c
   }
   ge_p3 Gamma;
   bool ok = true;
+  // throughput mode: Gamma's decode and Elligator2 share one paired
+  // exponentiation (fe_pow22523_x2); the latency split cores do one each
+  const bool pair = OURO_DECODE_PAIR && part == 0;
+  DecodePre gpre;
+  fe gbase;
   if (part != 1) {
     ok = ge_is_canonical(G);
-    ok = ge_decode(&Gamma, G, false) && ok;
+    if (pair) gbase = ge_decode_pre(gpre, G);
+    else ok = ge_decode(&Gamma, G, false) && ok;
   }
   if (part == 2) {
     build_table(lane + kSlotTab1, ge_p3_neg(Gamma), quad);
@@ -186,7 +192,16 @@ OURO_HD inline int32_t vrf_v_core(const uint32_t pk[8], const uint32_t pi[20], c
     uint32_t rw[16];
     sha512_digest_words(rw, Hs);
     rw[7] &= 0x7fffffffu;
-    ge_p3 Hp = elligator2_h(rw);
+    ge_p3 Hp;
+    if (pair) {
+      Ell2Pre epre;
+      const fe ebase = elligator2_pre(epre, rw);
+      const fe_pair pw = fe_pow22523_x2(gbase, ebase);
+      ok = ge_decode_post(&Gamma, gpre, pw.a, G, false) && ok;
+      Hp = elligator2_post(epre, pw.b);
+    } else {
+      Hp = elligator2_h(rw);
+    }
     st_point(res, ptH, Hp.X, Hp.Y, Hp.Z);
     build_table(lane + kSlotTab1, Hp, quad);
     st_words8(lane + kSlotA1, s);

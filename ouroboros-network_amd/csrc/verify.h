@@ -279,6 +279,16 @@ constexpr uint32_t dsm_cfg(int nw1, int nw2, bool useB, int tab1 = 0, int tab2 =
 // 0.643 -> 0.638 ms (two runs each); lane mode keeps the rolled loop
 #define OURO_ADD_UNROLL_QUAD 4
 #endif
+// A/B: where a window's table entries are touched: 0 = before its four
+// doublings (default), 3 = before the last one (the last doubling peeled off
+// the loop).  Measured (profiles/r03e): touching before the last doubling
+// keeps the lines in L2 until the additions read them -- header kernel HBM
+// traffic 212 -> 160 KB/header -- but runs no faster (71.35 vs 70.90 ms;
+// an in-loop `if (k == at)` variant cost +2.8 % in code generation alone):
+// the kernel is bound by VALU issue, not by these loads.
+#ifndef OURO_PF_AT
+#define OURO_PF_AT 0
+#endif
 template <bool kQuad>
 OURO_FI void dsm_body(Slot lane, const int32_t* btab, uint32_t cfg) {
   const int nw1 = (int)(cfg & 0x7f), nw2 = (int)((cfg >> 8) & 0x7f);
@@ -336,24 +346,34 @@ OURO_FI void dsm_body(Slot lane, const int32_t* btab, uint32_t cfg) {
     const Slot e1 = tab1.chunks((i1 > 0 ? i1 : 0) * (kCachedWords / 4));
     const Slot e2 = tab2.chunks((i2 > 0 ? i2 : 0) * (kCachedWords / 4));
     uint32_t pf1 = 0, pf2 = 0, pf3 = 0, pf4 = 0, pf5 = 0, pf6 = 0;
-    if (act1) { pf1 = (uint32_t)ldg1(e1.word(0)); pf2 = (uint32_t)ldg1(e1.word(kCachedWords - 1)); }
-    if (act2) { pf3 = (uint32_t)ldg1(e2.word(0)); pf4 = (uint32_t)ldg1(e2.word(kCachedWords - 1)); }
-    if (actB) {
-      // the B entries (one 128-B line each) come from the 8 MiB tables
-      const int i3 = (d3 < 0 ? -d3 : d3) - 1, i4 = (d4 < 0 ? -d4 : d4) - 1;
-      pf5 = (uint32_t)ldg1(btab + (size_t)(i3 > 0 ? i3 : 0) * kNielsWords);
-      pf6 = (uint32_t)ldg1(btab + ((size_t)kBTabEntries + (i4 > 0 ? i4 : 0)) * kNielsWords);
-    }
+    const int i3 = (d3 < 0 ? -d3 : d3) - 1, i4 = (d4 < 0 ? -d4 : d4) - 1;
+#define OURO_TOUCH_ENTRIES()                                                                   \
+  do {                                                                                         \
+    if (act1) { pf1 = (uint32_t)ldg1(e1.word(0)); pf2 = (uint32_t)ldg1(e1.word(kCachedWords - 1)); } \
+    if (act2) { pf3 = (uint32_t)ldg1(e2.word(0)); pf4 = (uint32_t)ldg1(e2.word(kCachedWords - 1)); } \
+    if (actB) { /* the B entries (one 128-B line each) come from the 8 MiB tables */          \
+      pf5 = (uint32_t)ldg1(btab + (size_t)(i3 > 0 ? i3 : 0) * kNielsWords);                    \
+      pf6 = (uint32_t)ldg1(btab + ((size_t)kBTabEntries + (i4 > 0 ? i4 : 0)) * kNielsWords);   \
+    }                                                                                          \
+  } while (0)
+    const bool skip_dbl = OURO_DSM_SKIP_ID && j == top - 1;
+    if (kQuad || OURO_PF_AT == 0 || skip_dbl) OURO_TOUCH_ENTRIES();
     // (the top window starts from the identity: its doublings are skipped)
-    if (!OURO_DSM_SKIP_ID || j != top - 1) {
+    if (!skip_dbl) {
       if constexpr (kQuad) {
 #pragma unroll OURO_DBL_UNROLL_QUAD
         for (int k = 0; k < 4; k++) t = ge_dbl_from_p1p1_quad(t);
-      } else {
+      } else if (OURO_PF_AT == 0) {
 #pragma unroll OURO_DBL_UNROLL
         for (int k = 0; k < 4; k++) t = ge_p2_dbl(ge_p1p1_to_p2(t));
+      } else {
+#pragma unroll 1
+        for (int k = 0; k < 3; k++) t = ge_p2_dbl(ge_p1p1_to_p2(t));
+        OURO_TOUCH_ENTRIES();
+        t = ge_p2_dbl(ge_p1p1_to_p2(t));
       }
     }
+#undef OURO_TOUCH_ENTRIES
     prefetch ^= pf1 ^ pf2 ^ pf3 ^ pf4 ^ pf5 ^ pf6;
     // up to four additions, each from a wave-uniform source
     constexpr int kAddUnroll = kQuad ? OURO_ADD_UNROLL_QUAD : 1;
@@ -528,8 +548,7 @@ OURO_HD inline bool ed25519_verify_lane(const uint32_t sig[16], const uint32_t p
   if (quad) {
     ge_decode_pair_quad(&negA, &okA, &negR, &okR, pk, R, true);
   } else {
-    okA = ge_decode(&negA, pk, true);
-    okR = ge_decode(&negR, R, true);
+    ge_decode_pair(&negA, &okA, &negR, &okR, pk, R, true);
   }
   ok = okA && ok;
   // encode(R') == R_bytes  <=>  R_bytes is the canonical encoding of R' (a point)
@@ -585,20 +604,30 @@ OURO_HD inline bool ed25519_verify_lane(const uint32_t sig[16], const uint32_t p
 // wide exponentiation (wide.h), everything else fe_pow22523.  kMul8 = false
 // returns the Elligator2 point before the cofactor clearing (the wave-wide
 // item doubles it three times on the wave).
-template <class Pow, bool kMul8 = true>
-OURO_HD inline ge_p3 elligator2_h_with(const uint32_t r[8], Pow pow22523) {
-  const fe A = fe_mont_a();
-  fe rr = fe_from_words(r);
-  fe r2 = fe_sq(rr);
-  fe D = fe_carry(fe_add(fe_add(r2, r2), fe_one()));    // 1 + 2 r^2 (re-balanced:
-                                                        // n = Xn - D below sums 4 terms)
-  fe A2r2 = fe_mul(fe_mont_a2(), r2);                   // A^2 r^2
-  fe W = fe_carry(fe_sub4(fe_sq(D), fe_add(A2r2, A2r2)));  // D^2 - 2 A^2 r^2
-  fe num = fe_mul(fe_mont_a2a(), D);                    // (A + 2) A D
+// Split around its exponentiation like ge_decode (the throughput header core
+// pairs it with Gamma's decode, fe_pow22523_x2): elligator2_pre returns the
+// base num W^7, elligator2_post takes its (p-5)/8 power.
+struct Ell2Pre {
+  fe rr, r2, D, num, W, W3;
+};
+OURO_HD inline fe elligator2_pre(Ell2Pre& e, const uint32_t r[8]) {
+  e.rr = fe_from_words(r);
+  e.r2 = fe_sq(e.rr);
+  e.D = fe_carry(fe_add(fe_add(e.r2, e.r2), fe_one()));  // 1 + 2 r^2 (re-balanced:
+                                                         // n = Xn - D below sums 4 terms)
+  fe A2r2 = fe_mul(fe_mont_a2(), e.r2);                  // A^2 r^2
+  e.W = fe_carry(fe_sub4(fe_sq(e.D), fe_add(A2r2, A2r2)));  // D^2 - 2 A^2 r^2
+  e.num = fe_mul(fe_mont_a2a(), e.D);                    // (A + 2) A D
   // beta = num W^3 (num W^7)^((p-5)/8)
-  fe W3 = fe_mul(fe_sq(W), W);
-  fe W7 = fe_mul(fe_sq(W3), W);
-  fe beta = fe_mul(fe_mul(num, W3), pow22523(fe_mul(num, W7)));
+  e.W3 = fe_mul(fe_sq(e.W), e.W);
+  const fe W7 = fe_mul(fe_sq(e.W3), e.W);
+  return fe_mul(e.num, W7);
+}
+template <bool kMul8 = true>
+OURO_HD inline ge_p3 elligator2_post(const Ell2Pre& e, const fe& pw) {
+  const fe A = fe_mont_a();
+  const fe rr = e.rr, r2 = e.r2, D = e.D, W = e.W, num = e.num;
+  fe beta = fe_mul(fe_mul(num, e.W3), pw);
   fe vxx = fe_mul(fe_sq(beta), W);
   const bool lam_p1 = fe_iszero(fe_sub4(vxx, num));
   const bool lam_m1 = fe_iszero(fe_add(vxx, num));
@@ -616,6 +645,12 @@ OURO_HD inline ge_p3 elligator2_h_with(const uint32_t r[8], Pow pow22523) {
   ge_p3 P{fe_mul(x, m), nc, m, fe_mul(x, nc)};
   if constexpr (!kMul8) return P;
   return ge_mul8(P);
+}
+template <class Pow, bool kMul8 = true>
+OURO_HD inline ge_p3 elligator2_h_with(const uint32_t r[8], Pow pow22523) {
+  Ell2Pre e;
+  const fe base = elligator2_pre(e, r);
+  return elligator2_post<kMul8>(e, pow22523(base));
 }
 OURO_HD inline ge_p3 elligator2_h(const uint32_t r[8]) {
   return elligator2_h_with(r, [](const fe& z) { return fe_pow22523(z); });
@@ -676,10 +711,12 @@ OURO_HD inline bool vrf03_verify_lane(uint32_t beta[16], const uint32_t pk[8],
   }
   // validate_key + decode_proof
   ge_p3 Y, Gamma;
+  bool okY, okG;
+  ge_decode_pair(&Y, &okY, &Gamma, &okG, pk, G, false);
   bool ok = !ge_has_small_order(pk) && ge_is_canonical(pk);
-  ok = ge_decode(&Y, pk, false) && ok;
+  ok = okY && ok;
   ok = ge_is_canonical(G) && ok;
-  ok = ge_decode(&Gamma, G, false) && ok;
+  ok = okG && ok;
   sc_reduce256(s, s_raw);
   // H = hash_to_curve(Y, alpha): r = SHA-512(0x04 || 0x01 || Y || alpha)[0:32]
   uint32_t pre[9];

@@ -13,23 +13,7 @@
 // By default the shim aborts the process with the error on stderr (a node
 // must not silently fork off on a GPU fault); OURO_SHIM_ON_ERROR=invalid
 // selects the libsodium reading (error -> -1) for callers that accept it.
-#include <cstdio>
-#include <cstdlib>
-#include <cstring>
-
-#include "../../include/ouro_verify.h"
-
-namespace {
-int shim_rc(int rc, const char* what) {
-  if (rc == OURO_OK || rc == OURO_INVALID) return rc;
-  const char* mode = getenv("OURO_SHIM_ON_ERROR");
-  if (mode && strcmp(mode, "invalid") == 0) return OURO_INVALID;
-  fprintf(stderr, "libouro_vrf_shim: %s failed with %d (%s); aborting rather than "
-                  "reporting a valid proof as invalid (OURO_SHIM_ON_ERROR=invalid to "
-                  "return -1 instead)\n", what, rc, ouro_last_error());
-  abort();
-}
-}  // namespace
+#include "shim_common.h"
 
 extern "C" {
 

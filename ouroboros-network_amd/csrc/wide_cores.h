@@ -20,6 +20,7 @@ namespace wide {
 #endif
 #if OURO_LAT_STAMPS
 __device__ unsigned long long g_vstamps[8];
+__device__ unsigned long long g_kstamps[2][8];  // header 0's KES points / scalars items
 #endif
 // phase k of that item (0 start, 1 sha, 2 elligator, 3 table, 4 chain,
 // 5 combine-add, 6 encoded), kept in device memory: printed once at the end
@@ -28,6 +29,29 @@ __device__ __forceinline__ void vstamp(int k) {
   if (blockIdx.x == 4 && threadIdx.x == 0) g_vstamps[k] = __builtin_amdgcn_s_memrealtime();
 #else
   (void)k;
+#endif
+}
+// phase k of header 0's KES points (block 1) / scalars (block 9) item:
+// 0 start, 1 Merkle walk, 2 decodes / SHA + lattice, 3 arrival, 4 chain
+__device__ __forceinline__ void kstamp(int k) {
+#if OURO_LAT_STAMPS
+  if ((blockIdx.x == 1 || blockIdx.x == 9) && threadIdx.x == 0) {
+    unsigned long long* s = g_kstamps[blockIdx.x == 9];
+    if (k == 0)
+      for (int j = 1; j < 8; j++) s[j] = 0;
+    s[k] = __builtin_amdgcn_s_memrealtime();
+  }
+#else
+  (void)k;
+#endif
+}
+__device__ __forceinline__ void kstamp_print() {
+#if OURO_LAT_STAMPS
+  if ((blockIdx.x == 1 || blockIdx.x == 9) && threadIdx.x == 0) {
+    const unsigned long long* s = g_kstamps[blockIdx.x == 9];
+    printf("kstamp %d %llu %llu %llu %llu %llu %llu %llu %llu\n", blockIdx.x == 9 ? 9 : 1, s[0],
+           s[1], s[2], s[3], s[4], s[5], s[6], s[7]);
+  }
 #endif
 }
 __device__ __forceinline__ void vstamp_print() {
@@ -471,7 +495,38 @@ __device__ __forceinline__ void ed_scalars_item(Slot e, const uint32_t sig[16], 
     S[i] = sig[8 + i];
   }
   HalfScalars hs;
+#if OURO_LAT_STAMPS
+  {  // ed25519_scalars with phase stamps (5 SHA-512, 6 reduction, 7 lattice)
+    uint32_t pre[16];
+    for (int i = 0; i < 8; i++) {
+      pre[i] = R[i];
+      pre[8 + i] = pk[i];
+    }
+    uint64_t H[8];
+    sha512_prefixed<64>(H, pre, msg, mlen);
+    kstamp(5);
+    uint32_t hw[16], h[8];
+    sha512_digest_words(hw, H);
+    sc_reduce512(h, hw);
+    kstamp(6);
+    ed25519_half_scalars(hs, h);
+    kstamp(7);
+    uint32_t prod[16];
+    for (int i = 0; i < 16; i++) prod[i] = 0;
+    for (int i = 0; i < 8; i++) {
+      uint64_t carry = 0;
+      for (int j = 0; j < 8; j++) {
+        const uint64_t t = (uint64_t)hs.c1[i] * S[j] + prod[i + j] + carry;
+        prod[i + j] = (uint32_t)t;
+        carry = t >> 32;
+      }
+      prod[i + 8] = (uint32_t)carry;
+    }
+    sc_reduce512(b, prod);
+  }
+#else
   ed25519_scalars(hs, b, R, S, pk, msg, mlen);
+#endif
   int nw = (hs.bits + 4) >> 2;
   nw = nw < 1 ? 1 : (nw > 64 ? 64 : nw);
   if ((threadIdx.x & 63u) == 0) {

@@ -85,6 +85,7 @@ def test_struct_offsets_match_the_c_compiler(tmp_path):
 
 
 SHIM = os.path.join(ROOT, "ouroboros-network_amd", "lib", "libouro_vrf_shim.so")
+SODIUM_SHIM = os.path.join(ROOT, "ouroboros-network_amd", "lib", "libouro_sodium_shim.so")
 
 
 def test_vrf_names_only_in_the_opt_in_shim():
@@ -107,6 +108,12 @@ def test_vrf_names_only_in_the_opt_in_shim():
     text = open(os.path.join(ROOT, "include", "ouro_verify.h")).read()
     for name in _native.VRF_ALIASES:
         assert name in text
+    # libsodium's Ed25519 verify: only from its own opt-in shim
+    sod = subprocess.run(["nm", "-D", "--defined-only", SODIUM_SHIM], check=True,
+                         capture_output=True, text=True).stdout
+    assert " crypto_sign_ed25519_verify_detached\n" not in syms
+    assert " T crypto_sign_ed25519_verify_detached\n" in sod
+    assert "crypto_sign_ed25519_verify_detached" in text
 
 
 _SHIM_CALL = """
@@ -114,12 +121,16 @@ import ctypes, sys
 ctypes.CDLL(sys.argv[1], mode=ctypes.RTLD_GLOBAL)
 shim = ctypes.CDLL(sys.argv[2])
 out = ctypes.create_string_buffer(64)
-print(shim.crypto_vrf_ietfdraft03_verify(out, bytes(32), bytes(80), b"x", 1), flush=True)
+if sys.argv[3] == "vrf":
+    print(shim.crypto_vrf_ietfdraft03_verify(out, bytes(32), bytes(80), b"x", 1), flush=True)
+else:
+    print(shim.crypto_sign_ed25519_verify_detached(bytes(64), b"x", 1, bytes(32)), flush=True)
 """
 
 
+@pytest.mark.parametrize("which", ["vrf", "sodium"])
 @pytest.mark.parametrize("mode", ["default", "invalid"])
-def test_shim_never_reports_a_device_error_as_an_invalid_proof(mode):
+def test_shim_never_reports_a_device_error_as_an_invalid_proof(mode, which):
     """PraosVRF reads any nonzero as 'invalid proof'.  With no device the
     product returns an error code; the shim must abort (default) rather than
     pass it on, or return -1 only when OURO_SHIM_ON_ERROR=invalid says so."""
@@ -134,8 +145,9 @@ def test_shim_never_reports_a_device_error_as_an_invalid_proof(mode):
     env.pop("OURO_SHIM_ON_ERROR", None)
     if mode == "invalid":
         env["OURO_SHIM_ON_ERROR"] = "invalid"
-    r = subprocess.run([sys.executable, "-c", _SHIM_CALL, LIB, SHIM], capture_output=True,
-                       text=True, env=env, timeout=120)
+    r = subprocess.run([sys.executable, "-c", _SHIM_CALL, LIB,
+                        SHIM if which == "vrf" else SODIUM_SHIM, which],
+                       capture_output=True, text=True, env=env, timeout=120)
     if mode == "default":
         assert r.returncode == -6, (r.returncode, r.stdout, r.stderr)  # SIGABRT
         assert "aborting rather than reporting a valid proof as invalid" in r.stderr

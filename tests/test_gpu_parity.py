@@ -61,6 +61,24 @@ def test_ed25519_edge_cases(small_path, gpu_lib):
     np.testing.assert_array_equal(got, want)
 
 
+def test_sodium_shim_matches_libsodium_rules(gpu_lib):
+    """lib/libouro_sodium_shim.so's crypto_sign_ed25519_verify_detached (the
+    opt-in link alias of ouro_ed25519_verify) on the edge-case set: the
+    oracle's (= libsodium 1.0.18's) verdict for every case."""
+    import ctypes
+    import os
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    shim = ctypes.CDLL(os.path.join(root, "ouroboros-network_amd", "lib",
+                                    "libouro_sodium_shim.so"))
+    fn = shim.crypto_sign_ed25519_verify_detached
+    fn.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_ulonglong, ctypes.c_char_p]
+    cases = ed25519_edge_cases()
+    for pk, sig, msg in cases[:24]:
+        want = 0 if O.ed25519_verify(sig, msg, pk) else -1
+        assert fn(sig, msg, len(msg), pk) == want
+
+
 def test_ed25519_variable_messages(small_path, gpu_lib):
     from ouroboros_network_amd import Ed25519DSIGN
 

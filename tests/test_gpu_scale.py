@@ -22,6 +22,21 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
+def _ge_l(s):
+    """Rows of 32-byte little-endian scalars that are >= L (vectorised)."""
+    L = (2**252 + 27742317777372353535851937790883648493).to_bytes(32, "little")
+    gt = np.zeros(s.shape[0], bool)
+    eq = np.ones(s.shape[0], bool)
+    for b in range(31, -1, -1):
+        gt |= eq & (s[:, b] > L[b])
+        eq &= s[:, b] == L[b]
+    return gt | eq
+
+
+def _s_unreduced_bits(se, sl):
+    return (_ge_l(se) * 0x40 | _ge_l(sl) * 0x80).astype(np.uint8)
+
+
 def test_full_size_batch_with_corruptions():
     import ctypes
 
@@ -47,6 +62,10 @@ def test_full_size_batch_with_corruptions():
         view = t[name].view(n, w)
         view[rows.to(dev), cols.to(dev)] += 1
         expect[rows] = 15 ^ bit
+    # a corrupted byte of a proof's s can lift it to s >= L: the header then
+    # also carries that proof's OURO_HDR_*_S_UNREDUCED bit (include/ouro_verify.h)
+    expect |= torch.from_numpy(_s_unreduced_bits(t["eta_proof"].view(n, 80)[:, 48:].cpu().numpy(),
+                                                 t["leader_proof"].view(n, 80)[:, 48:].cpu().numpy()))
     hdr = bench.DeviceHeaders(t, n, dev)
     st = torch.cuda.current_stream()
     hdr.launch(st)
@@ -67,6 +86,7 @@ def test_full_size_batch_with_corruptions():
     _native.check(rc, "vrf batch")
     torch.cuda.synchronize()
     assert torch.equal(ok.cpu(), ((expect & 0x04) != 0).to(torch.uint8))
+    assert int((expect & 0xC0 != 0).sum()) > 0  # the s >= L corner did occur
     assert torch.equal(beta, hdr.beta_eta)
 
     # bit-exact oracle comparison on a random sample

@@ -46,8 +46,11 @@ def main():
                        text=True, timeout=600)
     if p.returncode:
         sys.exit(p.stderr[-2000:])
-    launches, cur, vst = [], [], {}
+    launches, cur, vst, kst = [], [], {}, {}
     for line in p.stdout.splitlines():
+        if line.startswith("kstamp "):
+            f = line.split()
+            kst.setdefault(len(launches), {})[int(f[1])] = [int(x) for x in f[2:]]
         if line.startswith("vstamp "):
             ts = [int(x) for x in line.split()[1:]]
             tags = ["start", "sha", "elligator", "table", "chain", "combine-add", "encoded"]
@@ -79,6 +82,21 @@ def main():
     if phases:
         print("eta V item phases (us after its start):",
               ", ".join(f"{k} {np.median(v):.1f}" for k, v in phases.items()))
+    # header 0's KES items (kstamp): phases relative to the earlier start of the two
+    tags = ["start", "walk", "prep", "arrive", "chain", "sha", "reduce", "lattice"]
+    kph = {}
+    for k, st in kst.items():
+        if k < 2 or 1 not in st or 9 not in st:
+            continue
+        t0 = min(st[1][0], st[9][0])
+        for item in (1, 9):
+            for tag, t in zip(tags, st[item]):
+                if t:
+                    kph.setdefault((item, tag), []).append((t - t0) / 100.0)
+    for item, name in ((1, "KES points"), (9, "KES scalars")):
+        row = [f"{tag} {np.median(kph[(item, tag)]):.1f}" for tag in tags if (item, tag) in kph]
+        if row:
+            print(f"{name} item phases (us):", ", ".join(row))
 
 
 if __name__ == "__main__":

@@ -13,7 +13,7 @@
 #include <cstring>
 #include <vector>
 
-#include "../../ouroboros-network_amd/csrc/fe25519.h"
+#include "../../../ouroboros-network_amd/csrc/fe25519.h"
 #include "fe8_proto.h"
 
 #define CHECK(x)                                                                          \
