@@ -50,11 +50,17 @@ def test_full_size_batch_with_corruptions():
     n = 1 << 20
     t, _ = bench.synth_headers(n, 1024, dev)
     g = torch.Generator().manual_seed(20261016)
-    pick = torch.randint(0, 8, (n,), generator=g) == 0
-    which = torch.randint(0, 4, (n,), generator=g)
-    # (field, row width, verdict bit the corruption must clear)
+    # (field, row width, verdict bits the corruption must clear): signatures
+    # and proofs, and -- SURVEY.md §8(d)'s pk | sig | msg | proof | alpha --
+    # the keys (the hot key is both the OCert's message and the KES root),
+    # the VRF inputs, the OCert counter / KES period (the OCert's message) and
+    # the header body (the KES message)
     fields = [("ocert_sigma", 64, 0x01), ("kes_sig", 448, 0x02), ("eta_proof", 80, 0x04),
-              ("leader_proof", 80, 0x08)]
+              ("leader_proof", 80, 0x08), ("issuer_vk", 32, 0x01), ("hot_vk", 32, 0x03),
+              ("vrf_vk", 32, 0x0C), ("eta_alpha", 32, 0x04), ("leader_alpha", 32, 0x08),
+              ("ocert_counter", 8, 0x01), ("ocert_kes_period", 8, 0x01), ("body", 544, 0x02)]
+    pick = torch.randint(0, 8, (n,), generator=g) == 0
+    which = torch.randint(0, len(fields), (n,), generator=g)
     expect = torch.full((n,), 15, dtype=torch.uint8)
     for k, (name, w, bit) in enumerate(fields):
         rows = torch.nonzero(pick & (which == k)).squeeze(1)
@@ -108,3 +114,50 @@ def test_full_size_batch_with_corruptions():
     np.testing.assert_array_equal(hv, verdict.numpy())
     np.testing.assert_array_equal(hbe.reshape(-1), hdr.beta_eta.cpu().numpy())
     np.testing.assert_array_equal(hbl.reshape(-1), hdr.beta_leader.cpu().numpy())
+
+
+def test_full_size_kes_batch_with_corruptions():
+    """configs[2] at its full size: 1,048,576 Sum6KES signatures (the headers'
+    hot keys, periods, bodies and KES signatures) through the standalone
+    kernel, 1/8 of them with one byte of the signature, the key or the body
+    incremented (each then fails), and a random sample of 1,024 against the
+    CPU oracle one by one."""
+    import ctypes
+
+    import torch
+
+    sys.path.insert(0, ROOT)
+    import bench
+    from ouroboros_network_amd import _native
+
+    dev = torch.device("cuda:0")
+    n = 1 << 20
+    t, blen = bench.synth_headers(n, 1024, dev)
+    g = torch.Generator().manual_seed(20261017)
+    pick = torch.randint(0, 8, (n,), generator=g) == 0
+    which = torch.randint(0, 3, (n,), generator=g)
+    expect = torch.ones(n, dtype=torch.uint8)
+    for k, (name, w) in enumerate((("kes_sig", 448), ("hot_vk", 32), ("body", blen))):
+        rows = torch.nonzero(pick & (which == k)).squeeze(1)
+        cols = torch.randint(0, w, (rows.numel(),), generator=g)
+        t[name].view(n, w)[rows.to(dev), cols.to(dev)] += 1
+        expect[rows] = 0
+    v = _native.load()
+    st = torch.cuda.current_stream()
+    ver = torch.zeros(n, dtype=torch.uint8, device=dev)
+    rc = v.ouro_sum6kes_verify_batch_device(ctypes.c_void_p(st.cuda_stream), n,
+                                             *[t[k].data_ptr() for k in (
+                                                 "hot_vk", "kes_t", "body", "body_off",
+                                                 "body_len", "kes_sig")], ver.data_ptr())
+    _native.check(rc, "kes batch")
+    torch.cuda.synchronize()
+    got = ver.cpu()
+    assert torch.equal(got, expect), int((got != expect).sum())
+    rng = np.random.default_rng(6)
+    vk = t["hot_vk"].cpu().numpy().reshape(n, 32)
+    kt = t["kes_t"].cpu().numpy().view(np.uint32)
+    body = t["body"].cpu().numpy().reshape(n, blen)
+    sig = t["kes_sig"].cpu().numpy().reshape(n, 448)
+    for i in rng.choice(n, 1024, replace=False):
+        want = O.kes_verify(vk[i].tobytes(), int(kt[i]), body[i].tobytes(), sig[i].tobytes())
+        assert bool(got[i]) == want, i
