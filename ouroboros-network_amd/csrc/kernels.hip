@@ -90,8 +90,12 @@ __global__ void __launch_bounds__(kBlock, OURO_WAVES) k_sum6kes_verify(
 #ifndef OURO_HDR_LOOP
 #define OURO_HDR_LOOP 1
 #endif
+// The finish (inversion, encodings, hashes) out of line with its own
+// register allocation (1, the default since round 3): kernel VGPR spills
+// 48 -> 9, scratch 3,760 -> 3,152 B/lane, time 69.57 -> 69.43 ms
+// (profiles/r03/ab_finish_prefetch.json).
 #ifndef OURO_HDR_FINISH_NI
-#define OURO_HDR_FINISH_NI 0
+#define OURO_HDR_FINISH_NI 1
 #endif
 #if OURO_HDR_FINISH_NI
 // A/B: the finish (inversion, encodings, hashes) with its own register allocation

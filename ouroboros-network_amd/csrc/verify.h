@@ -279,15 +279,17 @@ constexpr uint32_t dsm_cfg(int nw1, int nw2, bool useB, int tab1 = 0, int tab2 =
 // 0.643 -> 0.638 ms (two runs each); lane mode keeps the rolled loop
 #define OURO_ADD_UNROLL_QUAD 4
 #endif
-// A/B: where a window's table entries are touched: 0 = before its four
-// doublings (default), 3 = before the last one (the last doubling peeled off
-// the loop).  Measured (profiles/r03e): touching before the last doubling
-// keeps the lines in L2 until the additions read them -- header kernel HBM
-// traffic 212 -> 160 KB/header -- but runs no faster (71.35 vs 70.90 ms;
-// an in-loop `if (k == at)` variant cost +2.8 % in code generation alone):
-// the kernel is bound by VALU issue, not by these loads.
+// Where a window's table entries are touched: 3 = before its last doubling
+// (the default since round 3; that doubling peeled off the loop), 0 = before
+// all four (round 2).  The gathers of ~7 us of doublings over the whole grid
+// exceed an XCD's 4 MB L2, so lines touched four doublings ahead were often
+// evicted before the additions read them: touching one doubling ahead cuts
+// the header kernel's HBM traffic 202 -> 158 KB/header (Ed25519 40 -> 31 KB,
+// Sum6KES 43 -> 34 KB, VRF 60 -> 48 KB) and its time 69.57 -> 69.18 ms
+// (profiles/r03/ab_finish_prefetch.json).  (An in-loop `if (k == at)` form of
+// the same change cost +2.8 % in code generation: profiles/r03/ab_prefetch_position.json.)
 #ifndef OURO_PF_AT
-#define OURO_PF_AT 0
+#define OURO_PF_AT 3
 #endif
 template <bool kQuad>
 OURO_FI void dsm_body(Slot lane, const int32_t* btab, uint32_t cfg) {
