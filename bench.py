@@ -824,6 +824,43 @@ def raw_leg(n: int, npools: int, device, threads: int, chunk: int = 0, reps: int
     return res
 
 
+def byron_leg(n: int, threads: int, reps: int = 3):
+    """Raw Byron header CBOR -> verdicts: the golden
+    Byron headers (tests/golden/reference_kats.json "byron_wire": N2N v1 and
+    Cardano HFC forms, regular and epoch-boundary) repeated to n, host memory.
+      pack        the C slicer alone (ouro_byron_pack_cbor, `threads` host threads)
+      verify_cbor slicer + ByronDSIGN batch verify on the GPU in one call
+                  (ouro_byron_verify_cbor: H2D of the messages, kernel, D2H)
+      python      the per-header Python slicer (byron.parse_byron_header) on a
+                  sample, for contrast
+    Real keys and signatures (the golden ones, so every row is the same
+    work); never `value`."""
+    from ouroboros_network_amd import byron as B
+
+    with open(os.path.join(ROOT, "tests", "golden", "reference_kats.json")) as f:
+        wires = [bytes.fromhex(w["raw"]) for w in json.load(f)["byron_wire"]]
+    raws = [wires[i % len(wires)] for i in range(n)]
+    ln = np.array([len(r) for r in raws], np.uint32)
+    off = np.zeros(n, np.uint64)
+    off[1:] = np.cumsum(ln[:-1], dtype=np.uint64)
+    arg = (np.frombuffer(b"".join(raws), np.uint8), off, ln)
+    B.pack_byron_cbor(arg, nthreads=threads)  # warm
+    tp = min(_timed(lambda: B.pack_byron_cbor(arg, nthreads=threads)) for _ in range(reps))
+    v, st = B.verify_byron_cbor(arg)  # warm
+    tv = min(_timed(lambda: B.verify_byron_cbor(arg)) for _ in range(reps))
+    m = min(n, 4096)
+    t0 = time.perf_counter()
+    for r in raws[:m]:
+        B.byron_status(r)
+    tpy = time.perf_counter() - t0
+    return {"headers": n, "all_valid": bool(v.all()),
+            "boundary_headers": int((st == B.PACK_EBB).sum()),
+            "pack_headers_per_s": round(n / tp, 1), "pack_threads": threads,
+            "verify_cbor_headers_per_s": round(n / tv, 1),
+            "python_slicer_headers_per_s": round(m / tpy, 1),
+            "note": "golden Byron headers repeated; pageable host memory in, verdicts out"}
+
+
 def _timed(fn) -> float:
     t0 = time.perf_counter()
     fn()
@@ -1204,6 +1241,11 @@ def main():
                 out["raw_cbor"] = raw_leg(n, args.pools, device, cpu["usable"])
             except Exception as e:  # noqa: BLE001
                 out["raw_cbor"] = {"error": str(e)}
+        if not args.no_e2e and world == 1:
+            try:
+                out["byron_cbor"] = byron_leg(1 << 18, cpu["usable"])
+            except Exception as e:  # noqa: BLE001
+                out["byron_cbor"] = {"error": str(e)}
         if not args.no_latency and world == 1:
             try:
                 nt, _, npool = synth_headers(64, args.pools, device, keep_pool=True)

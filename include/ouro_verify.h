@@ -266,6 +266,9 @@ int ouro_tpraos_verify_batch(const ouro_tpraos_batch *b, uint8_t *verdict,
 #define OURO_PACK_ESIZE 3u  /* a fixed-size crypto field has the wrong length  */
 #define OURO_PACK_EBYRON 4u /* HFC era 0: a Byron header, not TPraos          */
 #define OURO_PACK_ESPAN 5u  /* (device slicer) span outside raw_bytes          */
+#define OURO_PACK_EBB 6u    /* (Byron slicer) an epoch-boundary header: PBFT
+                               checks no signature on it (PBFT.hs:327-328)     */
+#define OURO_PACK_ESHELLEY 7u /* (Byron slicer) HFC era >= 1: not a Byron header */
 size_t ouro_tpraos_pack_bytes(size_t n);
 int ouro_tpraos_pack_cbor(const uint8_t *raw, size_t raw_bytes, const uint64_t *off,
                           const uint32_t *len, size_t n, uint64_t slots_per_kes_period,
@@ -283,6 +286,58 @@ int ouro_tpraos_pack_cbor_device(void *stream, const uint8_t *raw, size_t raw_by
                                  uint64_t slots_per_kes_period, void *arena, size_t arena_bytes,
                                  ouro_tpraos_batch *out, uint64_t *slot, uint8_t *era,
                                  uint8_t *status);
+
+/* Raw Byron header CBOR -> the inputs of its PBFT block-signature check
+ * (SURVEY.md §8(f) row 4).  Replaces the per-header decode + message assembly
+ * in front of ByronDSIGN.verifyDSIGN: Byron/Ledger/PBFT.hs:47-73 builds
+ * PBftFields and recoverSignedBytes from the decoded header, PBFT.hs:332-337
+ * verifies them (caller: ChainSync's validateHeader; Integrity.hs:32-35 from
+ * storage).  Header i is raw[off[i] .. off[i] + len[i]) in any of the forms
+ * the reference sends (Byron/Node/Serialisation.hs:87-101, 197-210):
+ *   #6.24(bytes .cbor [kind, header])                      Byron / Cardano N2N v1
+ *   [[kind, size], #6.24(bytes .cbor header)]              Byron N2N v2
+ *   [0, [[kind, size], #6.24(bytes .cbor header)]]         Cardano N2N v2+
+ * kind 1 = regular, 0 = epoch boundary (status OURO_PACK_EBB: no signature,
+ * fields unchecked).  For a regular header the batch receives pk =
+ * delegateXPub[0:32] (pbftIssuer), sig, genesis_vk = the delegation
+ * certificate's issuer XPub (pbftGenKey), delegate_vk, the header's
+ * protocol magic, and the signed message
+ *   "01" || genesis_vk || 0x09 || CBOR(magic) || 0x85 || prevHash || bodyProof
+ *   || slotId || difficulty || extraData                    (raw field bytes)
+ * at msg + msg_off[i] (msg_len[i] bytes), magic = protocol_magic (the node's
+ * ProtocolMagicId, mkByronContextDSIGN at Byron/Ledger/PBFT.hs:43-44) or,
+ * for protocol_magic = -1, each header's own field.  The arena holds all of
+ * it: ouro_byron_pack_bytes(n, len) bytes, any alignment.  status[i] =
+ * OURO_PACK_* (OK, ECBOR, ESHAPE, ESIZE, EBB, ESHELLEY); rows of other
+ * statuses are zero with msg_len 0.  nthreads as for ouro_tpraos_pack_cbor.
+ * Host-only.  OURO_EINVAL for a span outside raw_bytes, a short arena, a
+ * protocol_magic outside -1 .. 2^32 - 1, NULLs. */
+typedef struct {
+  size_t n;
+  const uint8_t *pk;          /* n x 32  delegate XPub[0:32]                  */
+  const uint8_t *sig;         /* n x 64  block signature                      */
+  const uint8_t *msg;         /* signed messages                              */
+  const uint64_t *msg_off;    /* n       offsets into msg                     */
+  const uint32_t *msg_len;    /* n                                            */
+  const uint8_t *genesis_vk;  /* n x 64  delegation certificate issuer XPub   */
+  const uint8_t *delegate_vk; /* n x 64  delegate XPub                        */
+  const uint64_t *magic;      /* n       the header's protocolMagic field     */
+} ouro_byron_batch;
+size_t ouro_byron_pack_bytes(size_t n, const uint32_t *len);
+int ouro_byron_pack_cbor(const uint8_t *raw, size_t raw_bytes, const uint64_t *off,
+                         const uint32_t *len, size_t n, int64_t protocol_magic, void *arena,
+                         size_t arena_bytes, ouro_byron_batch *out, uint8_t *status,
+                         int nthreads);
+/* Raw Byron headers -> verdicts in one call: ouro_byron_pack_cbor, then the
+ * ByronDSIGN batch verify of the packed rows on the calling thread's stream.
+ * verdict[i] = 1 for a regular header whose block signature verifies and for
+ * an epoch-boundary header (PBftValidateBoundary checks nothing), else 0;
+ * status[i] as above.  The delegation lookup and the signing-window
+ * threshold (PBFT.hs:344-357) stay with the caller: they are ledger state,
+ * not crypto. */
+int ouro_byron_verify_cbor(const uint8_t *raw, size_t raw_bytes, const uint64_t *off,
+                           const uint32_t *len, size_t n, int64_t protocol_magic,
+                           uint8_t *status, uint8_t *verdict);
 
 /* The host-side UPDN fold (ledger-specs; the per-header step of
  * SL.updateChainDepState after the crypto): for i = 0..n-1

@@ -8,7 +8,8 @@ is the gfx950 library ``lib/libouro_verify.so`` behind the C ABI in
 """
 from . import _native
 from ._native import DeviceError, NativeUnavailable
-from .byron import ByronDSIGN, parse_byron_header, verify_byron_headers
+from .byron import (ByronDSIGN, pack_byron_cbor, parse_byron_header, verify_byron_cbor,
+                    verify_byron_headers)
 from .dsign import Ed25519DSIGN
 from .kes import Sum6KES, kes_period
 from .tpraos import HeaderBatch, first_invalid, verify_headers, verify_headers_multi
@@ -24,7 +25,9 @@ __all__ = [
     "Sum6KES",
     "first_invalid",
     "kes_period",
+    "pack_byron_cbor",
     "parse_byron_header",
+    "verify_byron_cbor",
     "verify_byron_headers",
     "verify_headers",
     "verify_headers_multi",

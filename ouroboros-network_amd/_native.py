@@ -76,6 +76,14 @@ class TPraosBatch(ctypes.Structure):
     ]
 
 
+class ByronBatch(ctypes.Structure):
+    """Mirror of ``ouro_byron_batch`` (include/ouro_verify.h)."""
+
+    _fields_ = [("n", ctypes.c_size_t)] + [
+        (f, ctypes.c_void_p) for f in ("pk", "sig", "msg", "msg_off", "msg_len", "genesis_vk",
+                                       "delegate_vk", "magic")]
+
+
 # every symbol include/ouro_verify.h declares, with its ctypes signature
 _P = ctypes.c_void_p
 _SZ = ctypes.c_size_t
@@ -119,6 +127,10 @@ SIGNATURES = {
     "ouro_tpraos_pack_bytes": (_SZ, [_SZ]),
     "ouro_tpraos_pack_cbor": (_I, [_P, _SZ, _P, _P, _SZ, ctypes.c_uint64, _P, _SZ,
                                    ctypes.POINTER(TPraosBatch), _P, _P, _P, _I]),
+    "ouro_byron_pack_bytes": (_SZ, [_SZ, _P]),
+    "ouro_byron_pack_cbor": (_I, [_P, _SZ, _P, _P, _SZ, ctypes.c_int64, _P, _SZ,
+                                  ctypes.POINTER(ByronBatch), _P, _I]),
+    "ouro_byron_verify_cbor": (_I, [_P, _SZ, _P, _P, _SZ, ctypes.c_int64, _P, _P]),
     "ouro_tpraos_pack_cbor_device": (_I, [_P, _P, _SZ, _P, _P, _SZ, ctypes.c_uint64, _P, _SZ,
                                           ctypes.POINTER(TPraosBatch), _P, _P, _P]),
 }

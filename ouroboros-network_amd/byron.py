@@ -22,13 +22,13 @@ the Byron storage integrity check,
 from __future__ import annotations
 
 from dataclasses import dataclass
-from typing import List, Sequence, Tuple
+from typing import List, Optional, Sequence, Tuple
 
 import numpy as np
 
 from . import _native
 from ._pack import as_rows, msgs_arg, ptr
-from .header import CBORError, _head, array_items, bytes_at
+from .header import CBORError, _head, array_items, skip
 
 SIZE_VERKEY = 64   # XPub = public key (32) || chain code (32)
 SIZE_SIG = 64
@@ -99,72 +99,281 @@ class ByronDSIGN:
 
 
 # ---- Byron header slicer -----------------------------------------------------
+# Wire forms (ouroboros-consensus-byron/src/Ouroboros/Consensus/Byron/Node/Serialisation.hs):
+#   F1  #6.24(bytes .cbor [kind, header])           Byron N2N v1 (:87-92), Cardano N2N v1
+#   F2  [[kind, size], #6.24(bytes .cbor header)]   Byron N2N v2 (encodeDisk, :197-210)
+#   F3  [0, F2]                                     Cardano N2N v2+ (HFC era 0)
+# kind 1 = regular, 0 = epoch boundary (EBB).  The C slicer (csrc/cbor_byron.h,
+# ouro_byron_pack_cbor) makes the same checks in the same order and reports
+# the same status (tests/test_pack_byron.py).
+
+PACK_OK, PACK_ECBOR, PACK_ESHAPE, PACK_ESIZE = 0, 1, 2, 3
+PACK_EBB, PACK_ESHELLEY = 6, 7
+WORD32_MAX = 0xFFFFFFFF
+MSG_EXTRA = 80  # message slot per header: len + MSG_EXTRA bytes (cbor_byron.h)
+
+
+class ByronPackError(CBORError):
+    """A header the slicer rejects; .status is the OURO_PACK_* code."""
+
+    def __init__(self, status: int, what: str):
+        super().__init__(what)
+        self.status = status
+
 
 @dataclass
 class ByronHeader:
     """The fields of a Byron regular (non-EBB) header the block signature needs."""
-    magic: int
+    magic: int            # the header's protocolMagic field
     to_sign: bytes        # recoverBytes of ToSign: 0x85 || prevHash || bodyProof || slot || diff || extra
     issuer_xpub: bytes    # delegation certificate issuer = the genesis key of SignBlock
     delegate_xpub: bytes  # signing (delegate) key
     sig: bytes            # 64-byte block signature
     slot_raw: bytes
 
-    def message(self) -> bytes:
-        return sign_tag_block(self.magic, self.issuer_xpub) + self.to_sign
+    def message(self, protocol_magic: Optional[int] = None) -> bytes:
+        """signTag magic (SignBlock genKey) || signed bytes; magic = the node's
+        configured ProtocolMagicId (mkByronContextDSIGN,
+        ouroboros-consensus-byron/src/Ouroboros/Consensus/Byron/Ledger/PBFT.hs:43-44),
+        or the header's own field when None."""
+        m = self.magic if protocol_magic is None else protocol_magic
+        return sign_tag_block(m, self.issuer_xpub) + self.to_sign
+
+
+def _fail(status: int, what: str):
+    raise ByronPackError(status, what)
+
+
+def _items(buf: bytes, i: int, want: int) -> List[Tuple[int, int]]:
+    """A definite array of exactly `want` items (cbor_byron.h fixed_array)."""
+    try:
+        it = array_items(buf, i)
+    except (CBORError, IndexError):
+        _fail(PACK_ECBOR, f"malformed array at {i}")
+    if len(it) != want:
+        _fail(PACK_ESHAPE, f"expected {want} items at {i}")
+    return it
+
+
+def _uint(buf: bytes, i: int, mx: int, what: str) -> int:
+    mt, arg, _ = _head(buf, i)
+    if mt != 0 or arg < 0 or arg > mx:
+        _fail(PACK_ESHAPE, what)
+    return arg
+
+
+def _bytes64(buf: bytes, i: int, what: str) -> bytes:
+    mt, arg, j = _head(buf, i)
+    if mt != 2 or arg < 0 or j + arg > len(buf):
+        _fail(PACK_ESHAPE, what)
+    if arg != SIZE_SIG:
+        _fail(PACK_ESIZE, f"{what}: expected 64 bytes")
+    return bytes(buf[j:j + arg])
+
+
+def _parse(raw: bytes) -> Optional[ByronHeader]:
+    buf = bytes(raw)
+    mt, arg, j = _head(buf, 0)
+    pos, kind = 0, 0
+    nested = mt == 4 and arg == 2
+    if nested:
+        mt1, a1, j1 = _head(buf, j)
+        if mt1 == 0:  # F3: the HFC era, then F2
+            if a1 < 0:
+                _fail(PACK_ESHAPE, "era")
+            if a1 != 0:
+                _fail(PACK_ESHELLEY, f"HFC era {a1}: not a Byron header")
+            pos = j1
+            mt, arg, j = _head(buf, pos)
+            if mt != 4 or arg != 2:
+                _fail(PACK_ESHAPE, "expected [[kind, size], header]")
+        ks = _items(buf, j, 2)
+        kind = _uint(buf, ks[0][0], 255, "kind: Word8")
+        _uint(buf, ks[1][0], WORD32_MAX, "size: Word32")
+        if kind > 1:
+            _fail(PACK_ESHAPE, f"unknown header kind {kind}")
+        pos = ks[1][1]
+    mt, arg, j = _head(buf, pos)
+    if mt != 6 or arg != 24:
+        _fail(PACK_ESHAPE, "expected tag 24")
+    mt, arg, k = _head(buf, j)
+    if mt != 2 or arg < 0:
+        _fail(PACK_ESHAPE, "expected definite CBOR-in-bytes")
+    if k + arg != len(buf):
+        _fail(PACK_ECBOR, "payload past the span or bytes after the header")
+    h = k
+    if not nested:  # F1: [kind, header]
+        top = _items(buf, k, 2)
+        kind = _uint(buf, top[0][0], 2**64 - 1, "kind")
+        if kind > 1:
+            _fail(PACK_ESHAPE, f"unknown header kind {kind}")
+        h = top[1][0]
+    if kind == 0:  # epoch boundary: no signature; its fields are not checked
+        if skip(buf, h) != len(buf):
+            _fail(PACK_ECBOR, "trailing bytes in CBOR-in-CBOR")
+        return None
+    f = _items(buf, h, 5)
+    if f[4][1] != len(buf):
+        _fail(PACK_ECBOR, "trailing bytes in CBOR-in-CBOR")
+    magic = _uint(buf, f[0][0], WORD32_MAX, "protocol magic: Word32")
+    cons = _items(buf, f[3][0], 4)
+    bsig = _items(buf, cons[3][0], 2)
+    mt, sigkind, _ = _head(buf, bsig[0][0])
+    if mt != 0 or sigkind != 2:
+        _fail(PACK_ESHAPE, "block signature kind (only delegated, 2)")
+    inner = _items(buf, bsig[1][0], 2)
+    cert = _items(buf, inner[0][0], 4)
+    shape = []
+    vals = []
+    for at, what in ((cert[1][0], "issuer"), (cert[2][0], "delegate"), (inner[1][0], "sig")):
+        try:
+            vals.append(_bytes64(buf, at, what))
+            shape.append(PACK_OK)
+        except ByronPackError as e:
+            vals.append(None)
+            shape.append(e.status)
+    if PACK_ESHAPE in shape:
+        _fail(PACK_ESHAPE, "key/signature types")
+    if PACK_ESIZE in shape:
+        _fail(PACK_ESIZE, "key/signature sizes")
+    raw_of = lambda it: buf[it[0]:it[1]]  # noqa: E731
+    to_sign = (b"\x85" + raw_of(f[1]) + raw_of(f[2]) + raw_of(cons[0]) + raw_of(cons[2])
+               + raw_of(f[4]))
+    return ByronHeader(magic=magic, to_sign=to_sign, issuer_xpub=vals[0], delegate_xpub=vals[1],
+                       sig=vals[2], slot_raw=raw_of(cons[0]))
+
+
+def byron_status(raw: bytes) -> Tuple[int, Optional[ByronHeader]]:
+    """(OURO_PACK_* status, the header or None) -- what ouro_byron_pack_cbor
+    reports for this header."""
+    try:
+        h = _parse(raw)
+    except ByronPackError as e:
+        return e.status, None
+    except (CBORError, IndexError):
+        return PACK_ECBOR, None
+    return (PACK_EBB, None) if h is None else (PACK_OK, h)
 
 
 def parse_byron_header(raw: bytes) -> ByronHeader:
-    """Slice a Byron N2N header, ``#6.24(bytes .cbor [1, header])`` with
-    header = [magic, prevHash, bodyProof, consensusData, extraData] and
-    consensusData = [slotId, leaderKey, difficulty, blockSig]; blockSig =
-    [2, [dlgCert, sig]] (the delegated signature used on mainnet; golden fixture
-    ouroboros-consensus-byron-test/test/golden/ByronNodeToNodeVersion1/Header_regular).
-    The signed bytes are the raw encodings of the ToSign fields, never re-encoded."""
-    mt, arg, j = _head(raw, 0)
-    if mt != 6 or arg != 24:
-        raise CBORError("Byron header: expected tag 24")
-    mt, arg, k = _head(raw, j)
-    if mt != 2:
-        raise CBORError("Byron header: expected bytes")
-    buf = raw[k:k + arg]
-    outer = array_items(buf, 0)
-    if len(outer) != 2:
-        raise CBORError("Byron header: expected [kind, header]")
-    kind = buf[outer[0][0]]
-    if kind != 0x01:
-        raise CBORError("Byron header: epoch-boundary headers carry no signature")
-    hdr = array_items(buf, outer[1][0])
-    if len(hdr) != 5:
-        raise CBORError("Byron header: expected 5 fields")
-    mt, magic, _ = _head(buf, hdr[0][0])
-    if mt != 0:
-        raise CBORError("Byron header: magic")
-    cons = array_items(buf, hdr[3][0])
-    if len(cons) != 4:
-        raise CBORError("Byron header: consensus data")
-    raw_of = lambda it: buf[it[0]:it[1]]  # noqa: E731
-    to_sign = (b"\x85" + raw_of(hdr[1]) + raw_of(hdr[2]) + raw_of(cons[0]) + raw_of(cons[2])
-               + raw_of(hdr[4]))
-    bsig = array_items(buf, cons[3][0])
-    mt, sigkind, _ = _head(buf, bsig[0][0])
-    if sigkind != 2:
-        raise CBORError(f"Byron header: block signature kind {sigkind} (only delegated, 2)")
-    inner = array_items(buf, bsig[1][0])
-    cert = array_items(buf, inner[0][0])
-    issuer = bytes_at(buf, cert[1][0])
-    delegate = bytes_at(buf, cert[2][0])
-    sig = bytes_at(buf, inner[1][0])
-    if len(issuer) != SIZE_VERKEY or len(delegate) != SIZE_VERKEY or len(sig) != SIZE_SIG:
-        raise CBORError("Byron header: key/signature sizes")
-    return ByronHeader(magic=magic, to_sign=to_sign, issuer_xpub=issuer, delegate_xpub=delegate,
-                       sig=sig, slot_raw=raw_of(cons[0]))
+    """Slice a regular Byron header in any of the wire forms F1-F3 above
+    (golden fixtures: ouroboros-consensus-byron-test/test/golden/ByronNodeToNodeVersion1/Header_regular,
+    ouroboros-consensus-cardano-test/test/golden/CardanoNodeToNodeVersion{1,2,3,4}/Header_Byron_regular).
+    The signed bytes are the raw encodings of the ToSign fields, never
+    re-encoded; the block signature is the delegated one, [2, [dlgCert, sig]].
+    Raises CBORError (ByronPackError with the slicer's status) otherwise, an
+    epoch-boundary header included."""
+    st, h = byron_status(raw)
+    if st != PACK_OK:
+        raise ByronPackError(st, "epoch-boundary headers carry no signature" if st == PACK_EBB
+                             else f"not a regular Byron header (status {st})")
+    return h
 
 
-def verify_byron_headers(headers: Sequence[ByronHeader]) -> np.ndarray:
-    """PBFT block-signature check of a batch of Byron headers (PBFT.hs:332-337):
-    one gfx950 launch, bool per header."""
-    msgs: List[bytes] = [h.message() for h in headers]
+@dataclass
+class PackedByron:
+    """ouro_byron_pack_cbor's output as arrays (views into its arena)."""
+    pk: np.ndarray           # (n, 32)
+    sig: np.ndarray          # (n, 64)
+    genesis_vk: np.ndarray   # (n, 64)
+    delegate_vk: np.ndarray  # (n, 64)
+    magic: np.ndarray        # (n,) uint64
+    msg: np.ndarray          # message bytes
+    msg_off: np.ndarray      # (n,) uint64
+    msg_len: np.ndarray      # (n,) uint32
+    status: np.ndarray       # (n,) uint8 PACK_*
+    _keep: tuple = ()
+
+    def message(self, i: int) -> bytes:
+        o = int(self.msg_off[i])
+        return bytes(self.msg[o:o + int(self.msg_len[i])])
+
+
+def _raw_arg(raw_headers):
+    if isinstance(raw_headers, tuple) and len(raw_headers) == 3:
+        buf, off, ln = raw_headers
+        buf = np.frombuffer(buf, np.uint8) if isinstance(buf, (bytes, bytearray)) else \
+            np.ascontiguousarray(buf, np.uint8).reshape(-1)
+        return buf, np.ascontiguousarray(off, np.uint64), np.ascontiguousarray(ln, np.uint32)
+    items = [bytes(r) for r in raw_headers]
+    ln = np.array([len(r) for r in items], np.uint32)
+    off = np.zeros(len(items), np.uint64)
+    if len(items) > 1:
+        off[1:] = np.cumsum(ln[:-1], dtype=np.uint64)
+    return np.frombuffer(b"".join(items) or b"\0", np.uint8), off, ln
+
+
+def _magic_arg(protocol_magic: Optional[int]) -> int:
+    if protocol_magic is None:
+        return -1
+    if not 0 <= protocol_magic <= WORD32_MAX:
+        raise ValueError("protocol_magic: a Word32")
+    return int(protocol_magic)
+
+
+def pack_byron_cbor(raw_headers, protocol_magic: Optional[int] = None,
+                    nthreads: int = 0) -> PackedByron:
+    """Raw Byron headers -> keys, signatures and signed messages through the C
+    slicer (include/ouro_verify.h ouro_byron_pack_cbor, csrc/pack.cpp).
+    raw_headers: a sequence of bytes, or (buf, off, len).  protocol_magic:
+    the node's ProtocolMagicId for the sign tag (None: each header's own)."""
+    import ctypes
+
+    from .header import _pack_lib
+    lib = _pack_lib() or _native.load()
+    buf, off, ln = _raw_arg(raw_headers)
+    n = int(off.size)
+    if ln.size != n:
+        raise ValueError("off / len: one entry per header")
+    nbytes = int(lib.ouro_byron_pack_bytes(n, ptr(ln)))
+    arena = np.empty(nbytes, np.uint8)
+    status = np.zeros(max(n, 1), np.uint8)
+    out = _native.ByronBatch()
+    rc = lib.ouro_byron_pack_cbor(ptr(buf), buf.size, ptr(off), ptr(ln), n,
+                                  _magic_arg(protocol_magic), ptr(arena), nbytes,
+                                  ctypes.byref(out), ptr(status), nthreads)
+    if rc != _native.OURO_OK:
+        raise ValueError(f"ouro_byron_pack_cbor: {rc} (spans outside the buffer?)")
+    base = arena.ctypes.data
+
+    def view(addr, dt, w, cnt=None):
+        if n == 0:
+            return np.zeros((0, w) if w else 0, dt)
+        cnt = cnt if cnt is not None else n * (w or 1)
+        a = arena[addr - base: addr - base + cnt * np.dtype(dt).itemsize].view(dt)
+        return a.reshape(n, w) if w else a
+
+    return PackedByron(
+        pk=view(out.pk, np.uint8, 32), sig=view(out.sig, np.uint8, 64),
+        genesis_vk=view(out.genesis_vk, np.uint8, 64),
+        delegate_vk=view(out.delegate_vk, np.uint8, 64), magic=view(out.magic, np.uint64, None),
+        msg=arena[out.msg - base:] if n else np.zeros(0, np.uint8),
+        msg_off=view(out.msg_off, np.uint64, None), msg_len=view(out.msg_len, np.uint32, None),
+        status=status[:n], _keep=(arena, buf))
+
+
+def verify_byron_cbor(raw_headers, protocol_magic: Optional[int] = None):
+    """Raw Byron headers -> (verdict bool array, status array) in one call
+    (ouro_byron_verify_cbor): a regular header is valid when its block
+    signature verifies, an epoch-boundary header always (PBFT.hs:327-328)."""
+    lib = _native.load()
+    buf, off, ln = _raw_arg(raw_headers)
+    n = int(off.size)
+    status = np.zeros(max(n, 1), np.uint8)
+    verdict = np.zeros(max(n, 1), np.uint8)
+    if n:
+        rc = lib.ouro_byron_verify_cbor(ptr(buf), buf.size, ptr(off), ptr(ln), n,
+                                        _magic_arg(protocol_magic), ptr(status), ptr(verdict))
+        _native.check(rc, "ouro_byron_verify_cbor")
+    return verdict[:n].astype(bool), status[:n]
+
+
+def verify_byron_headers(headers: Sequence[ByronHeader],
+                         protocol_magic: Optional[int] = None) -> np.ndarray:
+    """PBFT block-signature check of a batch of parsed Byron headers
+    (PBFT.hs:332-337): one gfx950 launch, bool per header.  Raw headers go
+    through verify_byron_cbor instead (the C slicer, no per-header Python)."""
+    msgs: List[bytes] = [h.message(protocol_magic) for h in headers]
     pks = [h.delegate_xpub[:32] for h in headers]
     sigs = [h.sig for h in headers]
     return ByronDSIGN.verify_batch(pks, msgs, sigs)

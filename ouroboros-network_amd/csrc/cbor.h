@@ -43,14 +43,14 @@ OURO_HD inline void copy_bytes(uint8_t* d, const uint8_t* s, int n) {
     stg4(d + k, make_int4((int)o[0], (int)o[1], (int)o[2], (int)o[3]));
   }
 #else
-  for (int k = 0; k < n; k++) d[k] = s[k];
+  __builtin_memcpy(d, s, (size_t)n);
 #endif
 }
 OURO_HD inline void zero_bytes(uint8_t* d, int n) {  // n a multiple of 16, d 16-byte aligned
 #if defined(__HIP_DEVICE_COMPILE__)
   for (int k = 0; k < n; k += 16) stg4(d + k, make_int4(0, 0, 0, 0));
 #else
-  for (int k = 0; k < n; k++) d[k] = 0;
+  __builtin_memset(d, 0, (size_t)n);
 #endif
 }
 

@@ -10,6 +10,8 @@
 #include <cstdio>
 #include <cstring>
 #include <map>
+#include <memory>
+#include <new>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -814,6 +816,26 @@ int ouro_byron_ed25519_verify_batch(size_t n, const uint8_t* pk, const uint8_t* 
                                     const uint8_t* msg, const uint64_t* msg_off,
                                     const uint32_t* msg_len, uint8_t* verdict) {
   return ed_batch_host(n, pk, sig, msg, msg_off, msg_len, verdict, 1);
+}
+
+int ouro_byron_verify_cbor(const uint8_t* raw, size_t raw_bytes, const uint64_t* off,
+                           const uint32_t* len, size_t n, int64_t protocol_magic,
+                           uint8_t* status, uint8_t* verdict) {
+  if (n == 0) return OURO_OK;
+  if (!status || !verdict || !len) return fail(OURO_EINVAL, "null argument");
+  const size_t nb = ouro_byron_pack_bytes(n, len);
+  std::unique_ptr<uint8_t[]> arena(new (std::nothrow) uint8_t[nb]);  // not zeroed: the slicer writes every row
+  if (!arena) return fail(OURO_EDEVICE, "ouro_byron_verify_cbor: out of host memory");
+  ouro_byron_batch b;
+  int rc = ouro_byron_pack_cbor(raw, raw_bytes, off, len, n, protocol_magic, arena.get(), nb, &b,
+                                status, 0);
+  if (rc) return fail(rc, "ouro_byron_pack_cbor: bad arguments");
+  // rejected rows are zero with msg_len 0; their verdicts are masked below
+  if ((rc = ouro_byron_ed25519_verify_batch(n, b.pk, b.sig, b.msg, b.msg_off, b.msg_len, verdict)))
+    return rc;
+  for (size_t i = 0; i < n; i++)
+    verdict[i] = status[i] == OURO_PACK_EBB ? 1 : (status[i] == OURO_PACK_OK && verdict[i]);
+  return OURO_OK;
 }
 
 int ouro_vrf03_verify_batch(size_t n, const uint8_t* pk, const uint8_t* proof, const uint8_t* alpha,

@@ -1,5 +1,7 @@
 // pack.cpp -- raw TPraos header CBOR -> the SoA of ouro_tpraos_batch
-// (include/ouro_verify.h ouro_tpraos_pack_cbor).
+// (include/ouro_verify.h ouro_tpraos_pack_cbor), and
+// raw Byron header CBOR -> ouro_byron_batch (row 4, ouro_byron_pack_cbor;
+// the parse is csrc/cbor_byron.h).
 //
 // Host code (no device): it sits between the ChainSync client, which hands
 // over headers as the raw CBOR it received, and the batch verifier.  Wire
@@ -25,10 +27,39 @@
 
 #include "../../include/ouro_verify.h"
 #include "cbor.h"
+#include "cbor_byron.h"
 
 namespace {
 
 using namespace ouro::cbor;
+
+// work(lo, hi) over [0, n) on up to `nthreads` threads (<= 0: one per
+// hardware thread), at least 4096 headers each: below that a thread costs
+// more than it saves
+template <class F>
+void parallel_rows(size_t n, int nthreads, F work) {
+  size_t threads = nthreads > 0 ? (size_t)nthreads
+                                : std::max<unsigned>(1, std::thread::hardware_concurrency());
+  threads = std::max<size_t>(1, std::min(threads, (n + 4095) / 4096));
+  threads = std::min<size_t>(threads, 64);
+  if (threads <= 1) {
+    work(0, n);
+    return;
+  }
+  std::vector<std::thread> pool;
+  const size_t per = (n + threads - 1) / threads;
+  for (size_t t = 0; t < threads; t++) {
+    const size_t lo = t * per, hi = std::min(n, lo + per);
+    if (lo < hi) pool.emplace_back(work, lo, hi);
+  }
+  for (auto& th : pool) th.join();
+}
+
+size_t byron_msg_bytes(size_t n, const uint32_t* len) {
+  size_t s = 0;
+  for (size_t i = 0; i < n; i++) s += (size_t)len[i] + kByronMsgExtra;
+  return s;
+}
 
 }  // namespace
 
@@ -46,30 +77,55 @@ int ouro_tpraos_pack_cbor(const uint8_t* raw, size_t raw_bytes, const uint64_t* 
   for (size_t i = 0; i < n; i++)  // every span inside raw (checked without wrapping)
     if (off[i] > raw_bytes || raw_bytes - off[i] < len[i]) return OURO_EINVAL;
   const Out o = arena_out(arena_base(arena), n, slot, era);
-  auto work = [&](size_t lo, size_t hi) {
+  parallel_rows(n, nthreads, [&](size_t lo, size_t hi) {
     for (size_t i = lo; i < hi; i++) {
       const uint8_t st = pack_one(raw, off[i], len[i], slots_per_kes_period, o, i);
       status[i] = st;
       if (st != OURO_PACK_OK) zero_row(o, i);
     }
-  };
-  // at least 4096 headers per thread: below that a thread costs more than it saves
-  size_t threads = nthreads > 0 ? (size_t)nthreads
-                                : std::max<unsigned>(1, std::thread::hardware_concurrency());
-  threads = std::max<size_t>(1, std::min(threads, (n + 4095) / 4096));
-  threads = std::min<size_t>(threads, 64);
-  if (threads <= 1) {
-    work(0, n);
-  } else {
-    std::vector<std::thread> pool;
-    const size_t per = (n + threads - 1) / threads;
-    for (size_t t = 0; t < threads; t++) {
-      const size_t lo = t * per, hi = std::min(n, lo + per);
-      if (lo < hi) pool.emplace_back(work, lo, hi);
-    }
-    for (auto& th : pool) th.join();
-  }
+  });
   batch_from(out, o, raw, n);
+  return OURO_OK;
+}
+
+size_t ouro_byron_pack_bytes(size_t n, const uint32_t* len) {
+  if (n > 0 && !len) return 0;
+  return byron_layout(n, byron_msg_bytes(n, len)).total + 64;
+}
+
+int ouro_byron_pack_cbor(const uint8_t* raw, size_t raw_bytes, const uint64_t* off,
+                         const uint32_t* len, size_t n, int64_t protocol_magic, void* arena,
+                         size_t arena_bytes, ouro_byron_batch* out, uint8_t* status,
+                         int nthreads) {
+  if (!out || !status) return OURO_EINVAL;
+  if (protocol_magic < -1 || protocol_magic > (int64_t)kWord32Max) return OURO_EINVAL;
+  if (n > 0 && (!raw || !off || !len || !arena)) return OURO_EINVAL;
+  if (arena_bytes < ouro_byron_pack_bytes(n, len)) return OURO_EINVAL;
+  for (size_t i = 0; i < n; i++)
+    if (off[i] > raw_bytes || raw_bytes - off[i] < len[i]) return OURO_EINVAL;
+  const ByronLayout l = byron_layout(n, byron_msg_bytes(n, len));
+  const ByronOut o = byron_arena_out(arena_base(arena), l);
+  uint64_t at = 0;  // message slots: len[i] + kByronMsgExtra bytes each, in order
+  for (size_t i = 0; i < n; i++) {
+    o.msg_off[i] = at;
+    at += (uint64_t)len[i] + kByronMsgExtra;
+  }
+  parallel_rows(n, nthreads, [&](size_t lo, size_t hi) {
+    for (size_t i = lo; i < hi; i++) {
+      const uint8_t st = byron_pack_one(raw, off[i], len[i], protocol_magic, o, i);
+      status[i] = st;
+      if (st != OURO_PACK_OK) byron_zero_row(o, i);
+    }
+  });
+  out->n = n;
+  out->pk = o.pk;
+  out->sig = o.sig;
+  out->msg = o.msg;
+  out->msg_off = o.msg_off;
+  out->msg_len = o.msg_len;
+  out->genesis_vk = o.genesis_vk;
+  out->delegate_vk = o.delegate_vk;
+  out->magic = o.magic;
   return OURO_OK;
 }
 

@@ -283,7 +283,8 @@ def _pack_lib():
 
         from . import _native
         lib = ctypes.CDLL(path)
-        for name in ("ouro_tpraos_pack_bytes", "ouro_tpraos_pack_cbor"):
+        for name in ("ouro_tpraos_pack_bytes", "ouro_tpraos_pack_cbor", "ouro_byron_pack_bytes",
+                     "ouro_byron_pack_cbor"):
             res, args = _native.SIGNATURES[name]
             getattr(lib, name).restype = res
             getattr(lib, name).argtypes = args

@@ -84,6 +84,29 @@ def test_struct_offsets_match_the_c_compiler(tmp_path):
         assert getattr(_native.TPraosBatch, name).offset == c_off == orc_off, name
 
 
+def test_byron_batch_offsets_match_the_c_compiler(tmp_path):
+    """ouro_byron_batch as gcc lays it out = the ctypes mirror."""
+    import subprocess
+
+    from ouroboros_network_amd import _native
+
+    names = [f[0] for f in _native.ByronBatch._fields_]
+    src = tmp_path / "boff.c"
+    src.write_text(
+        '#include <stdio.h>\n#include <stddef.h>\n#include "ouro_verify.h"\nint main(void){\n'
+        'printf("%zu\\n", sizeof(ouro_byron_batch));\n'
+        + "".join(f'printf("%zu\\n", offsetof(ouro_byron_batch, {n}));\n' for n in names)
+        + "return 0;}\n")
+    exe = tmp_path / "boff"
+    subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)],
+                   check=True)
+    rows = [int(x) for x in subprocess.run([str(exe)], check=True, capture_output=True,
+                                            text=True).stdout.split()]
+    assert rows[0] == ctypes.sizeof(_native.ByronBatch) == 9 * 8
+    for (name, _), off in zip(_native.ByronBatch._fields_, rows[1:]):
+        assert getattr(_native.ByronBatch, name).offset == off, name
+
+
 SHIM = os.path.join(ROOT, "ouroboros-network_amd", "lib", "libouro_vrf_shim.so")
 SODIUM_SHIM = os.path.join(ROOT, "ouroboros-network_amd", "lib", "libouro_sodium_shim.so")
 

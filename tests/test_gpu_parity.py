@@ -463,6 +463,43 @@ def test_byron_batch_matches_oracle(small_path, gpu_lib):
     assert want.sum() > 700
 
 
+def test_byron_raw_headers_to_verdicts(small_path, gpu_lib, kats):
+    """ouro_byron_verify_cbor: the golden Byron headers in every wire form
+    (regular + epoch boundary) and every single-byte corruption of the v1 and
+    HFC regular ones, raw CBOR -> verdicts in one call; the expected verdict
+    is the Python slicer's status + the oracle's donna-style verify of the
+    message it assembles (EBB: valid, PBFT.hs:327-328).  Then the configured
+    protocol magic: the golden magic verifies, another one does not."""
+    from ouroboros_network_amd import byron as B
+
+    wires = [bytes.fromhex(w["raw"]) for w in kats["byron_wire"]]
+    regular = [w for w, d in zip(wires, kats["byron_wire"]) if d["kind"] == "regular"]
+    raws = list(wires)
+    for g in (regular[0], regular[2]):  # n2n v1, hfc
+        for pos in range(len(g)):
+            m = bytearray(g)
+            m[pos] ^= 0x04
+            raws.append(bytes(m))
+    got, status = B.verify_byron_cbor(raws)
+    want = []
+    for r in raws:
+        st, h = B.byron_status(r)
+        if st == B.PACK_EBB:
+            want.append(True)
+        elif st != B.PACK_OK:
+            want.append(False)
+        else:
+            want.append(O.ed25519_verify_byron(h.sig, h.message(), h.delegate_xpub[:32]))
+        assert status[len(want) - 1] == st
+    np.testing.assert_array_equal(got, np.array(want))
+    assert got[:len(wires)].all()
+    assert 0 < got[len(wires):].sum() < len(raws) - len(wires)
+    ok, _ = B.verify_byron_cbor(regular, protocol_magic=kats["byron"]["magic"])
+    assert ok.all()
+    bad, st = B.verify_byron_cbor(regular, protocol_magic=764824073)
+    assert not bad.any() and (st == B.PACK_OK).all()
+
+
 def test_kes_periods_beyond_the_tree(gpu_lib):
     """Periods >= 64 (the reference's Period is a 64-bit Word): every t >= 63
     walks right at all six levels to leaf 63 (SumKES.verifyKES; SingleKES's

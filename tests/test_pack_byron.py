@@ -1,0 +1,207 @@
+"""The C Byron header slicer (include/ouro_verify.h ouro_byron_pack_cbor,
+csrc/cbor_byron.h) against the Python one (byron.byron_status /
+parse_byron_header) on the reference's golden Byron headers in every wire form
+they hold (tests/golden/reference_kats.json "byron_wire", made by
+tools/make_golden.py) and on every single-byte corruption and truncation of
+them: the same status for every header, the same key, signature, XPubs, magic
+and signed message for every accepted one.  Host-only: no GPU."""
+import ctypes
+
+import numpy as np
+import pytest
+
+from ouroboros_network_amd import _native
+from ouroboros_network_amd import byron as B
+
+
+@pytest.fixture(scope="module")
+def wires(kats):
+    return [(w["form"], w["kind"], bytes.fromhex(w["raw"])) for w in kats["byron_wire"]]
+
+
+def assert_same(raws, pk, protocol_magic=None):
+    for i, r in enumerate(raws):
+        st, h = B.byron_status(r)
+        assert pk.status[i] == st, f"header {i}: C status {pk.status[i]}, Python {st}"
+        if st != B.PACK_OK:
+            assert pk.msg_len[i] == 0 and pk.magic[i] == 0
+            for a in (pk.pk, pk.sig, pk.genesis_vk, pk.delegate_vk):
+                assert not a[i].any(), f"rejected header {i}: row not zeroed"
+            continue
+        assert pk.message(i) == h.message(protocol_magic), f"header {i}: message"
+        assert bytes(pk.pk[i]) == h.delegate_xpub[:32]
+        assert bytes(pk.sig[i]) == h.sig
+        assert bytes(pk.genesis_vk[i]) == h.issuer_xpub
+        assert bytes(pk.delegate_vk[i]) == h.delegate_xpub
+        assert int(pk.magic[i]) == h.magic
+
+
+def test_golden_wire_forms(kats, wires):
+    g = kats["byron"]
+    raws = [r for _, _, r in wires]
+    pk = B.pack_byron_cbor(raws, nthreads=1)
+    assert_same(raws, pk)
+    for i, (form, kind, _) in enumerate(wires):
+        if kind == "boundary":
+            assert pk.status[i] == B.PACK_EBB
+            continue
+        assert pk.status[i] == B.PACK_OK, form
+        # every wrapper carries the golden block signature
+        assert pk.message(i).hex() == g["msg"]
+        assert bytes(pk.pk[i]).hex() == g["pk"] and bytes(pk.sig[i]).hex() == g["sig"]
+        assert int(pk.magic[i]) == g["magic"]
+    assert {f for f, _, _ in wires} == {"n2n_v1", "hfc"}
+
+
+def test_configured_magic_goes_into_the_sign_tag(kats, wires):
+    raws = [r for _, k, r in wires if k == "regular"]
+    same = B.pack_byron_cbor(raws, protocol_magic=kats["byron"]["magic"])
+    assert all(same.message(i).hex() == kats["byron"]["msg"] for i in range(len(raws)))
+    other = B.pack_byron_cbor(raws, protocol_magic=764824073)  # mainnet's
+    assert_same(raws, other, protocol_magic=764824073)
+    assert other.message(0) != same.message(0)
+    assert other.message(0)[67:72] == B.cbor_uint(764824073)
+    assert int(other.magic[0]) == kats["byron"]["magic"]  # the header's own field, unchanged
+    for bad in (-2, 2**32):
+        with pytest.raises(ValueError):
+            B.pack_byron_cbor(raws, protocol_magic=bad)
+
+
+def test_every_byte_corruption_matches_python(wires):
+    raws = []
+    for form, kind, g in wires[:2] + [w for w in wires if w[0] == "hfc"][:2]:
+        for pos in range(len(g)):
+            for x in (0x01, 0x20, 0x80, 0xFF):
+                m = bytearray(g)
+                m[pos] ^= x
+                raws.append(bytes(m))
+    pk = B.pack_byron_cbor(raws, nthreads=4)
+    assert_same(raws, pk)
+    seen = set(pk.status.tolist())
+    assert {B.PACK_OK, B.PACK_ECBOR, B.PACK_ESHAPE, B.PACK_EBB} <= seen, seen
+
+
+def test_every_truncation_rejected(wires):
+    for _, _, g in wires[:2] + [w for w in wires if w[0] == "hfc"][:2]:
+        raws = [g[:k] for k in range(len(g))]
+        pk = B.pack_byron_cbor(raws)
+        assert (pk.status != B.PACK_OK).all()
+        assert_same(raws, pk)
+
+
+def test_cbor_in_cbor_bounds(wires):
+    """As the reference's unwrapCBORinCBOR (ouroboros-network/src/Ouroboros/Network/Block.hs:509-514):
+    a payload length off by one, trailing bytes inside the payload or after
+    the header, an indefinite byte string are all rejected."""
+    for form, kind, g in wires:
+        if kind != "regular":
+            continue
+        at = g.index(bytes.fromhex("d81859")) + 3
+        ln = int.from_bytes(g[at:at + 2], "big")
+        pre, payload = g[:at], g[at + 2:]
+        assert len(payload) == ln
+        enc = lambda n: n.to_bytes(2, "big")  # noqa: E731
+        cases = [pre + enc(ln - 1) + payload, pre + enc(ln + 1) + payload,
+                 pre + enc(ln + 1) + payload + b"\x00", g + b"\x00",
+                 pre[:-1] + b"\x5f" + b"\x59" + enc(ln) + payload + b"\xff"]
+        pk = B.pack_byron_cbor(cases)
+        assert (pk.status != B.PACK_OK).all(), form
+        assert_same(cases, pk)
+
+
+def test_shape_rules(kats, wires):
+    """Statuses for hand-made headers: the HFC era of a Shelley-based header,
+    an unknown kind, a non-delegated block signature, a short XPub."""
+    v1 = next(r for f, k, r in wires if f == "n2n_v1" and k == "regular")
+    hfc = next(r for f, k, r in wires if f == "hfc" and k == "regular")
+    assert hfc[:2] == b"\x82\x00" and hfc[2:4] == b"\x82\x82"
+    shelley = bytes.fromhex(kats["headers"][0]["raw"])
+    b = v1.index(bytes.fromhex("82028284"))  # blockSig = [2, [[epoch, issuer, ...
+    assert v1[b + 5:b + 7] == b"\x58\x40"     # the issuer XPub's head
+    ln = int.from_bytes(v1[3:5], "big")      # the tag-24 payload length
+    short = (v1[:3] + (ln - 1).to_bytes(2, "big") + v1[5:b + 5] + b"\x58\x3f"
+             + v1[b + 7:b + 7 + 63] + v1[b + 7 + 64:])
+    cases = {
+        "shelley_era_1": b"\x82\x01" + hfc[2:],
+        "shelley_header": b"\x82\x01" + shelley,
+        "era_indefinite": b"\x82\x1f" + hfc[2:],
+        "byron_v2_unwrapped": hfc[2:],                      # F2 without the HFC era
+        "v2_kind_2": hfc[:4] + b"\x02" + hfc[5:],
+        "v1_kind_3": v1[:5] + b"\x82\x03" + v1[7:],
+        "shelley_as_byron_v1": shelley,
+        "sig_kind_0": v1[:b + 1] + b"\x00" + v1[b + 2:],
+        "short_issuer_xpub": short,
+    }
+    raws = list(cases.values())
+    pk = B.pack_byron_cbor(raws)
+    assert_same(raws, pk)
+    got = dict(zip(cases, pk.status.tolist()))
+    assert got["shelley_era_1"] == got["shelley_header"] == B.PACK_ESHELLEY
+    assert got["era_indefinite"] == B.PACK_ESHAPE
+    assert got["byron_v2_unwrapped"] == B.PACK_OK
+    assert pk.message(3) == B.pack_byron_cbor([hfc]).message(0)
+    assert got["v2_kind_2"] == got["v1_kind_3"] == B.PACK_ESHAPE
+    assert got["shelley_as_byron_v1"] in (B.PACK_ESHAPE, B.PACK_ECBOR)
+    assert got["sig_kind_0"] == B.PACK_ESHAPE
+    assert got["short_issuer_xpub"] == B.PACK_ESIZE
+
+
+def test_threads_and_spans_inside_one_buffer(wires):
+    rng = np.random.default_rng(11)
+    pool = [r for _, _, r in wires]
+    raws = [pool[int(k)] for k in rng.integers(0, len(pool), 9000)]
+    parts, off, ln, at = [], [], [], 0
+    for r in raws:
+        pad = bytes(rng.integers(0, 256, int(rng.integers(0, 5)), dtype=np.uint8))
+        parts += [pad, r]
+        off.append(at + len(pad))
+        ln.append(len(r))
+        at += len(pad) + len(r)
+    buf = b"".join(parts)
+    one = B.pack_byron_cbor((buf, off, ln), nthreads=1)
+    many = B.pack_byron_cbor((buf, off, ln), nthreads=3)
+    assert np.array_equal(one.status, many.status)
+    assert set(one.status.tolist()) == {B.PACK_OK, B.PACK_EBB}
+    for f in ("pk", "sig", "genesis_vk", "delegate_vk", "magic", "msg_len"):
+        assert np.array_equal(getattr(one, f), getattr(many, f)), f
+    for i in (0, 1, 4500, 8999):
+        assert one.message(i) == many.message(i)
+        assert_same([raws[i]], B.pack_byron_cbor([raws[i]]))
+
+
+def test_bad_arguments_are_einval(wires):
+    g = wires[0][2]
+    with pytest.raises(ValueError):
+        B.pack_byron_cbor((g, [0], [len(g) + 1]))      # span past the end
+    with pytest.raises(ValueError):
+        B.pack_byron_cbor((g, [2 ** 64 - 1], [4]))     # wrapping offset
+    lib = _native.load()
+    out = _native.ByronBatch()
+    assert lib.ouro_byron_pack_cbor(None, 0, None, None, 0, -1, None, 0, ctypes.byref(out),
+                                    None, 0) == _native.OURO_EINVAL
+    st = (ctypes.c_uint8 * 1)()
+    small = (ctypes.c_uint8 * 64)()
+    buf = (ctypes.c_uint8 * len(g)).from_buffer_copy(g)
+    offs = (ctypes.c_uint64 * 1)(0)
+    lens = (ctypes.c_uint32 * 1)(len(g))
+    assert lib.ouro_byron_pack_cbor(buf, len(g), offs, lens, 1, -1, small, 64,
+                                    ctypes.byref(out), st, 0) == _native.OURO_EINVAL
+    need = lib.ouro_byron_pack_bytes(1, lens)
+    assert need >= len(g) + B.MSG_EXTRA
+    big = (ctypes.c_uint8 * need)()
+    assert lib.ouro_byron_pack_cbor(buf, len(g), offs, lens, 1, -1, big, need,
+                                    ctypes.byref(out), st, 0) == _native.OURO_OK
+    assert st[0] == B.PACK_OK
+
+
+def test_empty_batch():
+    pk = B.pack_byron_cbor([])
+    assert pk.status.size == 0 and pk.pk.shape == (0, 32)
+
+
+def test_parse_byron_header_rejects_boundary_and_shelley(kats, wires):
+    ebb = next(r for _, k, r in wires if k == "boundary")
+    with pytest.raises(B.CBORError):
+        B.parse_byron_header(ebb)
+    with pytest.raises(B.CBORError):
+        B.parse_byron_header(bytes.fromhex(kats["headers"][3]["raw"]))

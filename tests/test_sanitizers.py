@@ -60,7 +60,7 @@ def test_oracle_under_asan_ubsan():
 def test_cbor_slicer_under_asan_ubsan():
     _make(PKG, "lib/libouro_pack_asan.so")
     _run(_gcc_asan(), {"OURO_PACK_LIB": os.path.join(PKG, "lib", "libouro_pack_asan.so")},
-         ["tests/test_pack.py"])
+         ["tests/test_pack.py", "tests/test_pack_byron.py"])
 
 
 @pytest.mark.skipif(_clang_asan() is None, reason="clang ASan runtime not in the ROCm llvm")
