@@ -1,5 +1,7 @@
-"""GPU parity at BASELINE.json's full size (configs[3]: 1,048,576 headers on one
-GPU) through size-independent properties, plus a bit-exact oracle sample.
+"""GPU parity at BASELINE.json's full sizes (configs[3]: 1,048,576 headers on
+one GPU; configs[1] / configs[2]: 1M VRF proofs / Sum6KES signatures; the
+metric's Ed25519 leg: 1M signatures) through size-independent properties,
+plus a bit-exact oracle sample.
 
 1/8 of the device-synthesised headers get one byte incremented
 (applyCorruption-style, ouroboros-consensus-test/src/Test/Util/Corruption.hs)
@@ -161,3 +163,114 @@ def test_full_size_kes_batch_with_corruptions():
     for i in rng.choice(n, 1024, replace=False):
         want = O.kes_verify(vk[i].tobytes(), int(kt[i]), body[i].tobytes(), sig[i].tobytes())
         assert bool(got[i]) == want, i
+
+
+def test_full_size_vrf_batch_with_corruptions():
+    """configs[1] at its full size: 1,048,576 VRF proofs (the headers' eta
+    proofs under their VRF keys and alphas) through the standalone kernel, 1/8
+    of them with one byte of the proof, the key or alpha incremented (each then
+    fails).  Valid rows' outputs equal the header kernel's eta outputs of the
+    uncorrupted batch, failed rows' are zero, and a random sample of 1,024 is
+    compared with the CPU oracle (verdict and 64-byte output)."""
+    import ctypes
+
+    import torch
+
+    sys.path.insert(0, ROOT)
+    import bench
+    from ouroboros_network_amd import _native
+
+    dev = torch.device("cuda:0")
+    n = 1 << 20
+    t, _ = bench.synth_headers(n, 1024, dev)
+    v = _native.load()
+    st = torch.cuda.current_stream()
+    S = ctypes.c_void_p(st.cuda_stream)
+    hdr = bench.DeviceHeaders(t, n, dev)
+    hdr.launch(st)
+    torch.cuda.synchronize()
+    hv, be = hdr.verdict.clone(), hdr.beta_eta.clone()
+    del hdr
+    g = torch.Generator().manual_seed(20261018)
+    pick = torch.randint(0, 8, (n,), generator=g) == 0
+    which = torch.randint(0, 3, (n,), generator=g)
+    expect = torch.ones(n, dtype=torch.uint8)
+    for k, (name, w) in enumerate((("eta_proof", 80), ("vrf_vk", 32), ("eta_alpha", 32))):
+        rows = torch.nonzero(pick & (which == k)).squeeze(1)
+        cols = torch.randint(0, w, (rows.numel(),), generator=g)
+        t[name].view(n, w)[rows.to(dev), cols.to(dev)] += 1
+        expect[rows] = 0
+    a_off = torch.arange(n, dtype=torch.int64, device=dev) * 32
+    a_len = torch.full((n,), 32, dtype=torch.int32, device=dev)
+    beta = torch.full((n * 64,), 0xAA, dtype=torch.uint8, device=dev)
+    ver = torch.zeros(n, dtype=torch.uint8, device=dev)
+    rc = v.ouro_vrf03_verify_batch_device(S, n, t["vrf_vk"].data_ptr(), t["eta_proof"].data_ptr(),
+                                          t["eta_alpha"].data_ptr(), a_off.data_ptr(),
+                                          a_len.data_ptr(), beta.data_ptr(), ver.data_ptr())
+    _native.check(rc, "vrf batch")
+    torch.cuda.synchronize()
+    assert (hv.cpu() == 15).all()
+    got = ver.cpu()
+    assert torch.equal(got, expect), int((got != expect).sum())
+    b = beta.view(n, 64).cpu()
+    ok = expect.bool()
+    assert torch.equal(b[ok], be.view(n, 64).cpu()[ok])
+    assert not b[~ok].any()
+    rng = np.random.default_rng(7)
+    vk = t["vrf_vk"].cpu().numpy().reshape(n, 32)
+    pf = t["eta_proof"].cpu().numpy().reshape(n, 80)
+    al = t["eta_alpha"].cpu().numpy().reshape(n, 32)
+    bn = b.numpy()
+    for i in rng.choice(n, 1024, replace=False):
+        want = O.vrf_verify(vk[i].tobytes(), pf[i].tobytes(), al[i].tobytes())
+        assert bool(got[i]) == (want is not None), i
+        assert bn[i].tobytes() == (want or bytes(64)), i
+
+
+def test_full_size_ed25519_batch_with_corruptions():
+    """BASELINE's "Ed25519 ver/s" at the bench's size: 1,048,576 device-
+    synthesised signatures over 32-byte messages, 1/8 with one byte of the key,
+    the signature or the message incremented (each then fails libsodium's
+    rules), the verdicts known in advance, and a random sample of 1,024
+    compared with the CPU oracle."""
+    import ctypes
+
+    import torch
+
+    sys.path.insert(0, ROOT)
+    import bench
+    from ouroboros_network_amd import _native
+
+    dev = torch.device("cuda:0")
+    n = 1 << 20
+    syn = ctypes.CDLL(bench.SYNTH_SO)
+    syn.ouro_synth_ed25519.argtypes = [ctypes.c_size_t, ctypes.c_uint64] + [ctypes.c_void_p] * 3
+    u8 = dict(dtype=torch.uint8, device=dev)
+    pk, sig, msg = torch.empty(n * 32, **u8), torch.empty(n * 64, **u8), torch.empty(n * 32, **u8)
+    assert syn.ouro_synth_ed25519(n, 77, pk.data_ptr(), sig.data_ptr(), msg.data_ptr()) == 0
+    g = torch.Generator().manual_seed(20261019)
+    pick = torch.randint(0, 8, (n,), generator=g) == 0
+    which = torch.randint(0, 3, (n,), generator=g)
+    expect = torch.ones(n, dtype=torch.uint8)
+    for k, (x, w) in enumerate(((pk, 32), (sig, 64), (msg, 32))):
+        rows = torch.nonzero(pick & (which == k)).squeeze(1)
+        cols = torch.randint(0, w, (rows.numel(),), generator=g)
+        x.view(n, w)[rows.to(dev), cols.to(dev)] += 1
+        expect[rows] = 0
+    off = torch.arange(n, dtype=torch.int64, device=dev) * 32
+    ln = torch.full((n,), 32, dtype=torch.int32, device=dev)
+    ver = torch.full((n,), 7, **u8)
+    st = torch.cuda.current_stream()
+    rc = _native.load().ouro_ed25519_verify_batch_device(
+        ctypes.c_void_p(st.cuda_stream), n, pk.data_ptr(), sig.data_ptr(), msg.data_ptr(),
+        off.data_ptr(), ln.data_ptr(), ver.data_ptr())
+    _native.check(rc, "ed25519 batch")
+    torch.cuda.synchronize()
+    got = ver.cpu()
+    assert torch.equal(got, expect), int((got != expect).sum())
+    rng = np.random.default_rng(8)
+    P = pk.cpu().numpy().reshape(n, 32)
+    G = sig.cpu().numpy().reshape(n, 64)
+    M = msg.cpu().numpy().reshape(n, 32)
+    for i in rng.choice(n, 1024, replace=False):
+        assert bool(got[i]) == O.ed25519_verify(G[i].tobytes(), M[i].tobytes(), P[i].tobytes()), i
