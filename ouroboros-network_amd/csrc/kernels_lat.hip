@@ -26,6 +26,12 @@
 #ifndef OURO_V_WHOLE
 #define OURO_V_WHOLE 0
 #endif
+// waves per SIMD the cores kernel is compiled for: a window's 640 waves never
+// put two on one SIMD, so 1 gives each wave the whole register file (AGPRs
+// instead of scratch for the wide items' spills); 2 = the round-2 form
+#ifndef OURO_LAT_WAVES
+#define OURO_LAT_WAVES 2
+#endif
 
 using namespace ouro;
 
@@ -254,7 +260,7 @@ __device__ __forceinline__ int nth_clear_bit(uint32_t m, int k) { return nth_set
 // core number c of header i, so each wave runs one core type).  n (d_n[0])
 // and the batch's optional members (d_n[1], tpraos.h kOpt*) are read from
 // device memory so a captured graph serves any batch of n <= capacity.
-__global__ void __launch_bounds__(kBlock, OURO_WAVES) k_tpraos_cores(ouro_tpraos_batch b,
+__global__ void __launch_bounds__(kBlock, OURO_LAT_WAVES) k_tpraos_cores(ouro_tpraos_batch b,
                                                             const uint32_t* __restrict__ d_n,
                                                             int32_t* res_buf, int32_t* scratch,
                                                             const int32_t* __restrict__ btab,

@@ -215,6 +215,117 @@ OURO_FI void sha512_prefixed(uint64_t out[8], const uint32_t* prefix, const Tail
   for (int i = 0; i < 8; i++) out[i] = H[i];
 }
 
+#if defined(__HIP_DEVICE_COMPILE__)
+// ---- wave-cooperative SHA-512 (latency mode: one message per wave) ----------
+// A latency-mode work item runs on a whole wave with every lane holding the
+// same values, so a hash is one dependent chain issued by 64 lanes alike.  The
+// message schedule does not depend on the chaining state: lane b builds block
+// b's sixteen words and extends its schedule while the other lanes do the
+// same for theirs, all blocks at once, and stores K[t] + W[t] of every round
+// in LDS; the compression then runs the 80 rounds of each block with one LDS
+// broadcast read per round and no schedule.  A 5-block Sum6KES leaf message
+// (R || A || 544-B body) thus pays one schedule's latency instead of five.
+// kGroup = 32 hashes two messages per wave (one per half; same length).
+constexpr int kShaWaveMaxBlocks = 8;  // per wave (all groups together)
+constexpr int kShaWaveMaxWaves = 4;   // waves per workgroup (latency blocks <= 256 threads)
+__device__ __forceinline__ uint64_t* sha_wave_lds() {
+  __shared__ uint64_t s_kw[kShaWaveMaxWaves * kShaWaveMaxBlocks * 80];
+  return s_kw + (threadIdx.x >> 6) * (kShaWaveMaxBlocks * 80);
+}
+// blocks a group of kGroup lanes can hash (the caller falls back above it)
+template <int kGroup>
+constexpr uint32_t sha_wave_max_blocks() { return kShaWaveMaxBlocks * kGroup / 64; }
+
+// word w (compile-time) of static block b (compile-time: a block the prefix
+// reaches), padded, with the length words of an nb-block message
+template <int PL, class Tail>
+OURO_FI uint64_t sha_static_word(int b, int w, const uint32_t* prefix, const Tail& tail,
+                                 uint32_t tl, uint32_t total, uint32_t nb) {
+  const uint32_t p0 = (uint32_t)(b * 128 + w * 8);
+  uint64_t r = 0;
+  if (p0 >= (uint32_t)PL) {
+    r = sha_pad_word(sha_tail_word(tail, p0 - PL, tl), p0, total);
+  } else {
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      const uint32_t p = p0 + k;
+      uint32_t byte;
+      if (p < (uint32_t)PL) byte = byte_of(prefix, (int)p);
+      else byte = (p < total) ? tail.tail(p - PL) : (p == total ? 0x80u : 0u);
+      r = (r << 8) | byte;
+    }
+  }
+  const uint32_t widx = (uint32_t)(b * 16 + w);
+  if (widx == nb * 16 - 1) r = (uint64_t)total << 3;
+  else if (widx == nb * 16 - 2) r = 0;
+  return r;
+}
+
+template <int PL, int kGroup, class Tail>
+__device__ __forceinline__ void sha512_prefixed_wave(uint64_t out[8], const uint32_t* prefix,
+                                                     const Tail& tail, uint32_t tl) {
+  static_assert(kGroup == 64 || kGroup == 32, "one or two messages per wave");
+  constexpr uint32_t kMaxB = sha_wave_max_blocks<kGroup>();
+  constexpr int kStatic = (PL + 127) / 128 > 0 ? (PL + 127) / 128 : 1;
+  const uint32_t total = PL + tl;
+  const uint32_t nb = (total + 17 + 127) >> 7;  // <= kMaxB (callers check)
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t gb = lane & (uint32_t)(kGroup - 1);  // the block this lane schedules
+  uint64_t* kw = sha_wave_lds() + (lane / (uint32_t)kGroup) * kMaxB * 80;
+  if (gb < nb) {
+    uint64_t W[16];
+#pragma unroll
+    for (int w = 0; w < 16; w++) {
+      uint64_t r = 0;
+#pragma unroll
+      for (int sb = 0; sb < kStatic; sb++)
+        if (gb == (uint32_t)sb) r = sha_static_word<PL>(sb, w, prefix, tail, tl, total, nb);
+      if (gb >= (uint32_t)kStatic) {
+        const uint32_t p0 = gb * 128 + (uint32_t)w * 8;
+        r = sha_pad_word(sha_tail_word(tail, p0 - PL, tl), p0, total);
+        const uint32_t widx = gb * 16 + (uint32_t)w;
+        if (widx == nb * 16 - 1) r = (uint64_t)total << 3;
+        else if (widx == nb * 16 - 2) r = 0;
+      }
+      W[w] = r;
+    }
+    uint64_t* k = kw + gb * 80;
+#pragma unroll
+    for (int i = 0; i < 16; i++) k[i] = W[i] + kSha512K[i];
+#pragma unroll 1
+    for (int r0 = 16; r0 < 80; r0 += 16) {
+#pragma unroll
+      for (int i = 0; i < 16; i++) {
+        const uint64_t w15 = W[(i + 1) & 15], w2 = W[(i + 14) & 15];
+        const uint64_t s0 = rotr64(w15, 1) ^ rotr64(w15, 8) ^ shr64(w15, 7);
+        const uint64_t s1 = rotr64(w2, 19) ^ rotr64(w2, 61) ^ shr64(w2, 6);
+        W[i] += s0 + W[(i + 9) & 15] + s1;
+        k[r0 + i] = W[i] + kSha512K[r0 + i];
+      }
+    }
+  }
+  // LDS writes of this wave before its reads (one wave: a fence suffices)
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  uint64_t H[8];
+  sha512_init(H);
+#pragma unroll 1
+  for (uint32_t b = 0; b < nb; b++) {
+    const uint64_t* k = kw + b * 80;
+    uint64_t a = H[0], bb = H[1], c = H[2], d = H[3], e = H[4], f = H[5], g = H[6], h = H[7];
+#pragma unroll 1
+    for (int t0 = 0; t0 < 80; t0 += 16) {
+#pragma unroll
+      for (int i = 0; i < 16; i++) sha512_round(a, bb, c, d, e, f, g, h, 0, k[t0 + i]);
+    }
+    H[0] += a; H[1] += bb; H[2] += c; H[3] += d; H[4] += e; H[5] += f; H[6] += g; H[7] += h;
+  }
+#pragma unroll
+  for (int i = 0; i < 8; i++) out[i] = H[i];
+}
+#endif
+
 // big-endian digest word i -> little-endian packed byte words
 OURO_FI void sha512_digest_words(uint32_t out[16], const uint64_t H[8]) {
 #pragma unroll

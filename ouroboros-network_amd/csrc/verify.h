@@ -482,6 +482,8 @@ OURO_FI int wave_max_small(int x) {
 // identity projectively.
 // The scalar side of the half-size equation: h = SHA-512(R || A || M) mod L,
 // its lattice pair (c0, c1) and b = c1 S mod L.
+OURO_HD inline void ed25519_scalars_from_digest(HalfScalars& hs, uint32_t b[8], const uint64_t H[8],
+                                                const uint32_t S[8]);
 template <class Tail>
 OURO_HD inline void ed25519_scalars(HalfScalars& hs, uint32_t b[8], const uint32_t R[8],
                                     const uint32_t S[8], const uint32_t pk[8], const Tail& msg,
@@ -494,6 +496,12 @@ OURO_HD inline void ed25519_scalars(HalfScalars& hs, uint32_t b[8], const uint32
   }
   uint64_t H[8];
   sha512_prefixed<64>(H, pre, msg, mlen);
+  ed25519_scalars_from_digest(hs, b, H, S);
+}
+// the rest of ed25519_scalars from the digest H of R || A || M (the latency
+// mode hashes on the whole wave, wide_cores.h)
+OURO_HD inline void ed25519_scalars_from_digest(HalfScalars& hs, uint32_t b[8], const uint64_t H[8],
+                                                const uint32_t S[8]) {
   uint32_t hw[16], h[8];
   sha512_digest_words(hw, H);
   sc_reduce512(h, hw);

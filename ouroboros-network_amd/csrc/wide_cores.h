@@ -485,6 +485,53 @@ __device__ __forceinline__ void ed_points_item(Slot e, const uint32_t sig[16],
     stg1(e.word(124), ok ? 1 : 0);
   }
 }
+// verify.h ed25519_scalars with SHA-512(R || A || M) on the whole wave
+// (sha512.h sha512_prefixed_wave; messages beyond its block capacity hash on
+// the lane).  A/B switch OURO_SHA_WAVE=0: the lane hash.
+#ifndef OURO_SHA_WAVE
+#define OURO_SHA_WAVE 1
+#endif
+template <class Tail>
+__device__ __forceinline__ void ed25519_scalars_wave(HalfScalars& hs, uint32_t b[8],
+                                                     const uint32_t R[8], const uint32_t S[8],
+                                                     const uint32_t pk[8], const Tail& msg,
+                                                     uint32_t mlen) {
+  uint32_t pre[16];
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    pre[i] = R[i];
+    pre[8 + i] = pk[i];
+  }
+  uint64_t H[8];
+  if (OURO_SHA_WAVE && ((64 + mlen + 17 + 127) >> 7) <= sha_wave_max_blocks<64>())
+    sha512_prefixed_wave<64, 64>(H, pre, msg, mlen);
+  else
+    sha512_prefixed<64>(H, pre, msg, mlen);
+  ed25519_scalars_from_digest(hs, b, H, S);
+}
+
+// tpraos.h vrf_challenge_ok for the two VRFs of a header at once, one per
+// half-wave (sha512_prefixed_wave, two messages per wave)
+__device__ __forceinline__ bool vrf_challenge_ok_wave(const uint32_t Henc[8], const uint32_t Genc[8],
+                                                      const uint32_t Uenc[8], const uint32_t Venc[8],
+                                                      const uint32_t c[4]) {
+  if (!OURO_SHA_WAVE) return vrf_challenge_ok(Henc, Genc, Uenc, Venc, c);
+  uint32_t hp[33];
+  hp[0] = 0x04u | (0x02u << 8);
+  pack_shifted(hp, 1, Henc);
+  pack_shifted(hp, 9, Genc);
+  pack_shifted(hp, 17, Uenc);
+  pack_shifted(hp, 25, Venc);
+  uint64_t Hc[8];
+  sha512_prefixed_wave<130, 32>(Hc, hp, ShaNoTail{}, 0);
+  uint32_t cw[16];
+  sha512_digest_words(cw, Hc);
+  bool ceq = true;
+#pragma unroll
+  for (int i = 0; i < 4; i++) ceq = ceq && cw[i] == c[i];
+  return ceq;
+}
+
 template <class Tail>
 __device__ __forceinline__ void ed_scalars_item(Slot e, const uint32_t sig[16], const uint32_t pk[8],
                                                 const Tail& msg, uint32_t mlen) {
@@ -525,7 +572,7 @@ __device__ __forceinline__ void ed_scalars_item(Slot e, const uint32_t sig[16], 
     sc_reduce512(b, prod);
   }
 #else
-  ed25519_scalars(hs, b, R, S, pk, msg, mlen);
+  ed25519_scalars_wave(hs, b, R, S, pk, msg, mlen);
 #endif
   int nw = (hs.bits + 4) >> 2;
   nw = nw < 1 ? 1 : (nw > 64 ? 64 : nw);
@@ -602,7 +649,7 @@ __device__ __forceinline__ void hdr_tail_wide(const ouro_tpraos_batch& b, size_t
   if (fg & kFlagGammaX0) Genc[7] &= 0x7fffffffu;
 #pragma unroll
   for (int k = 0; k < 4; k++) c[k] = pi[8 + k];
-  const bool ceq = vrf_challenge_ok(Henc, Genc, Uenc, Venc, c);
+  const bool ceq = vrf_challenge_ok_wave(Henc, Genc, Uenc, Venc, c);
   const bool ok = (fu & fv & fg & kFlagOk) && ceq;
   ld_words8(beta, res + kLatBeta + 16 * which);
   ld_words8(beta + 8, res + kLatBeta + 16 * which + 8);

@@ -115,3 +115,45 @@ def seeded(kats, epoch_nonce, copies=4, rng=None):
     lo[4, 5] ^= 1         # a forged claimed leader output on a valid proof
     eo[5, 63] ^= 0x80     # a forged claimed eta output on a valid proof
     return batch.with_(eta_proof=ep, leader_proof=lp, eta_output=eo, leader_output=lo, slot=sl)
+
+
+# SHA-512 block boundaries of the KES leaf message R || A || body (64 + len
+# bytes): lengths around every nb-block limit (64 + len + 17 = 128 nb), up to
+# past the latency mode's wave-hash capacity (8 blocks: len <= 943), and 0.
+KES_BODY_LENGTHS = [0, 1, 7, 8, 46, 47, 48, 49, 111, 112, 175, 176, 303, 431, 544, 559, 560,
+                    687, 815, 942, 943, 944, 1000, 1200]
+
+
+def kes_body_lengths(kats, lengths=KES_BODY_LENGTHS, seed=b"\x07" * 32):
+    """The first golden header re-signed for bodies of the given lengths: a
+    fresh Sum6KES key (hot vk), its OCERT signed by the golden cold key (the
+    seed 32 x 0x01 key), the body random bytes, the KES
+    signature over it at the header's period.  Each length twice: valid, and
+    with one body byte (or, for the empty body, one leaf-signature byte)
+    changed after signing, so that KES alone fails."""
+    import dataclasses
+
+    h0 = H.parse_header(bytes.fromhex(kats["headers"][0]["raw"]))
+    cold_pk, cold_sk = O.ed25519_keypair(GOLDEN_VRF_SEED)
+    assert cold_pk == h0.issuer_vk
+    hot = O.kes_keygen(seed)
+    t = H.kes_t(h0.slot, 100, h0.ocert_kes_period)
+    ocert_msg = hot + h0.ocert_counter.to_bytes(8, "big") + h0.ocert_kes_period.to_bytes(8, "big")
+    sigma = O.ed25519_sign(cold_sk, ocert_msg)
+    rng = np.random.default_rng(2024)
+    rows = []
+    for n in lengths:
+        body = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+        sig = O.kes_sign(seed, t, body)
+        rows.append(dataclasses.replace(h0, hot_vk=hot, ocert_sigma=sigma, body=body, kes_sig=sig))
+        if n:
+            bad = bytearray(body)
+            bad[(n * 7) // 11] ^= 0x10
+            rows.append(dataclasses.replace(rows[-1], body=bytes(bad)))
+        else:  # nothing to change in an empty body: the leaf signature's R
+            bad = bytearray(sig)
+            bad[5] ^= 0x10
+            rows.append(dataclasses.replace(rows[-1], kes_sig=bytes(bad)))
+    ea = [bytes.fromhex(kats["headers"][0]["eta_alpha"])] * len(rows)
+    la = [bytes.fromhex(kats["headers"][0]["leader_alpha"])] * len(rows)
+    return H.pack(rows, ea, la, slots_per_kes_period=100)

@@ -293,6 +293,26 @@ def test_lowlat_equals_throughput_and_oracle(gpu_lib, kats, monkeypatch, form):
         np.testing.assert_array_equal(bl, wbl[lo:hi])
 
 
+@pytest.mark.parametrize("form", ["wide_fused", "wide_finish_launch"])
+def test_lowlat_kes_body_lengths(gpu_lib, kats, monkeypatch, form):
+    """KES leaf messages around every SHA-512 block boundary, up to past the
+    latency mode's wave-hash capacity (8 blocks; longer bodies hash on the
+    lane): latency and throughput verdicts equal the oracle's, and every
+    re-signed row verifies while its one-byte-changed twin fails KES only."""
+    from ouroboros_network_amd.tpraos import verify_headers, verify_headers_lowlat
+
+    for k, v in LAT_FORMS[form].items():
+        monkeypatch.setenv(k, v)
+    batch = HC.kes_body_lengths(kats)
+    wv, wbe, wbl = O.tpraos_verify_batch(batch)
+    assert (wv[0::2] == 0x3F).all() and (wv[1::2] == 0x3D).all()
+    for fn in (verify_headers, verify_headers_lowlat):
+        v, be, bl = fn(batch)
+        np.testing.assert_array_equal(v, wv)
+        np.testing.assert_array_equal(be, wbe)
+        np.testing.assert_array_equal(bl, wbl)
+
+
 def test_pipelined_host_batches(gpu_lib, kats, monkeypatch):
     """Host-buffer header batches larger than one chunk go through the
     two-stream pipeline (kernels.hip hdr_batch_pipelined): same verdicts and
