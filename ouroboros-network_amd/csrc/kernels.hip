@@ -152,6 +152,7 @@ __global__ void k_tpraos_cores(ouro_tpraos_batch b, const uint32_t* __restrict__
                                const int32_t* __restrict__ btab, int mode, int wide_waves,
                                uint8_t* __restrict__ verdict, uint8_t* __restrict__ beta_eta,
                                uint8_t* __restrict__ beta_leader);
+int lat_fused_items_host();  // kernels_lat.hip: waves per header of the fused launch
 __global__ void k_ed25519_wide(size_t n, const uint8_t* __restrict__ pk,
                                const uint8_t* __restrict__ sig, const uint8_t* __restrict__ msg,
                                const uint64_t* __restrict__ msg_off,
@@ -617,9 +618,9 @@ int launch_lowlat(hipStream_t st, const ouro_tpraos_batch& b, const uint32_t* d_
   const int nwide = __builtin_popcount((unsigned)wmask);
   // fused (all eight cores wide): the last core of a header finishes it, no
   // second launch (OURO_LAT_FUSE=0 keeps the finish launch, for A/B); its
-  // two Ed25519 checks take two waves each (kernels_lat.hip kFusedItems)
+  // items per header: kernels_lat.hip kFusedItems
   const bool fused = wmask == 0xff && lat_fuse();
-  const size_t wide_waves = (size_t)(fused ? kLatCores + 2 : nwide) * n_cap;
+  const size_t wide_waves = (size_t)(fused ? lat_fused_items_host() : nwide) * n_cap;
   const size_t wide_blocks = (wide_waves * 64 + blk - 1) / blk;
   const size_t quad_items = (size_t)(kLatCores - nwide) * n_cap;
   const int g1 = (int)wide_blocks + grid(quad_items << (quad ? 2 : 0), kCores);
@@ -1518,10 +1519,13 @@ int ouro_tpraos_plan_debug_poison(ouro_tpraos_plan* p) {
   for (size_t i = 0; i < p->cap; i++) {
     const Slot r = slot_of(h.data(), i, kLatResWords);
     *r.word(kLatCtr) = tag | (kLatCores - 1);     // the header's tail one arrival away
-    *r.word(kLatCtr + 1) = tag | 1;                // each V / Gamma pair, one of two in
-    *r.word(kLatCtr + 2) = tag | 1;
-    *r.word(kLatEd + 125) = tag | 1;               // each Ed25519 points / scalars pair
-    *r.word(kLatEd + kEdWords + 125) = tag | 1;
+    *r.word(kLatCtr + 1) = tag | 1;                // each V / Gamma pair (or V / V2 /
+    *r.word(kLatCtr + 2) = tag | 1;                // Gamma triple), one in
+    for (int e = 0; e < 2; e++) {
+      *r.word(kLatEd + kEdWords * e + 125) = tag | 1;  // each Ed25519 points / scalars pair
+      for (int k = 17; k <= 19; k++)                // split form: the chain and done counters
+        *r.word(kLatEd + kEdWords * e + k) = tag | 1;
+    }
   }
   OURO_HIP(hipMemcpy(p->res, h.data(), sizeof(int32_t) * words, hipMemcpyHostToDevice));
   return OURO_OK;

@@ -26,6 +26,11 @@
 #ifndef OURO_V_WHOLE
 #define OURO_V_WHOLE 0
 #endif
+// A/B switch: 1 = the fused launch's split form (hdr_item_fused: three waves
+// per Ed25519 check, V over V / V2 / Gamma), 0 = the two-wave form
+#ifndef OURO_LAT_SPLIT
+#define OURO_LAT_SPLIT 1
+#endif
 // waves per SIMD the cores kernel is compiled for: a window's 640 waves never
 // put two on one SIMD, so 1 gives each wave the whole register file (AGPRs
 // instead of scratch for the wide items' spills); 2 = the round-2 form
@@ -71,6 +76,14 @@ __device__ __noinline__ void hdr_core_wide(const ouro_tpraos_batch& b, size_t i,
       uint32_t p[8], pi[20];
       ld_words(p, b.vrf_vk + 32 * i, 2);
       ld_words(pi, (leader ? b.leader_proof : b.eta_proof) + 80 * i, 5);
+      if (fused && OURO_LAT_SPLIT) {  // the encoding on the wave (wide_cores.h encode1_wide)
+        pw Uw;
+        flag = vrf_u_wide_pw(Uw, p, pi, bw) ? kFlagOk : 0;
+        uint32_t enc[8];
+        encode1_wide(enc, Uw);
+        if (lead) st_words8(res + kLatEnc + 8 * (3 * (int)leader + 1), enc);
+        break;
+      }
       ge_p2 U;
       flag = vrf_u_wide(U, p, pi, bw) ? kFlagOk : 0;
       if (fused) {
@@ -99,6 +112,11 @@ __device__ __noinline__ void hdr_core_wide(const ouro_tpraos_batch& b, size_t i,
         flag = kFlagOk;
         break;
       }
+      if (fused && OURO_LAT_SPLIT) {  // [s windows 0..31]H; V2 and Gamma do the rest
+        vrf_sh_split(res + kLatVsplit + 4 * kPwWords * (int)leader, p, pi, alpha, false);
+        flag = kFlagOk;
+        break;
+      }
       // (fused, split V: H and [s]H to the record; vrf_combine_encode adds
       // the Gamma core's -[c]Gamma)
       ge_p3 H;
@@ -117,11 +135,12 @@ __device__ __noinline__ void hdr_core_wide(const ouro_tpraos_batch& b, size_t i,
       if (fused) {
         uint32_t beta[16];
         ge_p2 part;
-        flag = vrf_gamma_beta_wide(beta, part, pi);
+        const Slot vs = res + kLatVsplit + 4 * kPwWords * (int)leader + 3 * kPwWords;
+        flag = vrf_gamma_beta_wide(beta, part, pi, OURO_LAT_SPLIT ? &vs : nullptr);
         if (lead) {
           st_words8(res + kLatBeta + 16 * (int)leader, beta);
           st_words8(res + kLatBeta + 16 * (int)leader + 8, beta + 8);
-          if (!OURO_V_WHOLE)
+          if (!OURO_V_WHOLE && !OURO_LAT_SPLIT)
             st_point_at(res + kLatPart + (leader ? kPtWords : 0), part.X, part.Y, part.Z);
         }
         if (!leader && (opts & kOptEtaNonce)) eta_nonce_candidates(b, i, opts, res, beta);
@@ -141,12 +160,22 @@ __device__ __noinline__ void hdr_core_wide(const ouro_tpraos_batch& b, size_t i,
 #endif
 }
 
-// Fused mode: ten items per header -- the eight cores, with the OCERT and
-// KES Ed25519 checks each split into a points item (0 / 1) and a scalars
-// item (8 / 9) whose second to arrive runs the chain (wide_cores.h ed_*).
-// Every finished core arrives at the header's counter; the eighth runs the
-// finish (hdr_tail_wide).  skip: the timing probe's mask (cores 0..7).
-constexpr int kFusedItems = kLatCores + 2;
+// Fused mode, two-wave form (OURO_LAT_SPLIT=0): ten items per header -- the
+// eight cores, with the OCERT and KES Ed25519 checks each split into a points
+// item (0 / 1) and a scalars item (8 / 9) whose second to arrive runs the
+// chain (wide_cores.h ed_*).  Every finished core arrives at the header's
+// counter; the eighth runs the finish (hdr_tail_wide).
+// Split form (OURO_LAT_SPLIT=1, the default): fourteen items -- each Ed25519
+// check over three waves with no lattice pair (points 0 / 1, scalars 8 / 9,
+// doubling 10 / 11: wide_cores.h eds_*), each V over the V core (4 / 5, low
+// windows of s), a V2 item (12 / 13: H again, 2^128 H, high windows) and the
+// Gamma core (6 / 7); the last of a check's chains or of a VRF's three parts
+// finishes that check, and eight arrivals (two Ed25519 checks, two U, two VRF
+// combinations, two Gamma betas) complete a header.  skip: the timing probe's mask (cores
+// 0..7; the doubling and V2 items follow their cores).
+static_assert(!(OURO_V_WHOLE && OURO_LAT_SPLIT), "OURO_V_WHOLE needs the two-wave form");
+constexpr int kFusedItems = OURO_LAT_SPLIT ? kLatCores + 6 : kLatCores + 2;
+[[maybe_unused]] constexpr uint32_t kHdrParties = OURO_LAT_SPLIT ? 8u : (uint32_t)kLatCores;
 // stamps (a timing probe, tools/lat_stamps.py: a build with
 // -DOURO_LAT_STAMPS=1, run with OURO_LAT_STAMPS set): header 0's items print
 // their start / end times (s_memrealtime, 100 MHz) and the tail's end.  The
@@ -173,7 +202,64 @@ __device__ __noinline__ void hdr_item_fused(const ouro_tpraos_batch& b, size_t i
     (void)t0;
 #endif
   };
-  if (item == kCoreOcert || item == kCoreKes || item >= kLatCores) {
+  const bool ed_item = item == kCoreOcert || item == kCoreKes ||
+                       (item >= kLatCores && item < kLatCores + (OURO_LAT_SPLIT ? 4 : 2));
+  if (ed_item && OURO_LAT_SPLIT) {
+    // e: 0 OCERT, 1 KES; role: 0 points, 1 scalars, 2 doubling
+    const int e = item < kLatCores ? item : (item - kLatCores) & 1;
+    const int role = item < kLatCores ? 0 : (item < kLatCores + 2 ? 1 : 2);
+    const Slot ed = res + kLatEd + kEdWords * e;
+    const bool skipped = (skip >> e) & 1u;
+    bool run_x = false, run_y = false;
+    if (!skipped) {
+      uint32_t sig[16], pk[8];
+      bool walk_ok = true;
+      if (e == 0) {
+        ld_words(sig, b.ocert_sigma + 64 * i, 4);
+        ld_words(pk, b.issuer_vk + 32 * i, 2);
+      } else {
+        uint32_t hv[8];
+        ld_words(hv, b.hot_vk + 32 * i, 2);
+        const uint32_t* sw = reinterpret_cast<const uint32_t*>(b.kes_sig + 448 * i);
+        walk_ok = sum6kes_walk_wide(pk, sig, hv, b.kes_t[i], sw);
+      }
+      if (role == 0) {
+        eds_points(ed, sig, pk, walk_ok);
+      } else if (role == 2) {
+        eds_double(ed, pk);
+      } else if (e == 0) {
+        uint32_t hv[8];
+        ld_words(hv, b.hot_vk + 32 * i, 2);
+        OcertMsg m;
+        ocert_msg(m, hv, b.ocert_counter[i], b.ocert_kes_period[i]);
+        eds_scalars(ed, sig, pk, m, 48);
+      } else {
+        eds_scalars(ed, sig, pk, ShaGlobalTail{b.body + b.body_off[i]}, b.body_len[i]);
+      }
+    }
+    stamp("work");
+    // the scalars item is a party of both chains: it arrives at both before
+    // running either (X first: its other party, the points item, is earlier)
+    if (role != 0) run_y = arrive_last(ed.word(kEsCy), gen, 2);
+    if (role != 2) run_x = arrive_last(ed.word(kEsCx), gen, 2);
+    bool done = false;
+    if (run_x) {
+      if (!skipped) eds_chain(ed, bw, false);
+      stamp("chx");
+      done = arrive_last(ed.word(kEsCd), gen, 2) || done;
+    }
+    if (run_y) {
+      if (!skipped) eds_chain(ed, bw, true);
+      stamp("chy");
+      done = arrive_last(ed.word(kEsCd), gen, 2) || done;
+    }
+    if (!done) {
+      stamp("half");
+      return;
+    }
+    const int32_t flag = (!skipped && eds_combine(ed)) ? kFlagOk : 0;
+    if (lead) stg1(res.word(kResFlags + e), flag);
+  } else if (ed_item) {
     const int e = item >= kLatCores ? item - kLatCores : item;  // 0 OCERT, 1 KES
     const bool scal = item >= kLatCores;
     const Slot ed = res + kLatEd + kEdWords * e;
@@ -213,25 +299,88 @@ __device__ __noinline__ void hdr_item_fused(const ouro_tpraos_batch& b, size_t i
     kstamp(4);
     if (stamps && e == 1) kstamp_print();
     if (lead) stg1(res.word(kResFlags + e), flag);
+  } else if (OURO_LAT_SPLIT && item >= kLatCores + 4) {
+    // V2: [s windows 32..63](2^128 H), then the VRF's three-party arrival
+    const int which = item - (kLatCores + 4);
+    const bool skipped = (skip >> (kCoreVe + which)) & 1u;
+    if (!skipped) {
+      uint32_t p[8], pi[20];
+      ld_words(p, b.vrf_vk + 32 * i, 2);
+      ld_words(pi, (which ? b.leader_proof : b.eta_proof) + 80 * i, 5);
+      SeedMsg alpha;
+      hdr_seed(alpha, b, i, which != 0, opts);
+      vrf_sh_split(res + kLatVsplit + 4 * kPwWords * which, p, pi, alpha, true);
+    }
+    if (!arrive_last(res.word(kLatCtr + 1 + which), gen, 3)) {
+      stamp("half");
+      return;
+    }
+    if (!(((skip >> (kCoreVe + which)) | (skip >> (kCoreGe + which))) & 1u))
+      vrf_split_combine_encode(res, which);
+    stamp("comb");
+  } else if (OURO_LAT_SPLIT && (item == kCoreGe || item == kCoreGl)) {
+    // Gamma: -[c]Gamma first (the VRF's three-party combination waits for
+    // it), then [8]Gamma, beta and the nonce candidates (only the tail reads
+    // them: this item arrives at the header counter itself)
+    const int which = item == kCoreGl ? 1 : 0;
+    const bool skipped = (skip >> item) & 1u;
+    uint32_t pi[20];
+    pw Gw{0, 0, 0, 0};
+    int32_t flag = 0;
+    if (!skipped) {
+      ld_words(pi, (which ? b.leader_proof : b.eta_proof) + 80 * i, 5);
+      flag = vrf_gamma_part_wide(res + kLatVsplit + 4 * kPwWords * which + 3 * kPwWords, Gw, pi);
+    }
+    stamp("work");
+    if (arrive_last(res.word(kLatCtr + 1 + which), gen, 3)) {
+      if (!(((skip >> (kCoreVe + which)) | skipped) & 1u)) vrf_split_combine_encode(res, which);
+      stamp("comb");
+      // the combination's own arrival (this item arrives again for beta below)
+      if (arrive_last(res.word(kLatCtr), gen, kHdrParties))
+        hdr_tail_wide(b, i, opts, res, verdict, beta_eta, beta_leader);
+    }
+    if (!skipped) {
+      uint32_t beta[16];
+      vrf_gamma_beta_part_wide(beta, Gw);
+      if (lead) {
+        st_words8(res + kLatBeta + 16 * which, beta);
+        st_words8(res + kLatBeta + 16 * which + 8, beta + 8);
+      }
+      if (!which && (opts & kOptEtaNonce)) eta_nonce_candidates(b, i, opts, res, beta);
+    }
+    if (lead) stg1(res.word(kResFlags + item), flag);
   } else {
     if (!((skip >> item) & 1u)) hdr_core_wide(b, i, opts, item, res, bw, true);
-    // split V: the second of a VRF's V and Gamma cores combines and encodes
+    // split V: the last of a VRF's V and Gamma cores (and V2) combines and encodes
     const bool vg = item == kCoreVe || item == kCoreVl || item == kCoreGe || item == kCoreGl;
     if (!OURO_V_WHOLE && vg) {
       const int which = (item == kCoreVl || item == kCoreGl) ? 1 : 0;
-      if (arrive_last(res.word(kLatCtr + 1 + which), gen, 2) &&
-          !(((skip >> (kCoreVe + which)) | (skip >> (kCoreGe + which))) & 1u))
+      const bool last = arrive_last(res.word(kLatCtr + 1 + which), gen, OURO_LAT_SPLIT ? 3 : 2);
+      const bool skipped = ((skip >> (kCoreVe + which)) | (skip >> (kCoreGe + which))) & 1u;
+      if (OURO_LAT_SPLIT) {
+        if (!last) {
+          stamp("half");
+          return;
+        }
+        stamp("work");
+        if (!skipped) vrf_split_combine_encode(res, which);
+        stamp("comb");
+      } else if (last && !skipped) {
         vrf_combine_encode(res, which);
+      }
     }
   }
   stamp("core");
   if (stamps) vstamp_print();
-  if (arrive_last(res.word(kLatCtr), gen)) {
+  if (arrive_last(res.word(kLatCtr), gen, kHdrParties)) {
     hdr_tail_wide(b, i, opts, res, verdict, beta_eta, beta_leader);
     stamp("tail");
   }
 #endif
 }
+
+// items per header of the fused launch (the host sizes the grid with it)
+int lat_fused_items_host() { return kFusedItems; }
 
 // the k-th set bit of m (k < popcount(m))
 __device__ __forceinline__ int nth_set_bit(uint32_t m, int k) {

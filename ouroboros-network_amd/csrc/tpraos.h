@@ -39,12 +39,19 @@ constexpr int kLatCtr = kLatBeta + 32;
 // fused mode, each Ed25519 check (OCERT, KES leaf) split over two waves
 // (wide_cores.h): its scalars, decoded points and arrival counter
 constexpr int kLatEd = kLatCtr + 4;                   // Ed record e at kLatEd + kEdWords e
-constexpr int kEdWords = 128;
+// (two-wave form: words 0..125; the three-wave split form, wide_cores.h
+// ed_split_*: h 0, S 8, ok 16, counters 17..19, then five wave-wide points of
+// 64 words from word 32)
+constexpr int kEdWords = 352;
 // fused mode: the eta nonce's two candidates, Blake2b-256 of the output it
 // hashes if the eta VRF verifies (the claimed one when given) and of 64 zero
 // bytes (a failed proof), hashed by the eta Gamma core off the critical path
 constexpr int kLatNonce = kLatEd + 2 * kEdWords;
-constexpr int kLatResWords = kLatNonce + 16;          // 724 words (16-B multiple)
+// fused split form: per VRF the wave-wide points H, [s_lo]H, [s_hi]H and
+// -[c]Gamma (64 words each), combined by the last of three cores
+constexpr int kPwWords = 64;
+constexpr int kLatVsplit = kLatNonce + 16;            // VRF which at kLatVsplit + 4 kPwWords which
+constexpr int kLatResWords = kLatVsplit + 8 * kPwWords;  // 1,684 words (16-B multiple)
 enum HdrCore { kCoreOcert = 0, kCoreKes, kCoreUe, kCoreUl, kCoreVe, kCoreVl, kHdrCores,
                // latency mode splits each V = [s]H - [c]Gamma over two lanes: the V
                // cores do [s]H (252-bit chain), these do -[c]Gamma (128-bit chain)

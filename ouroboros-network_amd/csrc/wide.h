@@ -46,10 +46,14 @@ struct Lanes {
   int j;          // limb index (lane & 15)
   int32_t fac;    // 38 at limb 0 (the wrap 2^256 = 38), 1 elsewhere
   bool odd, high; // row 1 or 3; row 2 or 3
+  int32_t fac2;   // 38 at limbs 0 and 1 (a rotation by two lanes), 1 elsewhere
+  int32_t facr;   // 38 at limbs below 4 r in row r (a rotation by 4 r lanes), 1 elsewhere
 };
 __device__ __forceinline__ Lanes lanes() {
   const int j = (int)(threadIdx.x & 15u);
-  return Lanes{j, j == 0 ? 38 : 1, (threadIdx.x & 16u) != 0, (threadIdx.x & 32u) != 0};
+  const int r = (int)((threadIdx.x >> 4) & 3u);
+  return Lanes{j, j == 0 ? 38 : 1, (threadIdx.x & 16u) != 0, (threadIdx.x & 32u) != 0,
+               j < 2 ? 38 : 1, j < 4 * r ? 38 : 1};
 }
 
 __device__ __forceinline__ int32_t s24(int32_t x) { return (x << 8) >> 8; }
@@ -62,6 +66,22 @@ template <int I>
 __device__ __forceinline__ int32_t bcast(int32_t x) { return dpp<0x150 + I>(x); }  // row_newbcast:I
 
 // carry an accumulator (|acc| < 2^46) into limbs |l| < 2^16.01
+#ifndef OURO_FW_CARRY2
+#define OURO_FW_CARRY2 1  // A/B switch: 1 = two rounds (below), 0 = three rounds
+#endif
+// Two rounds: acc = a0 + a1 2^16 + a2 2^32 with a0, a1 in [0, 2^16) and
+// |a2| < 2^13.1; limb j takes a0_j + a1_(j-1) + a2_(j-2) (x 38 where the
+// rotation wrapped): below 2^16 + 38 (2^16 + 2^13.1) < 2^21.4, then one
+// shift-and-rotate round leaves it below 2^16 + 38 * 2^5.4 < 2^16.03.  Three
+// DPP reads in two dependent levels instead of three rounds in series.
+__device__ __forceinline__ int32_t fw_carry2(int64_t acc, const int32_t fac, const int32_t fac2) {
+  const uint32_t lo32 = (uint32_t)acc;
+  const int32_t a0 = (int32_t)(lo32 & 0xffffu);
+  const int32_t a1 = (int32_t)(lo32 >> 16);
+  const int32_t a2 = (int32_t)(acc >> 32);
+  const int32_t s = a0 + s24(dpp<0x121>(a1)) * s24(fac) + s24(dpp<0x122>(a2)) * s24(fac2);
+  return (s & 0xffff) + s24(ror1(s >> 16)) * s24(fac);
+}
 __device__ __forceinline__ int32_t fw_carry(int64_t acc, int32_t fac) {
   int32_t lo = (int32_t)acc & 0xffff;
   int32_t hi = (int32_t)(acc >> 16);
@@ -87,12 +107,16 @@ __device__ __forceinline__ void fw_mul_steps(int64_t& acc0, int64_t& acc1, int32
   if constexpr (I < 15) fw_mul_steps<I + 1>(acc0, acc1, G, f, fac);
 }
 
+__device__ __forceinline__ int32_t fw_carry_l(int64_t acc, const Lanes& L) {
+  return OURO_FW_CARRY2 ? fw_carry2(acc, L.fac, L.fac2) : fw_carry(acc, L.fac);
+}
+
 // f * g per row (g: the narrow operand, |g| <= 196,833 per limb)
 __device__ __forceinline__ int32_t fw_mul(int32_t f, int32_t g, const Lanes& L) {
   int64_t acc0, acc1 = 0;
   int32_t G = g;
   fw_mul_steps<0>(acc0, acc1, G, f, L.fac);
-  return fw_carry(OURO_FW_ACC2 ? acc0 + acc1 : acc0, L.fac);
+  return fw_carry_l(OURO_FW_ACC2 ? acc0 + acc1 : acc0, L);
 }
 __device__ __forceinline__ int32_t fw_sq(int32_t f, const Lanes& L) { return fw_mul(f, f, L); }
 
@@ -145,7 +169,29 @@ __device__ __forceinline__ int32_t fw_mul_rep(int32_t f, int32_t g, const Lanes&
   acc += (int64_t)bcast<2>(fr) * G;
   G = s24(ror1(G)) * s24(L.fac);
   acc += (int64_t)bcast<3>(fr) * G;
-  return fw_carry(add_rows_u64(acc), L.fac);
+  return fw_carry_l(add_rows_u64(acc), L);
+}
+
+// f^2 for a REPLICATED f: fw_mul_rep with g = f, the three row rotations
+// shared by both operands (the broadcast one is rotated left by 4 r, the
+// other right by 4 r: rows 1 and 3 swap them) and one multiply by the row's
+// wrap factors instead of three
+#ifndef OURO_FW_SQ_FAC
+#define OURO_FW_SQ_FAC 1  // A/B switch: 0 = fw_mul_rep(f, f)
+#endif
+__device__ __forceinline__ int32_t fw_sq_rep(int32_t f, const Lanes& L) {
+  if (!OURO_FW_SQ_FAC) return fw_mul_rep(f, f, L);
+  const int32_t d12 = dpp<0x12c>(f), d8 = dpp<0x128>(f), d4 = dpp<0x124>(f);  // ror 12 / 8 / 4
+  const int32_t fr = sel4(f, d12, d8, d4, L);
+  int32_t G = s24(sel4(f, d4, d8, d12, L)) * s24(L.facr);
+  int64_t acc = (int64_t)bcast<0>(fr) * G;
+  G = s24(ror1(G)) * s24(L.fac);
+  acc += (int64_t)bcast<1>(fr) * G;
+  G = s24(ror1(G)) * s24(L.fac);
+  acc += (int64_t)bcast<2>(fr) * G;
+  G = s24(ror1(G)) * s24(L.fac);
+  acc += (int64_t)bcast<3>(fr) * G;
+  return fw_carry_l(add_rows_u64(acc), L);
 }
 
 // ---- conversions -------------------------------------------------------------
@@ -205,9 +251,13 @@ __device__ __forceinline__ int32_t fw_mul_t(int32_t f, int32_t g, const Lanes& L
   return (kRep && OURO_FW_REP) ? fw_mul_rep(f, g, L) : fw_mul(f, g, L);
 }
 template <bool kRep>
+__device__ __forceinline__ int32_t fw_sq_t(int32_t f, const Lanes& L) {
+  return (kRep && OURO_FW_REP) ? fw_sq_rep(f, L) : fw_mul(f, f, L);
+}
+template <bool kRep>
 __device__ __forceinline__ int32_t fw_sqn(int32_t t, int n, const Lanes& L) {
 #pragma unroll 1
-  for (int i = 0; i < n; i++) t = fw_mul_t<kRep>(t, t, L);
+  for (int i = 0; i < n; i++) t = fw_sq_t<kRep>(t, L);
   return t;
 }
 // z^(2^252 - 3) (mode 1: the square-root helper) or z^(p - 2) (mode 0: the
@@ -217,7 +267,7 @@ template <bool kRep>
 __device__ __noinline__ int32_t fw_pow_chain(int32_t z, int mode) {
   const Lanes L = lanes();
 #define fw_mul(a, b, l) fw_mul_t<kRep>(a, b, l)
-#define fw_sq(a, l) fw_mul_t<kRep>(a, a, l)
+#define fw_sq(a, l) fw_sq_t<kRep>(a, l)
 #define fw_sqn fw_sqn<kRep>
   const int32_t z2 = fw_sq(z, L);
   int32_t t = fw_sqn(z2, 2, L);
@@ -344,7 +394,13 @@ __device__ __forceinline__ int32_t bw_operand(const uint16_t* bw, int half, int3
 // the register tables (nw1 / nw2 windows), b's 16-bit digits from the wide B
 // tables every fourth window (b split at bit 128, as verify.h dsm_body), all
 // digits wave-uniform (scalars read out of the first lane).  Result in p3 form.
-template <bool kT2, bool kB>
+// kBMask: which halves of b's digits are added -- 1 the low eight (with B), 2
+// the high eight (with 2^128 B), 3 both.  Both recode b as one number, so a
+// chain taking the low half and another taking the high half of the same b
+// sum to [b]B exactly (the carry out of digit 7 is digit 8's carry in).
+// Likewise only the windows below nw1 of a1 are added, their digits recoded
+// from the whole a1: the top one carries out what the windows above take in.
+template <bool kT2, bool kB, int kBMask = 3>
 __device__ __forceinline__ pw pw_dsm(const TabW& t1, const uint32_t a1_in[8], int nw1_in,
                                      const TabW& t2, const uint32_t a2_in[8], int nw2_in,
                                      const uint32_t b_in[8], const uint16_t* bw,
@@ -380,8 +436,10 @@ __device__ __forceinline__ pw pw_dsm(const TabW& t1, const uint32_t a1_in[8], in
       d3 = sc_digit_from<kBW>((b[k >> 1] >> (16 * (k & 1))) & 0xffffu, cb, k, 2 * kBDigitsHalf);
       d4 = sc_digit_from<kBW>((b[kh >> 1] >> (16 * (kh & 1))) & 0xffffu, cb, kh,
                               2 * kBDigitsHalf);
-      q3 = bw_operand(bw, 0, d3, L);
-      q4 = bw_operand(bw, 1, d4, L);
+      if (!(kBMask & 1)) d3 = 0;
+      if (!(kBMask & 2)) d4 = 0;
+      q3 = (kBMask & 1) ? bw_operand(bw, 0, d3, L) : 0;
+      q4 = (kBMask & 2) ? bw_operand(bw, 1, d4, L) : 0;
     }
     if (j != top - 1) {
 #pragma unroll
@@ -393,6 +451,27 @@ __device__ __forceinline__ pw pw_dsm(const TabW& t1, const uint32_t a1_in[8], in
     if (d4 != 0) acc = pw_add(acc, q4, L);
   }
   return acc;
+}
+
+// a wave-wide point in a record (kPwWords = 64 words): lanes 0..15 store their
+// limb of X, Y, Z, T (the rows hold copies); every lane loads its limb back
+__device__ __forceinline__ void st_pw(Slot p, const pw& P) {
+  const int j = (int)(threadIdx.x & 63u);
+  if (j < 16) {
+    *p.word(j) = P.X;
+    *p.word(16 + j) = P.Y;
+    *p.word(32 + j) = P.Z;
+    *p.word(48 + j) = P.T;
+  }
+}
+__device__ __forceinline__ pw ld_pw(Slot p) {
+  const int j = (int)(threadIdx.x & 15u);
+  return pw{ldg1(p.word(j)), ldg1(p.word(16 + j)), ldg1(p.word(32 + j)), ldg1(p.word(48 + j))};
+}
+
+// P + Q for two wave-wide points in p3 form (complete: a = -1, d non-square)
+__device__ __forceinline__ pw pw_add_p3(const pw& P, const pw& Q, int32_t d2, const Lanes& L) {
+  return pw_add(P, pw_cached(Q, d2, L).pos, L);
 }
 
 // [s]P for a 253-bit s (signed width-4 windows), result in p3 form

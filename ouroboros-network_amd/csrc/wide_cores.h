@@ -170,8 +170,8 @@ __device__ __forceinline__ bool sum6kes_verify_wide(const uint32_t vk[8], uint32
 }
 
 // tpraos.h vrf_u_core: U = [s]B - [c]Y (Y decoded and checked here)
-__device__ __forceinline__ bool vrf_u_wide(ge_p2& U, const uint32_t pk[8], const uint32_t pi[20],
-                                           const uint16_t* bw) {
+__device__ __forceinline__ bool vrf_u_wide_pw(pw& U, const uint32_t pk[8], const uint32_t pi[20],
+                                              const uint16_t* bw) {
   const Lanes L = lanes();
   ge_p3 Y;
   bool ok = !ge_has_small_order(pk) && ge_is_canonical(pk);
@@ -185,7 +185,14 @@ __device__ __forceinline__ bool vrf_u_wide(ge_p2& U, const uint32_t pk[8], const
   sc_reduce256(s, s_raw);
   TabW t;
   tab_build(t, pw_from_p3(ge_p3_neg(Y), L), d2_wide(L), L);
-  U = pw_to_p2(pw_dsm<false, true>(t, c, 33, t, c, 0, s, bw, L));
+  U = pw_dsm<false, true>(t, c, 33, t, c, 0, s, bw, L);
+  return ok;
+}
+__device__ __forceinline__ bool vrf_u_wide(ge_p2& U, const uint32_t pk[8], const uint32_t pi[20],
+                                           const uint16_t* bw) {
+  pw Uw;
+  const bool ok = vrf_u_wide_pw(Uw, pk, pi, bw);
+  U = pw_to_p2(Uw);
   return ok;
 }
 
@@ -379,11 +386,69 @@ __device__ __forceinline__ void vrf_v_full_wide(uint32_t Henc[8], uint32_t Venc[
   ge_encode_with_inv(Venc, V.X, V.Y, fe_mul(inv, H.Z));
 }
 
+// canonical encodings from this row's affine coordinate of x and y (rows
+// rx / ry of c): y with x's parity in bit 255 (ge25519.h ge_encode_with_inv)
+__device__ __forceinline__ void enc_from_rows(uint32_t out[8], int32_t c, int rx, int ry) {
+  uint32_t xw[8];
+  fe_to_words(out, fw_to_fe(c, ry));
+  fe_to_words(xw, fw_to_fe(c, rx));
+  out[7] ^= (xw[0] & 1u) << 31;
+}
+// encode(P) for a wave-wide point: Z^-1 on the wave, then x and y as one
+// layer of row products (rows 0 / 1)
+__device__ __forceinline__ void encode1_wide(uint32_t enc[8], const pw& P) {
+  const Lanes L = lanes();
+  const int32_t zi = fw_invert(P.Z);
+  const int32_t c = fw_mul(L.odd ? P.Y : P.X, zi, L);
+  enc_from_rows(enc, c, 0, 1);
+}
+// encode(H) and encode(V) with one inversion: 1 / (ZH ZV), then 1 / ZH and
+// 1 / ZV (rows 0 / 1), then xH, yH, xV, yV (rows 0..3), all on the wave
+__device__ __forceinline__ void encode2_wide(uint32_t Henc[8], uint32_t Venc[8], const pw& H,
+                                             const pw& V) {
+  const Lanes L = lanes();
+  const int32_t inv = fw_invert(fw_mul_rep(H.Z, V.Z, L));
+  const fw4 zi = fw_gather(fw_mul(inv, L.odd ? H.Z : V.Z, L));  // r0 = 1/ZH, r1 = 1/ZV
+  const int32_t c = fw_mul(sel4(H.X, H.Y, V.X, V.Y, L), L.high ? zi.r1 : zi.r0, L);
+  enc_from_rows(Henc, c, 0, 1);
+  enc_from_rows(Venc, c, 2, 3);
+}
+
+// The Gamma core of the split form in two parts: the acceptance checks and
+// the V part -[c]Gamma (stored at `part`, a wave-wide point) first -- a VRF's
+// combination waits for it -- then [8]Gamma and beta, which only the header's
+// tail reads.  Returns the flag word; Gw keeps the decoded Gamma.
+__device__ __forceinline__ int32_t vrf_gamma_part_wide(Slot part, pw& Gw, const uint32_t pi[20]) {
+  const Lanes L = lanes();
+  uint32_t G[8], c[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    G[i] = pi[i];
+    c[i] = i < 4 ? pi[8 + i] : 0u;
+  }
+  ge_p3 Gamma;
+  bool ok = ge_is_canonical(G);
+  ok = ge_decode_wide(&Gamma, G, false) && ok;
+  Gw = pw_from_p3(Gamma, L);
+  TabW t;
+  tab_build(t, pw_from_p3(ge_p3_neg(Gamma), L), d2_wide(L), L);
+  st_pw(part, pw_dsm<false, false>(t, c, 33, t, c, 0, c, nullptr, L));
+  return (ok ? kFlagOk : 0) | (fe_iszero(Gamma.X) ? kFlagGammaX0 : 0);
+}
+__device__ __forceinline__ void vrf_gamma_beta_part_wide(uint32_t beta[16], const pw& Gw) {
+  const Lanes L = lanes();
+  uint32_t enc[8];
+  encode1_wide(enc, pw_dbl(pw_dbl(pw_dbl(Gw, L), L), L));
+  vrf_beta(beta, enc);
+}
+
 // The Gamma core: acceptance checks, [8]Gamma, beta = SHA-512(suite || 0x03
 // || encode([8]Gamma)) and the V half -[c]Gamma (`partial`); returns the flag
 // word (with kFlagGammaX0)
+// (split form: -[c]Gamma stored as a wave-wide point at `split` instead)
 __device__ __forceinline__ int32_t vrf_gamma_beta_wide(uint32_t beta[16], ge_p2& partial,
-                                                       const uint32_t pi[20]) {
+                                                       const uint32_t pi[20],
+                                                       const Slot* split = nullptr) {
   const Lanes L = lanes();
   uint32_t G[8], c[8];
 #pragma unroll
@@ -401,7 +466,9 @@ __device__ __forceinline__ int32_t vrf_gamma_beta_wide(uint32_t beta[16], ge_p2&
   vrf_beta(beta, enc);
   TabW t;
   tab_build(t, pw_from_p3(ge_p3_neg(Gamma), L), d2_wide(L), L);
-  partial = pw_to_p2(pw_dsm<false, false>(t, c, 33, t, c, 0, c, nullptr, L));
+  const pw part = pw_dsm<false, false>(t, c, 33, t, c, 0, c, nullptr, L);
+  if (split) st_pw(*split, part);
+  else partial = pw_to_p2(part);
   return (ok ? kFlagOk : 0) | (fe_iszero(Gamma.X) ? kFlagGammaX0 : 0);
 }
 
@@ -603,6 +670,178 @@ __device__ __forceinline__ bool ed_chain(Slot e, const uint16_t* bw) {
   tab_build(t2, pw_from_p3(negR, L), d2, L);
   const pw Q = pw_dsm<true, true>(t1, c0, nw, t2, c1, nw, b, bw, L);
   return ok && pw_is_identity(Q);
+}
+
+// ---- fused mode, split form (kernels_lat.hip OURO_LAT_SPLIT) -------------------
+// Each Ed25519 check over THREE waves and without the lattice pair: libsodium
+// accepts iff Q = [S]B - [h]A - R == O (R_bytes canonical and decodable, x = 0
+// only with sign 0; h = SHA-512(R || A || M) mod L; the same precondition as
+// the half-size equation), and with h's signed width-4 windows 0..31 / 32..63
+// and S's 16-bit digits 0..7 / 8..15 (each recoded as one number)
+//   X = [h windows 0..31](-A) + [S digits 0..7]B           (128-bit chain)
+//   Y = [h windows 32..63](-A128) + [S digits 8..15]B'     (A128 = 2^128 A, B' = 2^128 B)
+//   Q = X + Y + (-R).
+// The points item P (checks, A and R decoded), the scalars item S (the hash)
+// and the doubling item D (A decoded again, 128 doublings to -A128) start
+// together; X runs on the second of P and S to arrive, Y on the second of D
+// and S, and the second chain to finish adds the three points and compares
+// with the identity.  No wave ever waits: whoever completes a pair runs what
+// the pair enables.  Record (Slot e, kEdWords): h 0, S 8, points ok 16,
+// counters 17 (X), 18 (Y), 19 (both chains done), wave-wide points -A 32,
+// -R 96, -A128 160, X 224, Y 288.
+constexpr int kEsH = 0, kEsS = 8, kEsOk = 16, kEsCx = 17, kEsCy = 18, kEsCd = 19;
+constexpr int kEsA = 32, kEsR = kEsA + kPwWords, kEsA128 = kEsR + kPwWords;
+constexpr int kEsX = kEsA128 + kPwWords, kEsY = kEsX + kPwWords;
+static_assert(kEsY + kPwWords <= kEdWords, "Ed record");
+
+__device__ __forceinline__ void eds_points(Slot e, const uint32_t sig[16], const uint32_t pk[8],
+                                           bool extra_ok) {
+  const Lanes L = lanes();
+  uint32_t R[8], S[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    R[i] = sig[i];
+    S[i] = sig[8 + i];
+  }
+  bool ok = ed25519_precheck(R, S, pk, false) && extra_ok;
+  ge_p3 negA, negR;
+  bool okA, okR;
+  ge_decode_pair_wide(&negA, &okA, &negR, &okR, pk, R, true);
+  ok = okA && ok;
+  ok = ge_is_canonical(R) && ok;
+  ok = okR && ok;
+  ok = ok && !(fe_iszero(negR.X) && (R[7] >> 31) != 0);
+  st_pw(e + kEsA, pw_from_p3(negA, L));
+  st_pw(e + kEsR, pw_from_p3(negR, L));
+  if ((threadIdx.x & 63u) == 0) stg1(e.word(kEsOk), ok ? 1 : 0);
+}
+
+template <class Tail>
+__device__ __forceinline__ void eds_scalars(Slot e, const uint32_t sig[16], const uint32_t pk[8],
+                                            const Tail& msg, uint32_t mlen) {
+  uint32_t pre[16];
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    pre[i] = sig[i];
+    pre[8 + i] = pk[i];
+  }
+  uint64_t H[8];
+  if (OURO_SHA_WAVE && ((64 + mlen + 17 + 127) >> 7) <= sha_wave_max_blocks<64>())
+    sha512_prefixed_wave<64, 64>(H, pre, msg, mlen);
+  else
+    sha512_prefixed<64>(H, pre, msg, mlen);
+  uint32_t hw[16], h[8];
+  sha512_digest_words(hw, H);
+  sc_reduce512(h, hw);
+  if ((threadIdx.x & 63u) == 0) {
+    st_words8(e + kEsH, h);
+    st_words8(e + kEsS, sig + 8);
+  }
+}
+
+// -A128 = [2^128](-A), A decoded once more on this wave
+__device__ __forceinline__ void eds_double(Slot e, const uint32_t pk[8]) {
+  const Lanes L = lanes();
+  ge_p3 negA;
+  ge_decode_wide(&negA, pk, true);
+  pw P = pw_from_p3(negA, L);
+#pragma unroll 1
+  for (int k = 0; k < 128; k++) P = pw_dbl(P, L);
+  st_pw(e + kEsA128, P);
+}
+
+// h >> 128 plus the carry h's signed windows 0..31 hand to window 32
+OURO_FI void sc_high_half_with_carry(uint32_t hh[8], const uint32_t h[8]) {
+  const uint32_t cin = (uint32_t)(sc_recode_carries<4, 64>(h) >> 32) & 1u;
+  uint64_t c = cin;
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    c += h[4 + i];
+    hh[i] = (uint32_t)c;
+    c >>= 32;
+    hh[4 + i] = 0;
+  }
+}
+
+__device__ __forceinline__ void eds_chain(Slot e, const uint16_t* bw, bool high) {
+  const Lanes L = lanes();
+  uint32_t h[8], S[8], a[8];
+  ld_words8(h, e + kEsH);
+  ld_words8(S, e + kEsS);
+  TabW t;
+  tab_build(t, ld_pw(e + (high ? kEsA128 : kEsA)), d2_wide(L), L);
+  if (high) {
+    sc_high_half_with_carry(a, h);
+    st_pw(e + kEsY, pw_dsm<false, true, 2>(t, a, 32, t, a, 0, S, bw, L));
+  } else {
+    st_pw(e + kEsX, pw_dsm<false, true, 1>(t, h, 32, t, h, 0, S, bw, L));
+  }
+}
+
+__device__ __forceinline__ bool eds_combine(Slot e) {
+  const Lanes L = lanes();
+  const int32_t d2 = d2_wide(L);
+  const pw Q = pw_add_p3(pw_add_p3(ld_pw(e + kEsX), ld_pw(e + kEsY), d2, L), ld_pw(e + kEsR), d2, L);
+  return ldg1(e.word(kEsOk)) != 0 && pw_is_identity(Q);
+}
+
+// V = [s]H - [c]Gamma over THREE waves: [s windows 0..31]H (the V item),
+// [s windows 32..63](2^128 H) (the V2 item: H again, then 128 doublings) and
+// -[c]Gamma (the Gamma item); the last of the three adds them and encodes H
+// and V.  Record per VRF (kLatVsplit + 4 kPwWords which): H, the low and
+// high parts, -[c]Gamma, as wave-wide points.
+template <class Tail>
+__device__ __forceinline__ void vrf_sh_split(Slot v, const uint32_t pk[8], const uint32_t pi[20],
+                                             const Tail& alpha, bool high) {
+  const Lanes L = lanes();
+  uint32_t s_raw[8], s[8];
+#pragma unroll
+  for (int k = 0; k < 8; k++) s_raw[k] = pi[12 + k];
+  sc_reduce256(s, s_raw);
+  uint32_t pre[9];
+  pre[0] = 0x04u | (0x01u << 8) | (pk[0] << 16);
+#pragma unroll
+  for (int k = 1; k < 8; k++) pre[k] = (pk[k - 1] >> 16) | (pk[k] << 16);
+  pre[8] = pk[7] >> 16;
+  uint64_t Hs[8];
+  sha512_prefixed<34>(Hs, pre, alpha, 32);
+  uint32_t rw[16];
+  sha512_digest_words(rw, Hs);
+  rw[7] &= 0x7fffffffu;
+  auto pw22523 = [](const fe& z) { return pow22523_wide(z); };
+  const ge_p3 P = elligator2_h_with<decltype(pw22523), false>(rw, pw22523);
+  pw Hw = pw_dbl(pw_dbl(pw_dbl(pw_from_p3(P, L), L), L), L);
+  if (!high) {
+    st_pw(v, Hw);
+  } else {
+#pragma unroll 1
+    for (int k = 0; k < 128; k++) Hw = pw_dbl(Hw, L);
+    uint32_t hh[8];
+    sc_high_half_with_carry(hh, s);
+#pragma unroll
+    for (int k = 0; k < 8; k++) s[k] = hh[k];
+  }
+  TabW tab;
+  tab_build(tab, Hw, d2_wide(L), L);
+  st_pw(v + (high ? 2 : 1) * kPwWords, pw_dsm<false, false>(tab, s, 32, tab, s, 0, s, nullptr, L));
+}
+
+// the last of a VRF's V, V2 and Gamma items: V = the three parts, H and V
+// encoded with one inversion
+__device__ __forceinline__ void vrf_split_combine_encode(Slot res, int which) {
+  const Lanes L = lanes();
+  const Slot v = res + kLatVsplit + 4 * kPwWords * which;
+  const int32_t d2 = d2_wide(L);
+  const pw Vw = pw_add_p3(pw_add_p3(ld_pw(v + kPwWords), ld_pw(v + 2 * kPwWords), d2, L),
+                          ld_pw(v + 3 * kPwWords), d2, L);
+  vstamp(5);
+  uint32_t Henc[8], Venc[8];
+  encode2_wide(Henc, Venc, ld_pw(v), Vw);
+  vstamp(6);
+  if ((threadIdx.x & 63u) == 0) {
+    st_words8(res + kLatEnc + 8 * (3 * which + 0), Henc);
+    st_words8(res + kLatEnc + 8 * (3 * which + 2), Venc);
+  }
 }
 
 // The eta nonce's candidates (tpraos.h hdr_eta_nonce): Blake2b-256 of the
