@@ -154,6 +154,32 @@ __device__ __forceinline__ int64_t add_rows_u64(int64_t a) {
   const auto h2 = __builtin_amdgcn_permlane32_swap(shi, shi, false, false);
   return (int64_t)(((uint64_t)h2[0] << 32 | l2[0]) + ((uint64_t)h2[1] << 32 | l2[1]));
 }
+// The replicated products' carry: each row's partial accumulator (four
+// steps: |acc_r| < 2^43.1) goes through the first carry round by itself
+// (a0 + a1 + a2 of fw_carry2, below 2^21.4), the four rows' 32-bit results
+// are summed across rows (below 2^23.4), then the last shift-and-rotate
+// round: limbs below 2^16 + 38 * 2^7.4 < 2^16.13 (3 of them sum below
+// 220,752, the narrow operand's limit).  Two 32-bit permlane sums instead of
+// two 64-bit ones before the carry.
+#ifndef OURO_FW_ROWSUM32
+#define OURO_FW_ROWSUM32 1  // A/B switch: 0 = 64-bit cross-row sum, then fw_carry_l
+#endif
+__device__ __forceinline__ int32_t add_rows_i32(int32_t x) {
+  const auto p = __builtin_amdgcn_permlane16_swap(x, x, false, false);
+  const int32_t s = (int32_t)p[0] + (int32_t)p[1];
+  const auto q = __builtin_amdgcn_permlane32_swap(s, s, false, false);
+  return (int32_t)q[0] + (int32_t)q[1];
+}
+__device__ __forceinline__ int32_t fw_carry_rows(int64_t acc, const Lanes& L) {
+  if (!OURO_FW_ROWSUM32) return fw_carry_l(add_rows_u64(acc), L);
+  const uint32_t lo32 = (uint32_t)acc;
+  const int32_t a2 = (int32_t)(acc >> 32);
+  const int32_t sr = (int32_t)(lo32 & 0xffffu) + s24(dpp<0x121>((int32_t)(lo32 >> 16))) * s24(L.fac) +
+                     s24(dpp<0x122>(a2)) * s24(L.fac2);
+  const int32_t s = add_rows_i32(sr);
+  return (s & 0xffff) + s24(ror1(s >> 16)) * s24(L.fac);
+}
+
 __device__ __forceinline__ int32_t fw_mul_rep(int32_t f, int32_t g, const Lanes& L) {
   const int j = L.j;
   // f' lane k = f_(4r + k); G lane j = g_(j - 4r) (x 38 where it wrapped)
@@ -169,7 +195,7 @@ __device__ __forceinline__ int32_t fw_mul_rep(int32_t f, int32_t g, const Lanes&
   acc += (int64_t)bcast<2>(fr) * G;
   G = s24(ror1(G)) * s24(L.fac);
   acc += (int64_t)bcast<3>(fr) * G;
-  return fw_carry_l(add_rows_u64(acc), L);
+  return fw_carry_rows(acc, L);
 }
 
 // f^2 for a REPLICATED f: fw_mul_rep with g = f, the three row rotations
@@ -191,7 +217,7 @@ __device__ __forceinline__ int32_t fw_sq_rep(int32_t f, const Lanes& L) {
   acc += (int64_t)bcast<2>(fr) * G;
   G = s24(ror1(G)) * s24(L.fac);
   acc += (int64_t)bcast<3>(fr) * G;
-  return fw_carry_l(add_rows_u64(acc), L);
+  return fw_carry_rows(acc, L);
 }
 
 // ---- conversions -------------------------------------------------------------
