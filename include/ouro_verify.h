@@ -411,6 +411,12 @@ int ouro_tpraos_plan_debug_poison(ouro_tpraos_plan *plan);
  * waiting in the pool.  Host-only. */
 int ouro_debug_contexts(int device, size_t *created, size_t *idle);
 
+/* TIMING PROBE (tools/lat_stamps.py): header 0's per-item stamps of the last
+ * fused latency launch, 16 items x 24 tags of s_memrealtime (100 MHz), for a
+ * library built with -DOURO_LAT_STAMPS=1 and run with OURO_LAT_STAMPS set.
+ * Returns the number of stamps written to out, or -1 (the product build). */
+int ouro_debug_lat_stamps(unsigned long long *out);
+
 /* ---------------------------------------------- leader threshold ----- */
 /* ledger-specs checkLeaderValue (shelley-spec-ledger BlockChain.hs), called by
  * meetsLeaderThreshold, ouroboros-consensus-shelley/src/Ouroboros/Consensus/

@@ -153,6 +153,7 @@ __global__ void k_tpraos_cores(ouro_tpraos_batch b, const uint32_t* __restrict__
                                uint8_t* __restrict__ verdict, uint8_t* __restrict__ beta_eta,
                                uint8_t* __restrict__ beta_leader);
 int lat_fused_items_host();  // kernels_lat.hip: waves per header of the fused launch
+int lat_stamps_read(unsigned long long* out);  // kernels_lat.hip: the latency probe's stamps
 __global__ void k_ed25519_wide(size_t n, const uint8_t* __restrict__ pk,
                                const uint8_t* __restrict__ sig, const uint8_t* __restrict__ msg,
                                const uint64_t* __restrict__ msg_off,
@@ -1530,6 +1531,12 @@ int ouro_tpraos_plan_debug_poison(ouro_tpraos_plan* p) {
   OURO_HIP(hipMemcpy(p->res, h.data(), sizeof(int32_t) * words, hipMemcpyHostToDevice));
   return OURO_OK;
 }
+
+// TIMING PROBE (tools/lat_stamps.py): header 0's per-item stamps of the last
+// fused latency launch, 16 items x 24 tags of s_memrealtime (100 MHz), from a
+// library built with -DOURO_LAT_STAMPS=1 and run with OURO_LAT_STAMPS set;
+// returns the count, or -1 in the product build.
+int ouro_debug_lat_stamps(unsigned long long* out) { return lat_stamps_read(out); }
 
 // Contexts of the per-thread pool on `device` (kernels.hip ThreadCtx):
 // created so far and idle (returned by exited threads).

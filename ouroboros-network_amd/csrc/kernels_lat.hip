@@ -191,16 +191,15 @@ __device__ __noinline__ void hdr_item_fused(const ouro_tpraos_batch& b, size_t i
 #if defined(__HIP_DEVICE_COMPILE__)
   using namespace wide;
   const bool lead = (threadIdx.x & 63u) == 0;
-  const uint64_t t0 = stamps ? __builtin_amdgcn_s_memrealtime() : 0;
+  (void)stamps;
+  lstamp(0);
+  // probe tags (wide_cores.h lstamp): 1 own part done, 2 / 3 chain X / Y done,
+  // 4..7 a VRF combination (start, adds, inverted, encoded), 8 the item's end,
+  // 9 / 10 / 11 the tail (start, challenges, end); V / V2 phases 12..18
   auto stamp = [&](const char* what) {
-#if OURO_LAT_STAMPS
-    if (stamps && lead && i == 0)
-      printf("stamp %d %s %llu %llu\n", item, what, (unsigned long long)t0,
-             (unsigned long long)__builtin_amdgcn_s_memrealtime());
-#else
-    (void)what;
-    (void)t0;
-#endif
+    const char c = what[0], c1 = what[1], c2 = what[2];
+    lstamp(c == 'w' ? 1 : c == 'c' && c1 == 'h' && c2 == 'x' ? 2 : c == 'c' && c1 == 'h' ? 3
+           : c == 't' ? 11 : c == 'c' && c1 == 'o' && c2 == 'm' ? 7 : 8);
   };
   const bool ed_item = item == kCoreOcert || item == kCoreKes ||
                        (item >= kLatCores && item < kLatCores + (OURO_LAT_SPLIT ? 4 : 2));
@@ -290,14 +289,12 @@ __device__ __noinline__ void hdr_item_fused(const ouro_tpraos_batch& b, size_t i
       kstamp(2);
     }
     if (!arrive_last(ed.word(125), gen, 2)) {
-      if (stamps && e == 1) kstamp_print();
       stamp("half");
       return;
     }
     kstamp(3);
     const int32_t flag = (!skipped && ed_chain(ed, bw)) ? kFlagOk : 0;
     kstamp(4);
-    if (stamps && e == 1) kstamp_print();
     if (lead) stg1(res.word(kResFlags + e), flag);
   } else if (OURO_LAT_SPLIT && item >= kLatCores + 4) {
     // V2: [s windows 32..63](2^128 H), then the VRF's three-party arrival
@@ -371,7 +368,6 @@ __device__ __noinline__ void hdr_item_fused(const ouro_tpraos_batch& b, size_t i
     }
   }
   stamp("core");
-  if (stamps) vstamp_print();
   if (arrive_last(res.word(kLatCtr), gen, kHdrParties)) {
     hdr_tail_wide(b, i, opts, res, verdict, beta_eta, beta_leader);
     stamp("tail");
@@ -381,6 +377,18 @@ __device__ __noinline__ void hdr_item_fused(const ouro_tpraos_batch& b, size_t i
 
 // items per header of the fused launch (the host sizes the grid with it)
 int lat_fused_items_host() { return kFusedItems; }
+
+// the probe's stamps of the last launch (a -DOURO_LAT_STAMPS=1 build; else -1)
+int lat_stamps_read(unsigned long long* out) {
+#if OURO_LAT_STAMPS
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_lat_stamps),
+                             sizeof(unsigned long long) * kStampItems * kStampTags) ==
+                 hipSuccess ? kStampItems * kStampTags : -1;
+#else
+  (void)out;
+  return -1;
+#endif
+}
 
 // the k-th set bit of m (k < popcount(m))
 __device__ __forceinline__ int nth_set_bit(uint32_t m, int k) {

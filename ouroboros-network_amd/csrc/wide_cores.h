@@ -10,6 +10,15 @@
 #include "wide.h"
 
 namespace ouro {
+// the latency probe's stamp table (lstamp below; host and device passes both
+// see it, so the host reads it with hipMemcpyFromSymbol)
+#ifndef OURO_LAT_STAMPS
+#define OURO_LAT_STAMPS 0
+#endif
+constexpr int kStampItems = 16, kStampTags = 24;
+#if OURO_LAT_STAMPS
+__device__ unsigned long long g_lat_stamps[kStampItems][kStampTags];
+#endif
 #if defined(__HIP_DEVICE_COMPILE__)
 namespace wide {
 
@@ -52,6 +61,18 @@ __device__ __forceinline__ void kstamp_print() {
     printf("kstamp %d %llu %llu %llu %llu %llu %llu %llu %llu\n", blockIdx.x == 9 ? 9 : 1, s[0],
            s[1], s[2], s[3], s[4], s[5], s[6], s[7]);
   }
+#endif
+}
+// printf-free probe of the fused launch (split form): the lead lane of header
+// 0's items (blocks 0..kStampItems-1 with 64-thread workgroups) records
+// s_memrealtime at tagged points into g_lat_stamps[item][tag]; the host reads
+// them after the launch (kernels.hip ouro_debug_lat_stamps, tools/lat_stamps.py)
+__device__ __forceinline__ void lstamp(int tag) {
+#if OURO_LAT_STAMPS
+  if (blockIdx.x < (unsigned)kStampItems && (threadIdx.x & 63u) == 0 && tag < kStampTags)
+    g_lat_stamps[blockIdx.x][tag] = __builtin_amdgcn_s_memrealtime();
+#else
+  (void)tag;
 #endif
 }
 __device__ __forceinline__ void vstamp_print() {
@@ -408,6 +429,7 @@ __device__ __forceinline__ void encode2_wide(uint32_t Henc[8], uint32_t Venc[8],
                                              const pw& V) {
   const Lanes L = lanes();
   const int32_t inv = fw_invert(fw_mul_rep(H.Z, V.Z, L));
+  lstamp(6);
   const fw4 zi = fw_gather(fw_mul(inv, L.odd ? H.Z : V.Z, L));  // r0 = 1/ZH, r1 = 1/ZV
   const int32_t c = fw_mul(sel4(H.X, H.Y, V.X, V.Y, L), L.high ? zi.r1 : zi.r0, L);
   enc_from_rows(Henc, c, 0, 1);
@@ -808,9 +830,16 @@ __device__ __forceinline__ void vrf_sh_split(Slot v, const uint32_t pk[8], const
   uint32_t rw[16];
   sha512_digest_words(rw, Hs);
   rw[7] &= 0x7fffffffu;
-  auto pw22523 = [](const fe& z) { return pow22523_wide(z); };
+  lstamp(12);
+  auto pw22523 = [](const fe& z) {
+    lstamp(13);
+    const fe r = pow22523_wide(z);
+    lstamp(14);
+    return r;
+  };
   const ge_p3 P = elligator2_h_with<decltype(pw22523), false>(rw, pw22523);
   pw Hw = pw_dbl(pw_dbl(pw_dbl(pw_from_p3(P, L), L), L), L);
+  lstamp(15);
   if (!high) {
     st_pw(v, Hw);
   } else {
@@ -821,9 +850,12 @@ __device__ __forceinline__ void vrf_sh_split(Slot v, const uint32_t pk[8], const
 #pragma unroll
     for (int k = 0; k < 8; k++) s[k] = hh[k];
   }
+  lstamp(16);
   TabW tab;
   tab_build(tab, Hw, d2_wide(L), L);
+  lstamp(17);
   st_pw(v + (high ? 2 : 1) * kPwWords, pw_dsm<false, false>(tab, s, 32, tab, s, 0, s, nullptr, L));
+  lstamp(18);
 }
 
 // the last of a VRF's V, V2 and Gamma items: V = the three parts, H and V
@@ -832,12 +864,13 @@ __device__ __forceinline__ void vrf_split_combine_encode(Slot res, int which) {
   const Lanes L = lanes();
   const Slot v = res + kLatVsplit + 4 * kPwWords * which;
   const int32_t d2 = d2_wide(L);
+  lstamp(4);
   const pw Vw = pw_add_p3(pw_add_p3(ld_pw(v + kPwWords), ld_pw(v + 2 * kPwWords), d2, L),
                           ld_pw(v + 3 * kPwWords), d2, L);
-  vstamp(5);
+  lstamp(5);
   uint32_t Henc[8], Venc[8];
   encode2_wide(Henc, Venc, ld_pw(v), Vw);
-  vstamp(6);
+  lstamp(7);
   if ((threadIdx.x & 63u) == 0) {
     st_words8(res + kLatEnc + 8 * (3 * which + 0), Henc);
     st_words8(res + kLatEnc + 8 * (3 * which + 2), Venc);
@@ -888,7 +921,9 @@ __device__ __forceinline__ void hdr_tail_wide(const ouro_tpraos_batch& b, size_t
   if (fg & kFlagGammaX0) Genc[7] &= 0x7fffffffu;
 #pragma unroll
   for (int k = 0; k < 4; k++) c[k] = pi[8 + k];
+  lstamp(9);
   const bool ceq = vrf_challenge_ok_wave(Henc, Genc, Uenc, Venc, c);
+  lstamp(10);
   const bool ok = (fu & fv & fg & kFlagOk) && ceq;
   ld_words8(beta, res + kLatBeta + 16 * which);
   ld_words8(beta + 8, res + kLatBeta + 16 * which + 8);

@@ -1,11 +1,17 @@
 #!/usr/bin/env python3
-"""Timing probe of the fused configs[4] launch: a library built with
--DOURO_LAT_STAMPS=1 (tools/build_variant.sh stamps -DOURO_LAT_STAMPS=1), run
-with OURO_LAT_STAMPS set, prints header 0's item start/end times
-(s_memrealtime, 100 MHz); this runs a 64-header plan R times on that library
-(OURO_VERIFY_LIB) and prints, per item, the median start and end in us
-relative to the earliest start of each launch.  Items: 0/8 OCERT points/
-scalars, 1/9 KES points/scalars, 2/3 U eta/leader, 4/5 V, 6/7 Gamma.
+"""Timing probe of the fused configs[4] launch (split form).
+
+A library built with -DOURO_LAT_STAMPS=1 (tools/build_lat_variant.sh stamps
+-DOURO_LAT_STAMPS=1) records, without printf, s_memrealtime (100 MHz) at tagged
+points of header 0's items into device memory (wide_cores.h lstamp); this
+runs a 64-header plan R times on that library (OURO_VERIFY_LIB), reads the
+stamps after each launch (ouro_debug_lat_stamps) and prints, per item and
+tag, the median time in us after the earliest start of the launch.
+Items: 0/8/10 OCERT points/scalars/doubling, 1/9/11 KES, 2/3 U eta/leader,
+4/5 V, 6/7 Gamma, 12/13 V2.  Tags: 0 start, 1 own part done, 2/3 chain X/Y
+done, 4..7 VRF combination (start, adds, inverted, encoded), 8 end, 9/10/11
+tail (start, challenges, end), 12..18 V/V2 phases (hash, exp start, exp end,
+H, H128, table, chain).
 
   python tools/lat_stamps.py [--runs R] [--lib PATH]
 """
@@ -16,29 +22,42 @@ import sys
 import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ITEMS = {0: "OCERT P", 8: "OCERT S", 10: "OCERT D", 1: "KES P", 9: "KES S", 11: "KES D",
+         2: "U eta", 3: "U leader", 4: "V eta", 5: "V leader", 6: "Gamma eta",
+         7: "Gamma leader", 12: "V2 eta", 13: "V2 leader"}
+TAGS = {0: "start", 1: "part", 2: "chainX", 3: "chainY", 4: "comb0", 5: "combAdd",
+        6: "combInv", 7: "combEnc", 8: "end", 9: "tail0", 10: "tailChal", 11: "tailEnd",
+        12: "hash", 13: "exp0", 14: "exp1", 15: "H", 16: "H128", 17: "table", 18: "chain"}
 
 CHILD = r"""
-import os, sys
+import ctypes, json, os, sys
 sys.path.insert(0, %r)
 import numpy as np, torch
 torch.cuda.init()
 import bench
 from ouroboros_network_amd.tpraos import HeaderPlan
+from ouroboros_network_amd import _native
 dev = torch.device("cuda", 0)
 t, _ = bench.synth_headers(256, 64, dev)
 hb = bench.DeviceHeaders(t, 256, dev).host_sample(64)
 plan = HeaderPlan(64, int(hb.body_len.astype(np.int64).sum()))
+lib = _native.load()
+buf = (ctypes.c_ulonglong * (16 * 24))()
+rows = []
 for r in range(%d):
+    ctypes.memset(buf, 0, ctypes.sizeof(buf))
     out = plan.run(hb)
     torch.cuda.synchronize()
-    print("run-end", flush=True)
+    assert lib.ouro_debug_lat_stamps(buf) == 16 * 24
+    rows.append(list(buf))
 assert (out[0] == 15).all()
 plan.close()
+print(json.dumps(rows))
 """
 
 
 def main():
-    runs = int(sys.argv[sys.argv.index("--runs") + 1]) if "--runs" in sys.argv else 20
+    runs = int(sys.argv[sys.argv.index("--runs") + 1]) if "--runs" in sys.argv else 30
     lib = sys.argv[sys.argv.index("--lib") + 1] if "--lib" in sys.argv else os.path.join(
         ROOT, "ouroboros-network_amd", "lib", "variants", "stamps.so")
     env = dict(os.environ, OURO_LAT_STAMPS="1", OURO_VERIFY_LIB=os.path.abspath(lib))
@@ -46,57 +65,20 @@ def main():
                        text=True, timeout=600)
     if p.returncode:
         sys.exit(p.stderr[-2000:])
-    launches, cur, vst, kst = [], [], {}, {}
-    for line in p.stdout.splitlines():
-        if line.startswith("kstamp "):
-            f = line.split()
-            kst.setdefault(len(launches), {})[int(f[1])] = [int(x) for x in f[2:]]
-        if line.startswith("vstamp "):
-            ts = [int(x) for x in line.split()[1:]]
-            tags = ["start", "sha", "elligator", "table", "chain", "combine-add", "encoded"]
-            vst.setdefault(len(launches), []).extend(zip(tags, ts))
-        if line.startswith("stamp "):
-            _, item, what, t0, t1 = line.split()
-            cur.append((int(item), what, int(t0), int(t1)))
-        elif line == "run-end":
-            launches.append(cur)
-            cur = []
-    rows = {}
-    for st in launches[2:]:  # skip warm-up launches
-        base = min(t0 for _, _, t0, _ in st)
-        for item, what, t0, t1 in st:
-            rows.setdefault((item, what), []).append(((t0 - base) / 100.0, (t1 - base) / 100.0))
-    print(f"{len(launches) - 2} launches; median start / end (us) per item of header 0")
-    for (item, what), v in sorted(rows.items(), key=lambda kv: np.median([e for _, e in kv[1]])):
-        a = np.array(v)
-        print(f"item {item:2d} {what:5s} start {np.median(a[:, 0]):7.1f}  end {np.median(a[:, 1]):7.1f}")
-    # phases of header 0's eta V item (vstamp), relative to its start
-    phases = {}
-    for k, st in vst.items():
-        if k < 2:
-            continue
-        t0 = dict(st).get("start")
-        for tag, t in st:
-            if t0 is not None:
-                phases.setdefault(tag, []).append((t - t0) / 100.0)
-    if phases:
-        print("eta V item phases (us after its start):",
-              ", ".join(f"{k} {np.median(v):.1f}" for k, v in phases.items()))
-    # header 0's KES items (kstamp): phases relative to the earlier start of the two
-    tags = ["start", "walk", "prep", "arrive", "chain", "sha", "reduce", "lattice"]
-    kph = {}
-    for k, st in kst.items():
-        if k < 2 or 1 not in st or 9 not in st:
-            continue
-        t0 = min(st[1][0], st[9][0])
-        for item in (1, 9):
-            for tag, t in zip(tags, st[item]):
-                if t:
-                    kph.setdefault((item, tag), []).append((t - t0) / 100.0)
-    for item, name in ((1, "KES points"), (9, "KES scalars")):
-        row = [f"{tag} {np.median(kph[(item, tag)]):.1f}" for tag in tags if (item, tag) in kph]
-        if row:
-            print(f"{name} item phases (us):", ", ".join(row))
+    import json
+    rows = json.loads(p.stdout.strip().splitlines()[-1])[2:]  # skip warm-up launches
+    a = np.array(rows, dtype=np.float64).reshape(len(rows), 16, 24)
+    base = np.where(a[:, :, 0] > 0, a[:, :, 0], np.inf).min(axis=1)
+    rel = (a - base[:, None, None]) / 100.0
+    print(f"{len(rows)} launches; header 0, median us after the launch's first item start")
+    ents = []
+    for item, name in ITEMS.items():
+        for tag, tname in TAGS.items():
+            v = rel[:, item, tag][a[:, item, tag] > 0]
+            if len(v) >= len(rows) // 2:
+                ents.append((float(np.median(v)), name, tname, len(v)))
+    for t, name, tname, n in sorted(ents):
+        print(f"{t:8.1f}  {name:13s} {tname:9s} (n={n})")
 
 
 if __name__ == "__main__":
