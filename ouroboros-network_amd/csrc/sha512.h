@@ -61,6 +61,35 @@ OURO_FI uint64_t shr64(uint64_t x, int n) {
 #endif
 }
 
+// three-input XOR and majority per 32-bit half: one gfx950 v_bitop3_b32 each
+// (truth tables 0x96 / 0xE8, both symmetric in their inputs) instead of two
+// XORs, or an AND-XOR chain
+#if defined(__HIP_DEVICE_COMPILE__)
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+template <int kTable>
+OURO_FI uint64_t bitop3_64(uint64_t a, uint64_t b, uint64_t c) {
+  const u32x2 x = __builtin_bit_cast(u32x2, a), y = __builtin_bit_cast(u32x2, b),
+              z = __builtin_bit_cast(u32x2, c);
+  const u32x2 r = {(uint32_t)__builtin_amdgcn_bitop3_b32(x.x, y.x, z.x, kTable),
+                   (uint32_t)__builtin_amdgcn_bitop3_b32(x.y, y.y, z.y, kTable)};
+  return __builtin_bit_cast(uint64_t, r);
+}
+#endif
+OURO_FI uint64_t xor3_64(uint64_t a, uint64_t b, uint64_t c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return bitop3_64<0x96>(a, b, c);
+#else
+  return a ^ b ^ c;
+#endif
+}
+OURO_FI uint64_t maj64(uint64_t a, uint64_t b, uint64_t c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return bitop3_64<0xE8>(a, b, c);
+#else
+  return (a & b) ^ (a & c) ^ (b & c);
+#endif
+}
+
 OURO_FI void sha512_init(uint64_t H[8]) {
   H[0] = 0x6a09e667f3bcc908ULL; H[1] = 0xbb67ae8584caa73bULL;
   H[2] = 0x3c6ef372fe94f82bULL; H[3] = 0xa54ff53a5f1d36f1ULL;
@@ -70,11 +99,11 @@ OURO_FI void sha512_init(uint64_t H[8]) {
 
 OURO_FI void sha512_round(uint64_t& a, uint64_t& b, uint64_t& c, uint64_t& d, uint64_t& e,
                           uint64_t& f, uint64_t& g, uint64_t& h, uint64_t k, uint64_t w) {
-  const uint64_t S1 = rotr64(e, 14) ^ rotr64(e, 18) ^ rotr64(e, 41);
+  const uint64_t S1 = xor3_64(rotr64(e, 14), rotr64(e, 18), rotr64(e, 41));
   const uint64_t ch = (e & f) ^ (~e & g);
   const uint64_t T1 = h + S1 + ch + k + w;
-  const uint64_t S0 = rotr64(a, 28) ^ rotr64(a, 34) ^ rotr64(a, 39);
-  const uint64_t mj = (a & b) ^ (a & c) ^ (b & c);
+  const uint64_t S0 = xor3_64(rotr64(a, 28), rotr64(a, 34), rotr64(a, 39));
+  const uint64_t mj = maj64(a, b, c);
   h = g; g = f; f = e; e = d + T1; d = c; c = b; b = a; a = T1 + S0 + mj;
 }
 
@@ -90,8 +119,8 @@ OURO_NI void sha512_compress(uint64_t H[8], uint64_t W[16]) {
 #pragma unroll
     for (int i = 0; i < 16; i++) {
       const uint64_t w15 = W[(i + 1) & 15], w2 = W[(i + 14) & 15];
-      const uint64_t s0 = rotr64(w15, 1) ^ rotr64(w15, 8) ^ shr64(w15, 7);
-      const uint64_t s1 = rotr64(w2, 19) ^ rotr64(w2, 61) ^ shr64(w2, 6);
+      const uint64_t s0 = xor3_64(rotr64(w15, 1), rotr64(w15, 8), shr64(w15, 7));
+      const uint64_t s1 = xor3_64(rotr64(w2, 19), rotr64(w2, 61), shr64(w2, 6));
       W[i] += s0 + W[(i + 9) & 15] + s1;
       sha512_round(a, b, c, d, e, f, g, h, kSha512K[r0 + i], W[i]);
     }
@@ -297,8 +326,8 @@ __device__ __forceinline__ void sha512_prefixed_wave(uint64_t out[8], const uint
 #pragma unroll
       for (int i = 0; i < 16; i++) {
         const uint64_t w15 = W[(i + 1) & 15], w2 = W[(i + 14) & 15];
-        const uint64_t s0 = rotr64(w15, 1) ^ rotr64(w15, 8) ^ shr64(w15, 7);
-        const uint64_t s1 = rotr64(w2, 19) ^ rotr64(w2, 61) ^ shr64(w2, 6);
+        const uint64_t s0 = xor3_64(rotr64(w15, 1), rotr64(w15, 8), shr64(w15, 7));
+        const uint64_t s1 = xor3_64(rotr64(w2, 19), rotr64(w2, 61), shr64(w2, 6));
         W[i] += s0 + W[(i + 9) & 15] + s1;
         k[r0 + i] = W[i] + kSha512K[r0 + i];
       }
