@@ -521,9 +521,15 @@ __device__ __forceinline__ void vrf_combine_encode(Slot res, int which) {
 // mid-count by an earlier launch that never completed (or a zeroed one) can
 // never make a header finish early with that launch's record contents --
 // every core rewrites its record fields before it arrives.
+// (A/B switch OURO_ARRIVE_RA: 1 = a release fence before the count and an
+// acquire fence after it for the last party only, 0 = two full fences)
+#ifndef OURO_ARRIVE_RA
+#define OURO_ARRIVE_RA 1
+#endif
 __device__ __forceinline__ bool arrive_last(int32_t* ctr, uint32_t gen,
                                             uint32_t parties = kLatCores) {
-  __threadfence();
+  if (OURO_ARRIVE_RA) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  else __threadfence();
   uint32_t mine = 0;
   if ((threadIdx.x & 63u) == 0) {
     unsigned int* c = reinterpret_cast<unsigned int*>(ctr);
@@ -541,7 +547,8 @@ __device__ __forceinline__ bool arrive_last(int32_t* ctr, uint32_t gen,
   }
   mine = (uint32_t)__builtin_amdgcn_readlane((int)mine, 0);
   if (mine != parties) return false;
-  __threadfence();
+  if (OURO_ARRIVE_RA) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  else __threadfence();
   return true;
 }
 
