@@ -117,6 +117,64 @@ __device__ __forceinline__ ge_p2 pw_to_p2(const pw& Q) {
   return ge_p2{fw_to_fe(Q.X), fw_to_fe(Q.Y), fw_to_fe(Q.Z)};
 }
 
+// ---- Elligator2 on the wave ------------------------------------------------------
+// verify.h elligator2_pre / elligator2_post (the one-exponentiation form of
+// libsodium's ge25519_from_uniform) with every product on the wave instead of
+// a lane (each lane-local product is one wave's dependent chain of ~200
+// instructions; a replicated wave product ~45): the same point, then the
+// cofactor cleared by three wave-wide doublings.  A/B switch OURO_ELL2_WIDE.
+// Bounds (wide.h): carried elements have limbs below 2^16.13; D and Xn are
+// 2-term sums and W a 3-term one (narrow operands: at most 3 terms); n and m
+// (4 terms) are renormalised by one shift-and-rotate round (fw_norm) before
+// they enter a product or the point.
+#ifndef OURO_ELL2_WIDE
+#define OURO_ELL2_WIDE 1
+#endif
+// one carry round of a limb vector below 2^20: limbs below 2^16 + 38 * 16
+__device__ __forceinline__ int32_t fw_norm(int32_t x, const Lanes& L) {
+  return (x & 0xffff) + s24(ror1(x >> 16)) * s24(L.fac);
+}
+// whether the replicated element in `row` of x is 0 mod p
+__device__ __forceinline__ bool fw_row_iszero(int32_t x, int row) {
+  return fe_iszero(fw_to_fe(x, row));
+}
+__device__ __forceinline__ pw elligator2_wide(const uint32_t r[8], const Lanes& L) {
+  const int32_t one = fw_one(L);
+  const int32_t rr = fe_to_fw(fe_from_words(r), L);
+  const int32_t r2 = fw_sq_rep(rr, L);
+  const int32_t D = r2 + r2 + one;                               // 1 + 2 r^2 (2 terms)
+  // A^2 r^2 (rows 0/2) and D^2 (rows 1/3) at once
+  const fw4 a = fw_gather(fw_mul(L.odd ? D : fe_to_fw(fe_mont_a2(), L), L.odd ? D : r2, L));
+  const int32_t W = a.r1 - a.r0 - a.r0;                          // D^2 - 2 A^2 r^2 (3 terms)
+  // (A + 2) A D (rows 0/2) and W^2 (rows 1/3)
+  const fw4 b = fw_gather(fw_mul(L.odd ? W : fe_to_fw(fe_mont_a2a(), L), L.odd ? W : D, L));
+  const int32_t num = b.r0;
+  const int32_t W3 = fw_mul_rep(b.r1, W, L);
+  const int32_t W7 = fw_mul_rep(fw_sq_rep(W3, L), W, L);
+  // num W3 and num sqrt(-1) (needed after the root) beside num W7 (its base)
+  const fw4 c = fw_gather(fw_mul(num, sel4(W7, W3, fe_to_fw(fe_sqrtm1(), L), W7, L), L));
+  const int32_t root = fw_pow22523(c.r0);                        // (num W^7)^((p-5)/8)
+  const int32_t beta = fw_mul_rep(c.r1, root, L);                // num W^3 (num W^7)^((p-5)/8)
+  const int32_t vxx = fw_mul_rep(fw_sq_rep(beta, L), W, L);      // beta^2 W
+  // the root's 4th root of unity: vxx = num (1), -num (-1), num i (i) or -num i
+  const int32_t d = sel4(vxx - num, vxx + num, vxx - c.r2, vxx - num, L);
+  const bool lam_p1 = fw_row_iszero(d, 0), lam_m1 = fw_row_iszero(d, 1);
+  const bool lam_pi = fw_row_iszero(d, 2);
+  const bool nonsq = !(lam_p1 || lam_m1);
+  const fe Ff = fe_select(fe_select(fe_one_minus_i(), fe_one_plus_i(), lam_pi),
+                          fe_select(fe_one(), fe_sqrtm1(), lam_p1), nonsq);
+  int32_t x = fw_mul_rep(beta, fe_to_fw(Ff, L), L);
+  if (nonsq) x = fw_mul_rep(x, rr, L);
+  if (fe_isnegative(fw_to_fe(x))) x = -x;                       // sign bit 0: even x
+  const int32_t Ar2 = fw_mul_rep(fe_to_fw(fe_mont_a(), L), r2, L);
+  const int32_t Xn = nonsq ? -(Ar2 + Ar2) : -fe_to_fw(fe_mont_a(), L);  // 2 terms
+  const int32_t n = fw_norm(Xn - D, L), m = fw_norm(Xn + D, L);
+  // P = (x m, n, m, x n): rows 0/2 x m, rows 1/3 x n
+  const fw4 e = fw_gather(fw_mul(x, L.odd ? n : m, L));
+  const pw P{e.r0, n, m, e.r1};
+  return pw_dbl(pw_dbl(pw_dbl(P, L), L), L);
+}
+
 // verify.h ed25519_verify_lane (libsodium 1.0.18 rules through the half-size
 // equation) on one wave
 template <class Tail>
@@ -309,7 +367,13 @@ __device__ __forceinline__ bool vrf03_verify_wide(uint32_t beta[16], const uint3
   uint32_t rw[16];
   sha512_digest_words(rw, Hs);
   rw[7] &= 0x7fffffffu;
-  const ge_p3 Hp = elligator2_h_with(rw, [](const fe& z) { return pow22523_wide(z); });
+  ge_p3 Hp;
+  if (OURO_ELL2_WIDE) {
+    const pw Hw = elligator2_wide(rw, L);
+    Hp = ge_p3{fw_to_fe(Hw.X), fw_to_fe(Hw.Y), fw_to_fe(Hw.Z), fw_to_fe(Hw.T)};
+  } else {
+    Hp = elligator2_h_with(rw, [](const fe& z) { return pow22523_wide(z); });
+  }
   const int32_t d2 = d2_wide(L);
   TabW tY, tH, tG;
   tab_build(tY, pw_from_p3(ge_p3_neg(Y), L), d2, L);
@@ -838,14 +902,19 @@ __device__ __forceinline__ void vrf_sh_split(Slot v, const uint32_t pk[8], const
   sha512_digest_words(rw, Hs);
   rw[7] &= 0x7fffffffu;
   lstamp(12);
-  auto pw22523 = [](const fe& z) {
-    lstamp(13);
-    const fe r = pow22523_wide(z);
-    lstamp(14);
-    return r;
-  };
-  const ge_p3 P = elligator2_h_with<decltype(pw22523), false>(rw, pw22523);
-  pw Hw = pw_dbl(pw_dbl(pw_dbl(pw_from_p3(P, L), L), L), L);
+  pw Hw;
+  if (OURO_ELL2_WIDE) {
+    Hw = elligator2_wide(rw, L);
+  } else {
+    auto pw22523 = [](const fe& z) {
+      lstamp(13);
+      const fe r = pow22523_wide(z);
+      lstamp(14);
+      return r;
+    };
+    const ge_p3 P = elligator2_h_with<decltype(pw22523), false>(rw, pw22523);
+    Hw = pw_dbl(pw_dbl(pw_dbl(pw_from_p3(P, L), L), L), L);
+  }
   lstamp(15);
   if (!high) {
     st_pw(v, Hw);
