@@ -161,6 +161,84 @@ OURO_FI ge_cached ld_cached(Slot p) {
            ouro_trk_load(p.word(20), c.Z2.b); ouro_trk_load(p.word(30), c.T2d.b);)
   return c;
 }
+// Packed entries of the per-lane tables (lane mode; lane quads keep the
+// 40-word form, which their per-operand loads index).  Each coordinate is
+// carried to the limb widths with limb 9 allowed 26 bits and packed into 256
+// bits, so an entry is 32 words -- one 128-B line instead of the two a 160-B
+// entry touches.  The gathers are the bulk of the kernels' HBM traffic.
+#ifndef OURO_TAB_PACK
+#define OURO_TAB_PACK 1
+#endif
+constexpr int kPackedWords = 32;
+constexpr int kLaneEntryWords = OURO_TAB_PACK ? kPackedWords : kCachedWords;
+// f (limbs < 2^28) as 256 bits: 2^255 wrapped first, then one carry pass that
+// leaves limbs 0..8 within their masks and limb 9 below 2^25 + 2^3
+OURO_FI void fe_pack256(uint32_t w[8], const fe& f) {
+  OURO_TRK(for (int i = 0; i < 10; i++) trk_check(f.b[i] < (1ull << 28));)
+  uint32_t h[10];
+#pragma unroll
+  for (int i = 0; i < 10; i++) h[i] = f.v[i];
+  uint32_t c = h[9] >> 25;
+  h[9] &= limb_mask(9);
+  h[0] += 19 * c;
+#pragma unroll
+  for (int i = 0; i < 9; i++) {
+    c = h[i] >> limb_bits(i);
+    h[i] &= limb_mask(i);
+    h[i + 1] += c;
+  }
+  w[0] = h[0] | (h[1] << 26);
+  w[1] = (h[1] >> 6) | (h[2] << 19);
+  w[2] = (h[2] >> 13) | (h[3] << 13);
+  w[3] = (h[3] >> 19) | (h[4] << 6);
+  w[4] = h[5] | (h[6] << 25);
+  w[5] = (h[6] >> 7) | (h[7] << 19);
+  w[6] = (h[7] >> 13) | (h[8] << 12);
+  w[7] = (h[8] >> 20) | (h[9] << 6);
+}
+OURO_FI fe fe_unpack256(const uint32_t w[8]) {
+  fe h;
+  h.v[0] = w[0] & 0x3ffffff;
+  h.v[1] = ((w[0] >> 26) | (w[1] << 6)) & 0x1ffffff;
+  h.v[2] = ((w[1] >> 19) | (w[2] << 13)) & 0x3ffffff;
+  h.v[3] = ((w[2] >> 13) | (w[3] << 19)) & 0x1ffffff;
+  h.v[4] = (w[3] >> 6) & 0x3ffffff;
+  h.v[5] = w[4] & 0x1ffffff;
+  h.v[6] = ((w[4] >> 25) | (w[5] << 7)) & 0x3ffffff;
+  h.v[7] = ((w[5] >> 19) | (w[6] << 13)) & 0x1ffffff;
+  h.v[8] = ((w[6] >> 12) | (w[7] << 20)) & 0x3ffffff;
+  h.v[9] = w[7] >> 6;  // 26 bits
+  OURO_TRK(for (int i = 0; i < 9; i++) h.b[i] = limb_mask(i); h.b[9] = (1u << 26) - 1;)
+  return h;
+}
+OURO_FI void st_cached_packed(Slot p, const ge_cached& c) {
+  const fe* s[4] = {&c.YplusX, &c.YminusX, &c.Z2, &c.T2d};
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    uint32_t w[8];
+    fe_pack256(w, *s[k]);
+    stg4(p.chunk(2 * k), make_int4((int)w[0], (int)w[1], (int)w[2], (int)w[3]));
+    stg4(p.chunk(2 * k + 1), make_int4((int)w[4], (int)w[5], (int)w[6], (int)w[7]));
+  }
+}
+OURO_FI ge_cached ld_cached_packed(Slot p) {
+  fe f[4];
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    const int4 a = ldg4(p.chunk(2 * k)), b = ldg4(p.chunk(2 * k + 1));
+    const uint32_t w[8] = {(uint32_t)a.x, (uint32_t)a.y, (uint32_t)a.z, (uint32_t)a.w,
+                           (uint32_t)b.x, (uint32_t)b.y, (uint32_t)b.z, (uint32_t)b.w};
+    f[k] = fe_unpack256(w);
+  }
+  return ge_cached{f[0], f[1], f[2], f[3]};
+}
+// a lane-mode table entry (packed or not) / a lane-quad one (never packed)
+OURO_FI void st_entry(Slot p, const ge_cached& c, bool quad) {
+  if (OURO_TAB_PACK && !quad)
+    st_cached_packed(p, c);
+  else
+    st_cached(p, c);
+}
 OURO_FI ge_niels ld_niels(const int32_t* p) {
   int32_t w[32];
 #pragma unroll
@@ -202,16 +280,17 @@ struct SlotTail {
 // [1..8]P in cached form into a per-lane table
 // (quad: the lane-quad formulas of ge25519.h, latency mode)
 OURO_HD inline void build_table(Slot tab, const ge_p3& P, bool quad = false) {
+  const int ec = (quad ? kCachedWords : kLaneEntryWords) / 4;  // chunks per entry
   ge_cached c1 = ge_p3_to_cached(P);
-  st_cached(tab, c1);
+  st_entry(tab, c1, quad);
   ge_p3 Pk = quad ? ge_p1p1_to_p3_quad(ge_p2_dbl_quad(ge_p3_to_p2(P)))
                   : ge_p1p1_to_p3(ge_p3_dbl(P));
-  st_cached(tab + kCachedWords, ge_p3_to_cached(Pk));
+  st_entry(tab.chunks(ec), ge_p3_to_cached(Pk), quad);
 #pragma unroll 1
   for (int k = 2; k < kTabEntries; k++) {
     Pk = quad ? ge_p1p1_to_p3_quad(ge_add_cached_quad(Pk, c1, false))
               : ge_p1p1_to_p3(ge_add_cached(Pk, c1, false));
-    st_cached(tab.chunks(k * (kCachedWords / 4)), ge_p3_to_cached(Pk));
+    st_entry(tab.chunks(k * ec), ge_p3_to_cached(Pk), quad);
   }
 }
 
@@ -297,6 +376,7 @@ OURO_FI void dsm_body(Slot lane, const int32_t* btab, uint32_t cfg) {
   const bool useB = (cfg >> 16) & 1;
   const Slot tab1 = lane.chunks((int)((cfg >> 20) & 3) * (kTabWords / 4));
   const Slot tab2 = lane.chunks((int)((cfg >> 22) & 3) * (kTabWords / 4));
+  constexpr int kE = kQuad ? kCachedWords : kLaneEntryWords;  // words per table entry
   uint32_t a1[8], a2[8], b[8];
   ld_words8(a1, lane + kSlotA1);
   ld_words8(a2, lane + kSlotA2);
@@ -345,14 +425,14 @@ OURO_FI void dsm_body(Slot lane, const int32_t* btab, uint32_t cfg) {
     // touch this window's per-lane table entries now, so that the loads
     // after the four doublings hit L2 instead of waiting on HBM
     const int i1 = (d1 < 0 ? -d1 : d1) - 1, i2 = (d2 < 0 ? -d2 : d2) - 1;
-    const Slot e1 = tab1.chunks((i1 > 0 ? i1 : 0) * (kCachedWords / 4));
-    const Slot e2 = tab2.chunks((i2 > 0 ? i2 : 0) * (kCachedWords / 4));
+    const Slot e1 = tab1.chunks((i1 > 0 ? i1 : 0) * (kE / 4));
+    const Slot e2 = tab2.chunks((i2 > 0 ? i2 : 0) * (kE / 4));
     uint32_t pf1 = 0, pf2 = 0, pf3 = 0, pf4 = 0, pf5 = 0, pf6 = 0;
     const int i3 = (d3 < 0 ? -d3 : d3) - 1, i4 = (d4 < 0 ? -d4 : d4) - 1;
 #define OURO_TOUCH_ENTRIES()                                                                   \
   do {                                                                                         \
-    if (act1) { pf1 = (uint32_t)ldg1(e1.word(0)); pf2 = (uint32_t)ldg1(e1.word(kCachedWords - 1)); } \
-    if (act2) { pf3 = (uint32_t)ldg1(e2.word(0)); pf4 = (uint32_t)ldg1(e2.word(kCachedWords - 1)); } \
+    if (act1) { pf1 = (uint32_t)ldg1(e1.word(0)); if (kE > 32) pf2 = (uint32_t)ldg1(e1.word(kE - 1)); } \
+    if (act2) { pf3 = (uint32_t)ldg1(e2.word(0)); if (kE > 32) pf4 = (uint32_t)ldg1(e2.word(kE - 1)); } \
     if (actB) { /* the B entries (one 128-B line each) come from the 8 MiB tables */          \
       pf5 = (uint32_t)ldg1(btab + (size_t)(i3 > 0 ? i3 : 0) * kNielsWords);                    \
       pf6 = (uint32_t)ldg1(btab + ((size_t)kBTabEntries + (i4 > 0 ? i4 : 0)) * kNielsWords);   \
@@ -409,7 +489,8 @@ OURO_FI void dsm_body(Slot lane, const int32_t* btab, uint32_t cfg) {
 #endif
       ge_cached q;
       if (src < 2) {
-        q = ld_cached((src == 0 ? tab1 : tab2).chunks(idx * (kCachedWords / 4)));
+        const Slot e = (src == 0 ? tab1 : tab2).chunks(idx * (kE / 4));
+        q = kE == kPackedWords ? ld_cached_packed(e) : ld_cached(e);
       } else {
         const size_t base = src == 3 ? kBTabEntries : 0;
         ge_niels nq = ld_niels(btab + (base + idx) * kNielsWords);
