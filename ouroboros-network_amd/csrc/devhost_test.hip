@@ -130,6 +130,15 @@ void dh_fe_limbs_tobytes(uint8_t* out, const uint32_t* limbs) {
                  limbs[8], limbs[9]);
   fe_to_bytes(out, f);
 }
+// a per-lane table coordinate's 256-bit packing (verify.h fe_pack256, limbs
+// < 2^28 in) and the limbs its unpacking yields
+void dh_fe_pack256(uint32_t* words8, uint32_t* limbs_out, const uint32_t* limbs) {
+  fe f = fe_make(limbs[0], limbs[1], limbs[2], limbs[3], limbs[4], limbs[5], limbs[6], limbs[7],
+                 limbs[8], limbs[9]);
+  fe_pack256(words8, f);
+  const fe g = fe_unpack256(words8);
+  for (int i = 0; i < 10; i++) limbs_out[i] = g.v[i];
+}
 unsigned long long dh_untracked_loads(void) {
 #if defined(OURO_COUNT_OPS)
   return g_untracked_loads;

@@ -96,6 +96,31 @@ def test_tobytes_canonicalises_unreduced_limbs(dh):
         assert dec(out.raw) == want
 
 
+def test_table_entry_packing(dh):
+    """verify.h fe_pack256 / fe_unpack256 (the per-lane table entries, one
+    128-B line each): every limb vector the tables store (limbs < 2^28) packs
+    to 256 bits congruent to it mod p, and unpacks to limbs within their
+    widths (limb 9 within 26 bits) whose value is exactly the packed word."""
+    rng = np.random.default_rng(11)
+    E = [0, 26, 51, 77, 102, 128, 153, 179, 204, 230]
+    words = (ctypes.c_uint32 * 8)()
+    back = (ctypes.c_uint32 * 10)()
+    cases = [[(1 << 28) - 1] * 10, [0] * 10, [(1 << 26) - 1, (1 << 25) - 1] * 5,
+             [1 << 26, 1 << 25] * 5, [(1 << 26) - 19] + [(1 << 25) - 1, (1 << 26) - 1] * 4 + [(1 << 25) - 1]]
+    for _ in range(2000):
+        top = int(rng.choice([1 << 25, 1 << 26, 1 << 27, 1 << 28]))
+        cases.append([int(rng.integers(0, top)) for _ in range(10)])
+    for limbs in cases:
+        dh.dh_fe_pack256(words, back, (ctypes.c_uint32 * 10)(*limbs))
+        w = sum(int(x) << (32 * i) for i, x in enumerate(words))
+        x = sum(l << E[i] for i, l in enumerate(limbs))
+        assert w % P == x % P
+        out = list(back)
+        assert all(out[i] < (1 << (26 if i % 2 == 0 else 25)) for i in range(9))
+        assert out[9] < (1 << 26)
+        assert sum(l << E[i] for i, l in enumerate(out)) == w
+
+
 def test_scalar_reduce(dh):
     rng = np.random.default_rng(2)
     out = ctypes.create_string_buffer(32)
