@@ -587,7 +587,7 @@ def latency_leg(hdr, batch: int, iters: int, cpu_threads: int, cpu_iters: int, n
            "iters": iters, **_pcts(lat),
            "headers_per_s_at_p50": round(batch / (np.percentile(lat, 50)), 1),
            "in_flight_4_plans_headers_per_s": round(batch * (4 * rounds + 4) / inflight_s, 1),
-           "all_valid": bool((out[0] == HDR_ALL_OK).all()), "gpu_equals_cpu": same,
+           "all_valid": bool(((out[0] & HDR_ALL_OK) == HDR_ALL_OK).all()), "gpu_equals_cpu": same,
            "cpu_1core": {"p50_ms": ms(c1, 50), "p99_ms": ms(c1, 99), "iters": cpu_iters},
            "cpu_ncores": {"cores": cpu_threads, "p50_ms": ms(cn, 50), "p99_ms": ms(cn, 99),
                           "iters": cpu_iters}}
@@ -807,7 +807,7 @@ def raw_leg(n: int, npools: int, device, threads: int, chunk: int = 0, reps: int
 
     run_host()  # warm: device buffers, pinned staging, arena pages
     best = min(_timed(run_host) for _ in range(reps))
-    ok = bool((status == 0).all() and (verdict == 0x3F).all())
+    ok = bool((status == 0).all() and ((verdict & 0x3F) == 0x3F).all())
     pk_t = []
     for _ in range(reps):
         t0 = time.perf_counter()
@@ -844,10 +844,11 @@ def byron_leg(n: int, threads: int, reps: int = 3):
     off = np.zeros(n, np.uint64)
     off[1:] = np.cumsum(ln[:-1], dtype=np.uint64)
     arg = (np.frombuffer(b"".join(raws), np.uint8), off, ln)
-    B.pack_byron_cbor(arg, nthreads=threads)  # warm
-    tp = min(_timed(lambda: B.pack_byron_cbor(arg, nthreads=threads)) for _ in range(reps))
-    v, st = B.verify_byron_cbor(arg)  # warm
-    tv = min(_timed(lambda: B.verify_byron_cbor(arg)) for _ in range(reps))
+    magic = B.HEADER_MAGIC  # the golden wire forms carry the test network's own magic
+    B.pack_byron_cbor(arg, magic, nthreads=threads)  # warm
+    tp = min(_timed(lambda: B.pack_byron_cbor(arg, magic, nthreads=threads)) for _ in range(reps))
+    v, st = B.verify_byron_cbor(arg, magic)  # warm
+    tv = min(_timed(lambda: B.verify_byron_cbor(arg, magic)) for _ in range(reps))
     m = min(n, 4096)
     t0 = time.perf_counter()
     for r in raws[:m]:
@@ -1079,7 +1080,7 @@ def main():
         step(w)
     torch.cuda.synchronize()
     # correctness gate: every synthetic header must verify
-    all_ok = bool((hdr.verdict == 15).all().item())
+    all_ok = bool(((hdr.verdict & 15) == 15).all().item())  # masks: ouro_verify.h
 
     if world > 1:
         dist.barrier()

@@ -11,8 +11,18 @@
  * Semantics shared by every call:
  *   - Return 0 = valid / OURO_OK, -1 = invalid (single-item calls), or a
  *     negative OURO_E* status for a call that could not run.  A device or
- *     runtime failure NEVER reports "valid": batch verdicts are then left
- *     untouched and the call returns OURO_EDEVICE.
+ *     runtime failure NEVER reports "valid" without a verification: a
+ *     host-buffer call (single item, ouro_*_batch, header batches, plans)
+ *     whose device run fails is recomputed on the library's host path -- the
+ *     same lane routines the kernels run, compiled for the CPU -- and returns
+ *     OURO_OK with those verdicts (ouro_last_error then says what failed);
+ *     with OURO_ON_DEVICE_ERROR=fail in the environment it returns
+ *     OURO_EDEVICE instead and leaves the verdicts untouched.  Device-pointer
+ *     calls (*_batch_device) cannot be recomputed on the host and return
+ *     OURO_EDEVICE.
+ *   - Verdict bytes carry several bits: test them with masks, e.g.
+ *     (v & OURO_HDR_ALL_OK) == OURO_HDR_ALL_OK, never with equality (a valid
+ *     header may also carry OURO_HDR_*_CLAIM_OK or OURO_HDR_*_S_UNREDUCED).
  *   - The caller owns every buffer; nothing is retained after return.
  *   - All calls are thread-safe and reentrant: each calling thread gets its own
  *     HIP stream and staging buffers on the current device, borrowed from a
@@ -55,6 +65,9 @@ extern "C" {
 #define OURO_HDR_LEADER_CLAIM_OK 0x20u
 #define OURO_HDR_ALL_OK 0x0fu    /* ref2020: every proof / signature valid    */
 #define OURO_HDR_STRICT_OK 0x3fu /* strict: and both claimed outputs correct  */
+/* Test verdicts with MASKS, never equality: valid(v) = (v & OURO_HDR_ALL_OK)
+ * == OURO_HDR_ALL_OK, strict(v) = (v & OURO_HDR_STRICT_OK) == OURO_HDR_STRICT_OK
+ * (a valid header may carry further bits, e.g. OURO_HDR_*_S_UNREDUCED). */
 /* The VRF proof's s is NOT below L (set from the proof bytes alone, whatever
  * the verdict).  Draft-03 leaves s's range to the implementation; this
  * library, like the libsodium fork as SURVEY.md App. B.3 recalls it, reduces
@@ -110,15 +123,15 @@ int ouro_vrf03_verify(unsigned char *output, const unsigned char *pk,
  * Shelley/Ledger/TPraos.hs:40).  Does not verify the proof. */
 int ouro_vrf03_proof_to_hash(unsigned char *output, const unsigned char *proof);
 
-/* Routing of single items.  Each single-item call above is ONE GPU round
- * trip (H2D, one wave, D2H): about 220 us for Ed25519 and 420 us for a VRF
- * proof on MI355X, against about 32 us for libsodium on one host core
- * (bench.py "single_item").  A caller with one item at a time -- the
- * reference's per-header OCERT / OVERLAY calls as they are today -- should
- * keep libsodium / the cardano-crypto-praos fork for n = 1; windows of
- * headers (ChainSync's 64-300, ouro_tpraos_plan_*) and bulk batches
- * (ouro_*_batch) are what the GPU path is for.  The names the reference's
- * Haskell binds are therefore NOT exported by this library; two OPT-IN link
+/* Routing of single items.  The single-item calls above run on the library's
+ * HOST path (the kernels' own lane routines compiled for the CPU; round 4):
+ * one GPU round trip (H2D, one wave, D2H) costs about 220 us for Ed25519 and
+ * 420 us for a VRF proof on MI355X, the host path about 1.5x libsodium's
+ * ~32 us per Ed25519 on one core (bench.py "single_item" has both routes).
+ * OURO_SINGLE_ITEM=gpu in the environment sends them to the device instead.
+ * Windows of headers (ChainSync's 64-300, ouro_tpraos_plan_*) and bulk
+ * batches (ouro_*_batch) are what the GPU path is for.  The names the
+ * reference's Haskell binds are NOT exported by this library; two OPT-IN link
  * shims provide them, with these exact signatures, for a maintainer who
  * wants the drop-in by link order instead of a Haskell edit:
  *   lib/libouro_vrf_shim.so (PraosVRF's foreign imports; the version-less
@@ -397,13 +410,44 @@ int ouro_tpraos_plan_submit(ouro_tpraos_plan *plan, const ouro_tpraos_batch *b);
 int ouro_tpraos_plan_wait(ouro_tpraos_plan *plan, uint8_t *verdict, uint8_t *beta_eta,
                           uint8_t *beta_leader);
 
-/* A plan's latency kernel counts each header's finished checks in per-header
- * arrival counters tagged with the launch's generation (a new one per
- * submit), so a counter an earlier launch left mid-count (one that never
- * completed) is never counted again.  TEST HOOK: leaves every counter of the
- * plan as its last launch would have left them had it been cut off one
- * arrival short of each finish (tests/test_gpu_claims.py). */
-int ouro_tpraos_plan_debug_poison(ouro_tpraos_plan *plan);
+/* (A plan's latency kernel counts each header's finished checks in
+ * per-header arrival counters tagged with the launch's generation -- a new
+ * one per submit -- so a counter an earlier launch left mid-count, one that
+ * never completed, is never counted again; tests/test_gpu_claims.py checks it
+ * through a test hook reached only from the environment.) */
+
+/* ------------------------------------------------------- host path ----- */
+/* The same batches on the library's host path, explicitly: the kernels' own
+ * lane routines compiled for the CPU (csrc/host_path.hip), the batch split
+ * over host threads (OURO_HOST_THREADS caps them; default the CPUs the
+ * process may run on, at most 64).  Same arguments, verdicts and outputs as
+ * the calls without _host; no device is touched.  For nodes without a GPU,
+ * for callers that keep small batches on the CPU, and the path the device
+ * calls recompute on after a device error. */
+int ouro_ed25519_verify_batch_host(size_t n, const uint8_t *pk, const uint8_t *sig,
+                                   const uint8_t *msg, const uint64_t *msg_off,
+                                   const uint32_t *msg_len, uint8_t *verdict);
+int ouro_byron_ed25519_verify_batch_host(size_t n, const uint8_t *pk, const uint8_t *sig,
+                                         const uint8_t *msg, const uint64_t *msg_off,
+                                         const uint32_t *msg_len, uint8_t *verdict);
+int ouro_vrf03_verify_batch_host(size_t n, const uint8_t *pk, const uint8_t *proof,
+                                 const uint8_t *alpha, const uint64_t *alpha_off,
+                                 const uint32_t *alpha_len, uint8_t *beta, uint8_t *verdict,
+                                 uint32_t flags);
+int ouro_sum6kes_verify_batch_host(size_t n, const uint8_t *vk, const uint32_t *t,
+                                   const uint8_t *msg, const uint64_t *msg_off,
+                                   const uint32_t *msg_len, const uint8_t *sig, uint8_t *verdict);
+int ouro_tpraos_verify_batch_host(const ouro_tpraos_batch *b, uint8_t *verdict,
+                                  uint8_t *beta_eta, uint8_t *beta_leader);
+int ouro_leader_check_batch_host(size_t n, const uint8_t *beta, const uint64_t *sigma_num,
+                                 const uint64_t *sigma_den, int64_t act_log_hi,
+                                 uint64_t act_log_lo, int f_is_one, uint8_t *verdict);
+
+/* Diagnostics: items the host path has verified since the process started --
+ * single items routed there, and host-buffer batches recomputed there after a
+ * device error.  Host-only. */
+int ouro_debug_host_path(unsigned long long *single_items,
+                         unsigned long long *recomputed_batches);
 
 /* Diagnostics: per-thread contexts (stream, scratch, staging) are pooled per
  * device; a thread borrows one on its first call and returns it when it

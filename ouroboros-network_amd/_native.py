@@ -103,7 +103,14 @@ SIGNATURES = {
     "ouro_vrf03_verify_batch_flags": (_I, [_SZ, _P, _P, _P, _P, _P, _P, _P, ctypes.c_uint32]),
     "ouro_vrf03_verify_batch_device_flags": (_I, [_P, _SZ, _P, _P, _P, _P, _P, _P, _P,
                                                   ctypes.c_uint32]),
-    "ouro_tpraos_plan_debug_poison": (_I, [_P]),
+    "ouro_debug_host_path": (_I, [_P, _P]),
+    "ouro_ed25519_verify_batch_host": (_I, [_SZ, _P, _P, _P, _P, _P, _P]),
+    "ouro_byron_ed25519_verify_batch_host": (_I, [_SZ, _P, _P, _P, _P, _P, _P]),
+    "ouro_vrf03_verify_batch_host": (_I, [_SZ, _P, _P, _P, _P, _P, _P, _P, ctypes.c_uint32]),
+    "ouro_sum6kes_verify_batch_host": (_I, [_SZ, _P, _P, _P, _P, _P, _P, _P]),
+    "ouro_tpraos_verify_batch_host": (_I, [ctypes.POINTER(TPraosBatch), _P, _P, _P]),
+    "ouro_leader_check_batch_host": (_I, [_SZ, _P, _P, _P, ctypes.c_int64, ctypes.c_uint64, _I,
+                                          _P]),
     "ouro_debug_contexts": (_I, [_I, _P, _P]),
     "ouro_debug_lat_stamps": (_I, [_P]),
     "ouro_sum6kes_verify_batch": (_I, [_SZ, _P, _P, _P, _P, _P, _P, _P]),

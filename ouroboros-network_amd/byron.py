@@ -22,7 +22,7 @@ the Byron storage integrity check,
 from __future__ import annotations
 
 from dataclasses import dataclass
-from typing import List, Optional, Sequence, Tuple
+from typing import List, Optional, Sequence, Tuple, Union
 
 import numpy as np
 
@@ -77,9 +77,10 @@ class ByronDSIGN:
     verify_signed_dsign = verify_dsign
 
     @staticmethod
-    def verify_batch(pks, msgs, sigs) -> np.ndarray:
+    def verify_batch(pks, msgs, sigs, host: bool = False) -> np.ndarray:
         """Batch verify of complete messages (tag included) under 32-byte keys
-        (XPub[0:32]) or 64-byte XPubs; returns a bool array."""
+        (XPub[0:32]) or 64-byte XPubs; returns a bool array.  host=True: the
+        library's host path (ouro_byron_ed25519_verify_batch_host)."""
         if isinstance(pks, np.ndarray) and pks.ndim == 2 and pks.shape[1] == SIZE_VERKEY:
             pks = pks[:, :32]
         elif not isinstance(pks, np.ndarray):
@@ -92,9 +93,10 @@ class ByronDSIGN:
             raise ValueError("pk, msg and sig batches differ in length")
         out = np.zeros(n, dtype=np.uint8)
         if n:
-            rc = _native.load().ouro_byron_ed25519_verify_batch(
-                n, ptr(pk), ptr(sg), ptr(buf), ptr(off), ptr(ln), ptr(out))
-            _native.check(rc, "ouro_byron_ed25519_verify_batch")
+            name = "ouro_byron_ed25519_verify_batch" + ("_host" if host else "")
+            rc = getattr(_native.load(), name)(n, ptr(pk), ptr(sg), ptr(buf), ptr(off), ptr(ln),
+                                               ptr(out))
+            _native.check(rc, name)
         return out.astype(bool)
 
 
@@ -131,12 +133,13 @@ class ByronHeader:
     sig: bytes            # 64-byte block signature
     slot_raw: bytes
 
-    def message(self, protocol_magic: Optional[int] = None) -> bytes:
+    def message(self, protocol_magic: Union[int, str]) -> bytes:
         """signTag magic (SignBlock genKey) || signed bytes; magic = the node's
         configured ProtocolMagicId (mkByronContextDSIGN,
         ouroboros-consensus-byron/src/Ouroboros/Consensus/Byron/Ledger/PBFT.hs:43-44),
-        or the header's own field when None."""
-        m = self.magic if protocol_magic is None else protocol_magic
+        or, only when asked for by name (protocol_magic=HEADER_MAGIC), the
+        header's own field -- which the peer chose."""
+        m = self.magic if _magic_arg(protocol_magic) < 0 else protocol_magic
         return sign_tag_block(m, self.issuer_xpub) + self.to_sign
 
 
@@ -303,20 +306,35 @@ def _raw_arg(raw_headers):
     return np.frombuffer(b"".join(items) or b"\0", np.uint8), off, ln
 
 
-def _magic_arg(protocol_magic: Optional[int]) -> int:
+# protocol_magic = HEADER_MAGIC: sign with each header's own protocolMagic
+# field instead of the node's configured ProtocolMagicId.  The reference
+# always uses the configured one (Byron/Ledger/PBFT.hs:43-45 mkByronContextDSIGN,
+# DSIGN.hs:111), so a header signed for another network fails there; the
+# header's field is the peer's choice, hence an explicit opt-in, never a
+# default.
+HEADER_MAGIC = "header"
+
+
+def _magic_arg(protocol_magic: Union[int, str]) -> int:
     if protocol_magic is None:
+        raise ValueError("protocol_magic is required: the node's ProtocolMagicId "
+                         "(or HEADER_MAGIC to use each header's own field)")
+    if isinstance(protocol_magic, str):
+        if protocol_magic != HEADER_MAGIC:
+            raise ValueError(f"protocol_magic: a Word32 or {HEADER_MAGIC!r}")
         return -1
     if not 0 <= protocol_magic <= WORD32_MAX:
         raise ValueError("protocol_magic: a Word32")
     return int(protocol_magic)
 
 
-def pack_byron_cbor(raw_headers, protocol_magic: Optional[int] = None,
+def pack_byron_cbor(raw_headers, protocol_magic: Union[int, str],
                     nthreads: int = 0) -> PackedByron:
     """Raw Byron headers -> keys, signatures and signed messages through the C
     slicer (include/ouro_verify.h ouro_byron_pack_cbor, csrc/pack.cpp).
     raw_headers: a sequence of bytes, or (buf, off, len).  protocol_magic:
-    the node's ProtocolMagicId for the sign tag (None: each header's own)."""
+    the node's ProtocolMagicId for the sign tag (required; HEADER_MAGIC:
+    each header's own field)."""
     import ctypes
 
     from .header import _pack_lib
@@ -352,7 +370,7 @@ def pack_byron_cbor(raw_headers, protocol_magic: Optional[int] = None,
         status=status[:n], _keep=(arena, buf))
 
 
-def verify_byron_cbor(raw_headers, protocol_magic: Optional[int] = None):
+def verify_byron_cbor(raw_headers, protocol_magic: Union[int, str]):
     """Raw Byron headers -> (verdict bool array, status array) in one call
     (ouro_byron_verify_cbor): a regular header is valid when its block
     signature verifies, an epoch-boundary header always (PBFT.hs:327-328)."""
@@ -369,7 +387,7 @@ def verify_byron_cbor(raw_headers, protocol_magic: Optional[int] = None):
 
 
 def verify_byron_headers(headers: Sequence[ByronHeader],
-                         protocol_magic: Optional[int] = None) -> np.ndarray:
+                         protocol_magic: Union[int, str]) -> np.ndarray:
     """PBFT block-signature check of a batch of parsed Byron headers
     (PBFT.hs:332-337): one gfx950 launch, bool per header.  Raw headers go
     through verify_byron_cbor instead (the C slicer, no per-header Python)."""

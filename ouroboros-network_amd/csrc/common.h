@@ -3,14 +3,21 @@
 // Every lane-level routine is `__host__ __device__` so the exact code the
 // kernels run can also be compiled for the host by hipcc and exercised in the
 // CPU test suite (tests/test_devcode_host.py) without a GPU.  The product
-// library only ever runs these routines inside kernels.
+// library runs them inside kernels and, since round 4, on the host for single
+// items and as the recompute path after a device error (host_path.hip).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
 #define OURO_HD __host__ __device__
 #define OURO_FI __host__ __device__ __forceinline__
-#define OURO_NI __host__ __device__ __noinline__
+// Out-of-line routines have external linkage, one definition per library
+// (kernels.hip); the host path's translation unit (host_path.hip) defines
+// OURO_NI_LINKAGE static to keep its own host copies apart.
+#ifndef OURO_NI_LINKAGE
+#define OURO_NI_LINKAGE
+#endif
+#define OURO_NI __host__ __device__ __noinline__ OURO_NI_LINKAGE
 
 namespace ouro {
 
@@ -56,16 +63,29 @@ OURO_FI void stg2(void* p, int2 v) { *(OURO_AS1 ouro_v2i*)p = ouro_v2i{v.x, v.y}
 OURO_FI void stg1(void* p, int32_t v) { *(OURO_AS1 int32_t*)p = v; }
 OURO_FI void stg8(void* p, uint64_t v) { *(OURO_AS1 uint64_t*)p = v; }
 #else
-OURO_FI int4 ldg4(const void* p) { return *static_cast<const int4*>(p); }
-OURO_FI int2 ldg2(const void* p) { return *static_cast<const int2*>(p); }
-OURO_FI int32_t ldg1(const void* p) { return *static_cast<const int32_t*>(p); }
-OURO_FI uint64_t ldg8(const void* p) { return *static_cast<const uint64_t*>(p); }
+// Host: byte-wise copies, so the host path (host_path.hip) reads the caller's
+// buffers at any alignment (the kernels' inputs are 16-B aligned device
+// buffers; a host caller's ByteStrings need not be).  Same code at -O2.
+template <class T>
+OURO_FI T ldh(const void* p) {
+  T v;
+  __builtin_memcpy(&v, p, sizeof(T));
+  return v;
+}
+template <class T>
+OURO_FI void sth(void* p, const T& v) {
+  __builtin_memcpy(p, &v, sizeof(T));
+}
+OURO_FI int4 ldg4(const void* p) { return ldh<int4>(p); }
+OURO_FI int2 ldg2(const void* p) { return ldh<int2>(p); }
+OURO_FI int32_t ldg1(const void* p) { return ldh<int32_t>(p); }
+OURO_FI uint64_t ldg8(const void* p) { return ldh<uint64_t>(p); }
 OURO_FI uint32_t ldg_u8(const void* p) { return *static_cast<const uint8_t*>(p); }
-OURO_FI uint32_t ldg_u16(const void* p) { return *static_cast<const uint16_t*>(p); }
-OURO_FI void stg4(void* p, int4 v) { *static_cast<int4*>(p) = v; }
-OURO_FI void stg2(void* p, int2 v) { *static_cast<int2*>(p) = v; }
-OURO_FI void stg1(void* p, int32_t v) { *static_cast<int32_t*>(p) = v; }
-OURO_FI void stg8(void* p, uint64_t v) { *static_cast<uint64_t*>(p) = v; }
+OURO_FI uint32_t ldg_u16(const void* p) { return ldh<uint16_t>(p); }
+OURO_FI void stg4(void* p, int4 v) { sth(p, v); }
+OURO_FI void stg2(void* p, int2 v) { sth(p, v); }
+OURO_FI void stg1(void* p, int32_t v) { sth(p, v); }
+OURO_FI void stg8(void* p, uint64_t v) { sth(p, v); }
 #endif
 
 }  // namespace ouro

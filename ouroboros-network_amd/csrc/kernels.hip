@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <condition_variable>
 #include <cstdio>
 #include <cstring>
@@ -19,6 +20,7 @@
 
 #include "../../include/ouro_verify.h"
 #include "cbor.h"
+#include "host_path.h"
 #include "launch.h"
 #include "leader.h"
 #include "tpraos.h"
@@ -290,12 +292,21 @@ const void* kernel_ptr(int id) {
 }
 
 int current_device(int* dev) {
+  // no usable device at all is OURO_ENODEV (not a device error: nothing is
+  // recomputed on the host path behind the caller's back)
+  auto nodev = [](hipError_t e) {
+    return e == hipErrorNoDevice || e == hipErrorInvalidDevice || e == hipErrorInsufficientDriver;
+  };
   if (t_device < 0) {
     int d = 0;
-    OURO_HIP(hipGetDevice(&d));
+    const hipError_t e = hipGetDevice(&d);
+    if (nodev(e)) return fail(OURO_ENODEV, std::string("hipGetDevice: ") + hipGetErrorString(e));
+    OURO_HIP(e);
     t_device = d;
   }
-  OURO_HIP(hipSetDevice(t_device));
+  const hipError_t e = hipSetDevice(t_device);
+  if (nodev(e)) return fail(OURO_ENODEV, std::string("hipSetDevice: ") + hipGetErrorString(e));
+  OURO_HIP(e);
   *dev = t_device;
   return OURO_OK;
 }
@@ -314,7 +325,7 @@ int device_state(DeviceState** out) {
     s.cus = prop.multiProcessorCount;
     // niels B tables, then their wave-wide form (latency mode, wide.h)
     std::vector<int32_t> tab(kBTabWords + kBTabWideWords);
-    build_btab(tab.data());
+    memcpy(tab.data(), ouro_host::btab(), sizeof(int32_t) * kBTabWords);  // built once per process
     build_btab_wide(reinterpret_cast<uint16_t*>(tab.data() + kBTabWords), tab.data());
     OURO_HIP(hipMalloc(&s.btab, sizeof(int32_t) * tab.size()));
     OURO_HIP(hipMemcpy(s.btab, tab.data(), sizeof(int32_t) * tab.size(), hipMemcpyHostToDevice));
@@ -473,9 +484,43 @@ int plan(DeviceState* ds, int id, size_t n, hipStream_t stream, int* grid, int32
   return OURO_OK;
 }
 
+// TEST HOOK (tests/test_gpu_host_path.py): with OURO_TEST_DEVICE_ERROR set in
+// the environment every launch reports a device error, so the tests reach the
+// host recompute path on a healthy GPU.  No ABI surface.
+bool injected_device_error() { return getenv("OURO_TEST_DEVICE_ERROR") != nullptr; }
+
 int launch_check() {
   OURO_HIP(hipGetLastError());
+  if (injected_device_error()) return fail(OURO_EDEVICE, "injected device error (OURO_TEST_DEVICE_ERROR)");
   return OURO_OK;
+}
+
+// ---- the host path (host_path.h) -------------------------------------------
+// A host-buffer batch whose device run fails with OURO_EDEVICE is recomputed
+// on the host path (SURVEY.md §5, §8(b) "Errors": never a silent accept, and
+// the caller still gets verdicts); OURO_ON_DEVICE_ERROR=fail returns the error
+// instead.  Device-pointer calls (*_batch_device) cannot: their buffers are
+// device memory, so they return the error.
+std::atomic<unsigned long long> g_host_single{0}, g_host_recompute{0};
+bool recompute_on_error() {
+  const char* e = getenv("OURO_ON_DEVICE_ERROR");
+  return !(e && strcmp(e, "fail") == 0);
+}
+template <class F>
+int or_host(int rc, F&& recompute) {
+  if (rc != OURO_EDEVICE || !recompute_on_error()) return rc;
+  g_host_recompute++;
+  const std::string why = t_last_error;
+  const int r = recompute();
+  t_last_error = "recomputed on the host path after: " + why;
+  return r;
+}
+// Single items run on the host path (one GPU round trip is ~220-420 us, the
+// host path ~1.5x libsodium); OURO_SINGLE_ITEM=gpu sends them to the device
+// (A/B, bench.py single_item).
+bool single_on_gpu() {
+  const char* e = getenv("OURO_SINGLE_ITEM");
+  return e && strcmp(e, "gpu") == 0;
 }
 
 // Small batches (n <= OURO_WIDE_SMALL_MAX, default 2048; 0 = never) run one
@@ -811,13 +856,17 @@ extern "C" {
 
 int ouro_ed25519_verify_batch(size_t n, const uint8_t* pk, const uint8_t* sig, const uint8_t* msg,
                               const uint64_t* msg_off, const uint32_t* msg_len, uint8_t* verdict) {
-  return ed_batch_host(n, pk, sig, msg, msg_off, msg_len, verdict, 0);
+  return or_host(ed_batch_host(n, pk, sig, msg, msg_off, msg_len, verdict, 0), [&] {
+    return ouro_host::ed_batch(n, pk, sig, msg, msg_off, msg_len, verdict, 0);
+  });
 }
 
 int ouro_byron_ed25519_verify_batch(size_t n, const uint8_t* pk, const uint8_t* sig,
                                     const uint8_t* msg, const uint64_t* msg_off,
                                     const uint32_t* msg_len, uint8_t* verdict) {
-  return ed_batch_host(n, pk, sig, msg, msg_off, msg_len, verdict, 1);
+  return or_host(ed_batch_host(n, pk, sig, msg, msg_off, msg_len, verdict, 1), [&] {
+    return ouro_host::ed_batch(n, pk, sig, msg, msg_off, msg_len, verdict, 1);
+  });
 }
 
 int ouro_byron_verify_cbor(const uint8_t* raw, size_t raw_bytes, const uint64_t* off,
@@ -846,10 +895,12 @@ int ouro_vrf03_verify_batch(size_t n, const uint8_t* pk, const uint8_t* proof, c
   return ouro_vrf03_verify_batch_flags(n, pk, proof, alpha, alpha_off, alpha_len, beta, verdict, 0);
 }
 
-int ouro_vrf03_verify_batch_flags(size_t n, const uint8_t* pk, const uint8_t* proof,
-                                  const uint8_t* alpha, const uint64_t* alpha_off,
-                                  const uint32_t* alpha_len, uint8_t* beta, uint8_t* verdict,
-                                  uint32_t flags) {
+}  // extern "C"
+
+namespace {
+int vrf_batch_dev(size_t n, const uint8_t* pk, const uint8_t* proof, const uint8_t* alpha,
+                  const uint64_t* alpha_off, const uint32_t* alpha_len, uint8_t* beta,
+                  uint8_t* verdict, uint32_t flags) {
   if (n == 0) return OURO_OK;
   if (flags & ~OURO_VRF_STRICT_S) return fail(OURO_EINVAL, "unknown VRF flags");
   if (!pk || !proof || !alpha_off || !alpha_len || !verdict) return fail(OURO_EINVAL, "null argument");
@@ -878,9 +929,9 @@ int ouro_vrf03_verify_batch_flags(size_t n, const uint8_t* pk, const uint8_t* pr
   return OURO_OK;
 }
 
-int ouro_sum6kes_verify_batch(size_t n, const uint8_t* vk, const uint32_t* t, const uint8_t* msg,
-                              const uint64_t* msg_off, const uint32_t* msg_len, const uint8_t* sig,
-                              uint8_t* verdict) {
+int kes_batch_dev(size_t n, const uint8_t* vk, const uint32_t* t, const uint8_t* msg,
+                  const uint64_t* msg_off, const uint32_t* msg_len, const uint8_t* sig,
+                  uint8_t* verdict) {
   if (n == 0) return OURO_OK;
   if (!vk || !t || !msg_off || !msg_len || !sig || !verdict) return fail(OURO_EINVAL, "null argument");
   hipStream_t st;
@@ -904,6 +955,28 @@ int ouro_sum6kes_verify_batch(size_t n, const uint8_t* vk, const uint32_t* t, co
   if ((rc = finish(st))) return rc;
   memcpy(verdict, tv.data(), n);
   return OURO_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int ouro_vrf03_verify_batch_flags(size_t n, const uint8_t* pk, const uint8_t* proof,
+                                  const uint8_t* alpha, const uint64_t* alpha_off,
+                                  const uint32_t* alpha_len, uint8_t* beta, uint8_t* verdict,
+                                  uint32_t flags) {
+  return or_host(vrf_batch_dev(n, pk, proof, alpha, alpha_off, alpha_len, beta, verdict, flags),
+                 [&] {
+                   return ouro_host::vrf_batch(n, pk, proof, alpha, alpha_off, alpha_len, beta,
+                                               verdict, flags);
+                 });
+}
+
+int ouro_sum6kes_verify_batch(size_t n, const uint8_t* vk, const uint32_t* t, const uint8_t* msg,
+                              const uint64_t* msg_off, const uint32_t* msg_len, const uint8_t* sig,
+                              uint8_t* verdict) {
+  return or_host(kes_batch_dev(n, vk, t, msg, msg_off, msg_len, sig, verdict), [&] {
+    return ouro_host::kes_batch(n, vk, t, msg, msg_off, msg_len, sig, verdict);
+  });
 }
 
 }  // extern "C"
@@ -1052,8 +1125,8 @@ int ouro_tpraos_verify_batch(const ouro_tpraos_batch* b, uint8_t* verdict, uint8
   if ((rc = device_state(&ds))) return rc;
   const HdrOut o{verdict, beta_eta, beta_leader, b->eta_nonce};
   const size_t chunk = host_chunk(ds);
-  if (chunk && b->n > chunk) return hdr_batch_pipelined(b, chunk, o);
-  return hdr_batch_once(b, o, false);
+  rc = chunk && b->n > chunk ? hdr_batch_pipelined(b, chunk, o) : hdr_batch_once(b, o, false);
+  return or_host(rc, [&] { return ouro_host::hdr_batch(b, verdict, beta_eta, beta_leader); });
 }
 
 // ---- latency mode (ChainSync windows) ----
@@ -1065,7 +1138,8 @@ int ouro_tpraos_verify_batch_lowlat(const ouro_tpraos_batch* b, uint8_t* verdict
   if (!verdict) return fail(OURO_EINVAL, "null verdict");
   int rc = check_hdr_batch(b);
   if (rc) return rc;
-  return hdr_batch_once(b, HdrOut{verdict, beta_eta, beta_leader, b->eta_nonce}, true);
+  return or_host(hdr_batch_once(b, HdrOut{verdict, beta_eta, beta_leader, b->eta_nonce}, true),
+                 [&] { return ouro_host::hdr_batch(b, verdict, beta_eta, beta_leader); });
 }
 
 int ouro_nonce_fold(size_t n, const uint8_t* eta_nonce, const uint64_t* slot,
@@ -1108,22 +1182,28 @@ int ouro_leader_check_batch(size_t n, const uint8_t* beta, const uint64_t* sigma
                             int f_is_one, uint8_t* verdict) {
   if (n == 0) return OURO_OK;
   if (!beta || !sigma_num || !sigma_den || !verdict) return fail(OURO_EINVAL, "null argument");
-  hipStream_t st;
-  int rc = thread_stream(&st);
-  if (rc) return rc;
-  Stager sg{st};
-  auto dbeta = sg.up(beta, 64 * n);
-  auto dnum = sg.up(sigma_num, n);
-  auto dden = sg.up(sigma_den, n);
-  auto dver = sg.out<uint8_t>(n);
-  if (sg.rc) return sg.rc;
-  if ((rc = launch_leader(st, n, dbeta, dnum, dden, act_log_hi, act_log_lo, f_is_one, dver)))
-    return rc;
-  std::vector<uint8_t> tv(n);
-  if ((rc = download(st, tv.data(), dver, n))) return rc;
-  if ((rc = finish(st))) return rc;
-  memcpy(verdict, tv.data(), n);
-  return OURO_OK;
+  auto dev = [&]() -> int {
+    hipStream_t st;
+    int rc = thread_stream(&st);
+    if (rc) return rc;
+    Stager sg{st};
+    auto dbeta = sg.up(beta, 64 * n);
+    auto dnum = sg.up(sigma_num, n);
+    auto dden = sg.up(sigma_den, n);
+    auto dver = sg.out<uint8_t>(n);
+    if (sg.rc) return sg.rc;
+    if ((rc = launch_leader(st, n, dbeta, dnum, dden, act_log_hi, act_log_lo, f_is_one, dver)))
+      return rc;
+    std::vector<uint8_t> tv(n);
+    if ((rc = download(st, tv.data(), dver, n))) return rc;
+    if ((rc = finish(st))) return rc;
+    memcpy(verdict, tv.data(), n);
+    return OURO_OK;
+  };
+  return or_host(dev(), [&] {
+    return ouro_host::leader_batch(n, beta, sigma_num, sigma_den, act_log_hi, act_log_lo, f_is_one,
+                                   verdict);
+  });
 }
 
 // ---- single item: a batch of one (ABI-identical to the symbols replaced) ----
@@ -1135,7 +1215,13 @@ int ouro_ed25519_verify(const unsigned char* sig, const unsigned char* m, unsign
   if ((unsigned long long)len != mlen) return fail(OURO_EINVAL, "message too long");
   uint8_t v = 0;
   static const uint8_t empty[1] = {0};
-  int rc = ouro_ed25519_verify_batch(1, pk, sig, mlen ? m : empty, &off, &len, &v);
+  int rc;
+  if (single_on_gpu()) {
+    rc = ouro_ed25519_verify_batch(1, pk, sig, mlen ? m : empty, &off, &len, &v);
+  } else {
+    g_host_single++;
+    rc = ouro_host::ed_batch(1, pk, sig, mlen ? m : empty, &off, &len, &v, 0);
+  }
   if (rc) return rc;
   return v ? OURO_OK : OURO_INVALID;
 }
@@ -1148,7 +1234,13 @@ int ouro_byron_ed25519_verify(const unsigned char* m, size_t mlen, const unsigne
   if ((size_t)len != mlen) return fail(OURO_EINVAL, "message too long");
   uint8_t v = 0;
   static const uint8_t empty[1] = {0};
-  int rc = ouro_byron_ed25519_verify_batch(1, pk, sig, mlen ? m : empty, &off, &len, &v);
+  int rc;
+  if (single_on_gpu()) {
+    rc = ouro_byron_ed25519_verify_batch(1, pk, sig, mlen ? m : empty, &off, &len, &v);
+  } else {
+    g_host_single++;
+    rc = ouro_host::ed_batch(1, pk, sig, mlen ? m : empty, &off, &len, &v, 1);
+  }
   if (rc) return rc;
   return v ? OURO_OK : OURO_INVALID;
 }
@@ -1161,7 +1253,13 @@ int ouro_vrf03_verify(unsigned char* output, const unsigned char* pk, const unsi
   if ((unsigned long long)len != msglen) return fail(OURO_EINVAL, "message too long");
   uint8_t v = 0, beta[64];
   static const uint8_t empty[1] = {0};
-  int rc = ouro_vrf03_verify_batch(1, pk, proof, msglen ? msg : empty, &off, &len, beta, &v);
+  int rc;
+  if (single_on_gpu()) {
+    rc = ouro_vrf03_verify_batch(1, pk, proof, msglen ? msg : empty, &off, &len, beta, &v);
+  } else {
+    g_host_single++;
+    rc = ouro_host::vrf_batch(1, pk, proof, msglen ? msg : empty, &off, &len, beta, &v, 0);
+  }
   if (rc) return rc;
   if (!v) return OURO_INVALID;
   if (output) memcpy(output, beta, 64);  // written only on success, like the original
@@ -1170,6 +1268,10 @@ int ouro_vrf03_verify(unsigned char* output, const unsigned char* pk, const unsi
 
 int ouro_vrf03_proof_to_hash(unsigned char* output, const unsigned char* proof) {
   if (!output || !proof) return OURO_INVALID;
+  if (!single_on_gpu()) {
+    g_host_single++;
+    return ouro_host::proof_to_hash(output, proof);
+  }
   hipStream_t st;
   int rc = thread_stream(&st);
   if (rc) return rc;
@@ -1203,7 +1305,13 @@ int ouro_sum6kes_verify(const unsigned char* vk, unsigned int t, const unsigned 
   uint8_t v = 0;
   const uint32_t tt = t;
   static const uint8_t empty[1] = {0};
-  int rc = ouro_sum6kes_verify_batch(1, vk, &tt, mlen ? m : empty, &off, &len, sig, &v);
+  int rc;
+  if (single_on_gpu()) {
+    rc = ouro_sum6kes_verify_batch(1, vk, &tt, mlen ? m : empty, &off, &len, sig, &v);
+  } else {
+    g_host_single++;
+    rc = ouro_host::kes_batch(1, vk, &tt, mlen ? m : empty, &off, &len, sig, &v);
+  }
   if (rc) return rc;
   return v ? OURO_OK : OURO_INVALID;
 }
@@ -1327,7 +1435,9 @@ struct ouro_tpraos_plan {
   uint32_t gen = 0;             // generation of the last launch (arrive_last), 1..2^28-1
   size_t pending = 0;           // headers of the batch in flight (submit .. wait)
   uint8_t* nonce_dst = nullptr;  // that batch's eta_nonce (written by wait)
+  uint32_t opts = 0;             // that batch's option bits (tpraos.h kOpt*)
   bool inflight = false;
+  bool failed = false;           // its launch failed: wait recomputes it on the host path
 };
 
 namespace {
@@ -1413,6 +1523,66 @@ int plan_build(ouro_tpraos_plan* p) {
   OURO_HIP(hipGraphInstantiate(&p->exec, p->graph, nullptr, nullptr, 0));
   return OURO_OK;
 }
+
+// The batch in the plan's pinned input block as a host batch (the layout
+// ouro_tpraos_plan_submit wrote), for the host recompute after a failed
+// launch; results go straight to the caller's buffers.
+ouro_tpraos_batch plan_host_batch(const ouro_tpraos_plan* p) {
+  const uint8_t* h = p->h_in;
+  ouro_tpraos_batch b{};
+  b.n = p->pending;
+  b.issuer_vk = h + p->off[0];
+  b.vrf_vk = h + p->off[1];
+  b.eta_proof = h + p->off[2];
+  b.leader_proof = h + p->off[3];
+  b.hot_vk = h + p->off[6];
+  b.ocert_counter = reinterpret_cast<const uint64_t*>(h + p->off[7]);
+  b.ocert_kes_period = reinterpret_cast<const uint64_t*>(h + p->off[8]);
+  b.ocert_sigma = h + p->off[9];
+  b.kes_t = reinterpret_cast<const uint32_t*>(h + p->off[10]);
+  b.kes_sig = h + p->off[11];
+  b.body = h + p->off[12];
+  b.body_off = reinterpret_cast<const uint64_t*>(h + p->off[13]);
+  b.body_len = reinterpret_cast<const uint32_t*>(h + p->off[14]);
+  if (p->opts & kOptEtaClaim) b.eta_output = h + p->off[15];
+  if (p->opts & kOptLeaderClaim) b.leader_output = h + p->off[16];
+  if (p->opts & kOptSeeds) {
+    b.slot = reinterpret_cast<const uint64_t*>(h + p->off[17]);
+    if (p->opts & kOptEpochNonce) b.epoch_nonce = h + p->off[18];
+  } else {
+    b.eta_alpha = h + p->off[4];
+    b.leader_alpha = h + p->off[5];
+  }
+  if (p->opts & kOptEtaNonce) b.eta_nonce = p->nonce_dst;
+  return b;
+}
+
+// TEST HOOK (tests/test_gpu_claims.py::test_plan_counters_from_cut_off_launch),
+// reached only through the environment (OURO_TEST_PLAN_POISON, read by
+// ouro_tpraos_plan_submit; no ABI surface): leaves every arrival counter of the
+// plan's records as a launch of its last generation would have left them had
+// it been cut off one arrival short of each finish, so the test can show the
+// next launch ignores them.
+int plan_poison(ouro_tpraos_plan* p) {
+  OURO_HIP(hipSetDevice(p->dev));
+  const size_t words = slot_region_words(p->cap, kLatResWords);
+  std::vector<int32_t> h(words);
+  OURO_HIP(hipMemcpy(h.data(), p->res, sizeof(int32_t) * words, hipMemcpyDeviceToHost));
+  const int32_t tag = (int32_t)((p->gen & 0x0fffffffu) << 4);
+  for (size_t i = 0; i < p->cap; i++) {
+    const Slot r = slot_of(h.data(), i, kLatResWords);
+    *r.word(kLatCtr) = tag | (kLatCores - 1);     // the header's tail one arrival away
+    *r.word(kLatCtr + 1) = tag | 1;                // each V / Gamma pair (or V / V2 /
+    *r.word(kLatCtr + 2) = tag | 1;                // Gamma triple), one in
+    for (int e = 0; e < 2; e++) {
+      *r.word(kLatEd + kEdWords * e + 125) = tag | 1;  // each Ed25519 points / scalars pair
+      for (int k = 17; k <= 19; k++)                // split form: the chain and done counters
+        *r.word(kLatEd + kEdWords * e + k) = tag | 1;
+    }
+  }
+  OURO_HIP(hipMemcpy(p->res, h.data(), sizeof(int32_t) * words, hipMemcpyHostToDevice));
+  return OURO_OK;
+}
 }  // namespace
 
 extern "C" {
@@ -1462,15 +1632,25 @@ int ouro_tpraos_plan_submit(ouro_tpraos_plan* p, const ouro_tpraos_batch* b) {
                                             : (kFieldBytes[f] == 0 ? w.span() : 32);
     if (bytes && src[f]) memcpy(p->h_in + p->off[f], src[f], bytes);
   }
+  if (p->gen && getenv("OURO_TEST_PLAN_POISON") && (rc = plan_poison(p))) return rc;
   // every launch a new generation, so no counter an earlier launch left
   // behind (one that never completed) is ever counted again
   p->gen = p->gen % 0x0fffffffu + 1u;
-  const uint32_t nw[3] = {(uint32_t)n, batch_opts(*b), p->gen};
+  p->opts = batch_opts(*b);
+  const uint32_t nw[3] = {(uint32_t)n, p->opts, p->gen};
   memcpy(p->h_in, nw, sizeof nw);
-  OURO_HIP(hipSetDevice(p->dev));
-  OURO_HIP(hipGraphLaunch(p->exec, p->st));
   p->pending = n;
   p->nonce_dst = b->eta_nonce;
+  p->failed = false;
+  const bool injected = injected_device_error();
+  hipError_t e = hipSetDevice(p->dev);
+  if (e == hipSuccess && !injected) e = hipGraphLaunch(p->exec, p->st);
+  if (e != hipSuccess || injected) {
+    fail(OURO_EDEVICE, std::string("plan launch: ") +
+                           (e != hipSuccess ? hipGetErrorString(e) : "injected device error"));
+    if (!recompute_on_error()) return OURO_EDEVICE;
+    p->failed = true;  // the inputs stay staged in h_in: wait verifies them on the host
+  }
   p->inflight = true;
   return OURO_OK;
 }
@@ -1483,8 +1663,20 @@ int ouro_tpraos_plan_wait(ouro_tpraos_plan* p, uint8_t* verdict, uint8_t* beta_e
   if (n && !verdict) return fail(OURO_EINVAL, "null verdict");
   p->inflight = false;
   if (n == 0) return OURO_OK;
-  OURO_HIP(hipSetDevice(p->dev));
-  OURO_HIP(hipStreamSynchronize(p->st));
+  int rc = OURO_OK;
+  if (!p->failed) {
+    hipError_t e = hipSetDevice(p->dev);
+    if (e == hipSuccess) e = hipStreamSynchronize(p->st);
+    if (e != hipSuccess) rc = fail(OURO_EDEVICE, std::string("plan wait: ") + hipGetErrorString(e));
+  } else {
+    rc = OURO_EDEVICE;
+  }
+  if (rc) {
+    const ouro_tpraos_batch hb = plan_host_batch(p);
+    p->nonce_dst = nullptr;
+    p->failed = false;
+    return or_host(rc, [&] { return ouro_host::hdr_batch(&hb, verdict, beta_eta, beta_leader); });
+  }
   const uint8_t* o = p->h_out + align16(p->cap);
   memcpy(verdict, p->h_out, n);
   if (beta_eta) memcpy(beta_eta, o, 64 * n);
@@ -1505,38 +1697,68 @@ int ouro_tpraos_plan_run(ouro_tpraos_plan* p, const ouro_tpraos_batch* b, uint8_
 
 void ouro_tpraos_plan_destroy(ouro_tpraos_plan* p) { plan_free(p); }
 
-// TEST HOOK (tests/test_gpu_claims.py::test_plan_counters_from_cut_off_launch):
-// leaves every arrival counter of the plan's records as a launch of its last
-// generation would have left them had it been cut off one arrival short of
-// each finish, so a test can show the next launch ignores them.
-int ouro_tpraos_plan_debug_poison(ouro_tpraos_plan* p) {
-  if (!p) return fail(OURO_EINVAL, "null plan");
-  if (p->inflight) return fail(OURO_EINVAL, "the plan has a batch in flight");
-  OURO_HIP(hipSetDevice(p->dev));
-  const size_t words = slot_region_words(p->cap, kLatResWords);
-  std::vector<int32_t> h(words);
-  OURO_HIP(hipMemcpy(h.data(), p->res, sizeof(int32_t) * words, hipMemcpyDeviceToHost));
-  const int32_t tag = (int32_t)((p->gen & 0x0fffffffu) << 4);
-  for (size_t i = 0; i < p->cap; i++) {
-    const Slot r = slot_of(h.data(), i, kLatResWords);
-    *r.word(kLatCtr) = tag | (kLatCores - 1);     // the header's tail one arrival away
-    *r.word(kLatCtr + 1) = tag | 1;                // each V / Gamma pair (or V / V2 /
-    *r.word(kLatCtr + 2) = tag | 1;                // Gamma triple), one in
-    for (int e = 0; e < 2; e++) {
-      *r.word(kLatEd + kEdWords * e + 125) = tag | 1;  // each Ed25519 points / scalars pair
-      for (int k = 17; k <= 19; k++)                // split form: the chain and done counters
-        *r.word(kLatEd + kEdWords * e + k) = tag | 1;
-    }
-  }
-  OURO_HIP(hipMemcpy(p->res, h.data(), sizeof(int32_t) * words, hipMemcpyHostToDevice));
-  return OURO_OK;
-}
-
 // TIMING PROBE (tools/lat_stamps.py): header 0's per-item stamps of the last
 // fused latency launch, 16 items x 24 tags of s_memrealtime (100 MHz), from a
 // library built with -DOURO_LAT_STAMPS=1 and run with OURO_LAT_STAMPS set;
 // returns the count, or -1 in the product build.
 int ouro_debug_lat_stamps(unsigned long long* out) { return lat_stamps_read(out); }
+
+// ---- the host path, called explicitly (host_path.h) ----
+int ouro_ed25519_verify_batch_host(size_t n, const uint8_t* pk, const uint8_t* sig,
+                                   const uint8_t* msg, const uint64_t* msg_off,
+                                   const uint32_t* msg_len, uint8_t* verdict) {
+  if (n == 0) return OURO_OK;
+  if (!pk || !sig || !msg_off || !msg_len || !verdict) return fail(OURO_EINVAL, "null argument");
+  return ouro_host::ed_batch(n, pk, sig, msg, msg_off, msg_len, verdict, 0);
+}
+int ouro_byron_ed25519_verify_batch_host(size_t n, const uint8_t* pk, const uint8_t* sig,
+                                         const uint8_t* msg, const uint64_t* msg_off,
+                                         const uint32_t* msg_len, uint8_t* verdict) {
+  if (n == 0) return OURO_OK;
+  if (!pk || !sig || !msg_off || !msg_len || !verdict) return fail(OURO_EINVAL, "null argument");
+  return ouro_host::ed_batch(n, pk, sig, msg, msg_off, msg_len, verdict, 1);
+}
+int ouro_vrf03_verify_batch_host(size_t n, const uint8_t* pk, const uint8_t* proof,
+                                 const uint8_t* alpha, const uint64_t* alpha_off,
+                                 const uint32_t* alpha_len, uint8_t* beta, uint8_t* verdict,
+                                 uint32_t flags) {
+  if (n == 0) return OURO_OK;
+  if (flags & ~OURO_VRF_STRICT_S) return fail(OURO_EINVAL, "unknown VRF flags");
+  if (!pk || !proof || !alpha_off || !alpha_len || !verdict) return fail(OURO_EINVAL, "null argument");
+  return ouro_host::vrf_batch(n, pk, proof, alpha, alpha_off, alpha_len, beta, verdict, flags);
+}
+int ouro_sum6kes_verify_batch_host(size_t n, const uint8_t* vk, const uint32_t* t,
+                                   const uint8_t* msg, const uint64_t* msg_off,
+                                   const uint32_t* msg_len, const uint8_t* sig, uint8_t* verdict) {
+  if (n == 0) return OURO_OK;
+  if (!vk || !t || !msg_off || !msg_len || !sig || !verdict) return fail(OURO_EINVAL, "null argument");
+  return ouro_host::kes_batch(n, vk, t, msg, msg_off, msg_len, sig, verdict);
+}
+int ouro_tpraos_verify_batch_host(const ouro_tpraos_batch* b, uint8_t* verdict,
+                                  uint8_t* beta_eta, uint8_t* beta_leader) {
+  if (!b) return fail(OURO_EINVAL, "null batch");
+  if (b->n == 0) return OURO_OK;
+  if (!verdict) return fail(OURO_EINVAL, "null verdict");
+  int rc = check_hdr_batch(b);
+  if (rc) return rc;
+  return ouro_host::hdr_batch(b, verdict, beta_eta, beta_leader);
+}
+int ouro_leader_check_batch_host(size_t n, const uint8_t* beta, const uint64_t* sigma_num,
+                                 const uint64_t* sigma_den, int64_t act_log_hi,
+                                 uint64_t act_log_lo, int f_is_one, uint8_t* verdict) {
+  if (n == 0) return OURO_OK;
+  if (!beta || !sigma_num || !sigma_den || !verdict) return fail(OURO_EINVAL, "null argument");
+  return ouro_host::leader_batch(n, beta, sigma_num, sigma_den, act_log_hi, act_log_lo, f_is_one,
+                                 verdict);
+}
+
+// Items the host path has verified: single items routed there, and host-
+// buffer batches recomputed there after a device error.
+int ouro_debug_host_path(unsigned long long* single_items, unsigned long long* recomputed_batches) {
+  if (single_items) *single_items = g_host_single.load();
+  if (recomputed_batches) *recomputed_batches = g_host_recompute.load();
+  return OURO_OK;
+}
 
 // Contexts of the per-thread pool on `device` (kernels.hip ThreadCtx):
 // created so far and idle (returned by exited threads).

@@ -43,8 +43,10 @@ class Ed25519DSIGN:
     verify_signed_dsign = verify_dsign
 
     @staticmethod
-    def verify_batch(vks, msgs, sigs) -> np.ndarray:
-        """Batch verify; returns a bool array (True = valid)."""
+    def verify_batch(vks, msgs, sigs, host: bool = False) -> np.ndarray:
+        """Batch verify; returns a bool array (True = valid).  host=True runs
+        the library's host path (ouro_ed25519_verify_batch_host: the kernels'
+        lane routines on the CPU) instead of the GPU."""
         vk = as_rows(vks, SIZE_VERKEY, "vk")
         sg = as_rows(sigs, SIZE_SIG, "sig")
         buf, off, ln = msgs_arg(msgs)
@@ -53,9 +55,10 @@ class Ed25519DSIGN:
             raise ValueError("vk, msg and sig batches differ in length")
         out = np.zeros(n, dtype=np.uint8)
         if n:
-            rc = _native.load().ouro_ed25519_verify_batch(
-                n, ptr(vk), ptr(sg), ptr(buf), ptr(off), ptr(ln), ptr(out))
-            _native.check(rc, "ouro_ed25519_verify_batch")
+            name = "ouro_ed25519_verify_batch" + ("_host" if host else "")
+            rc = getattr(_native.load(), name)(n, ptr(vk), ptr(sg), ptr(buf), ptr(off), ptr(ln),
+                                               ptr(out))
+            _native.check(rc, name)
         return out.astype(bool)
 
 

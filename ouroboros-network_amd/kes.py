@@ -65,7 +65,9 @@ class Sum6KES:
     verify_signed_kes = verify_kes
 
     @staticmethod
-    def verify_batch(vks, periods, msgs, sigs) -> np.ndarray:
+    def verify_batch(vks, periods, msgs, sigs, host: bool = False) -> np.ndarray:
+        """Batch verify; True = valid.  host=True: the library's host path
+        (ouro_sum6kes_verify_batch_host) instead of the GPU."""
         vk = as_rows(vks, SIZE_VERKEY, "vk")
         sg = as_rows(sigs, SIZE_SIG, "sig")
         t = periods_u32(periods)
@@ -75,9 +77,10 @@ class Sum6KES:
             raise ValueError("vk, t, msg and sig batches differ in length")
         out = np.zeros(n, dtype=np.uint8)
         if n:
-            rc = _native.load().ouro_sum6kes_verify_batch(
+            name = "ouro_sum6kes_verify_batch" + ("_host" if host else "")
+            rc = getattr(_native.load(), name)(
                 n, ptr(vk), ptr(t), ptr(buf), ptr(off), ptr(ln), ptr(sg), ptr(out))
-            _native.check(rc, "ouro_sum6kes_verify_batch")
+            _native.check(rc, name)
         return out.astype(bool)
 
 

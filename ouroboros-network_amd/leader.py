@@ -48,10 +48,11 @@ class ActiveSlotCoeff:
 
 
 def check_leader_values(beta_leader: np.ndarray, sigma: Sequence[Fraction],
-                        f: ActiveSlotCoeff) -> np.ndarray:
+                        f: ActiveSlotCoeff, host: bool = False) -> np.ndarray:
     """checkLeaderValue for every row of ``beta_leader`` (n x 64 u8) with the
     issuer's relative stake ``sigma[i]``; returns u8 LEADER_YES / LEADER_NO /
-    LEADER_BADARG (sigma or f outside the supported domain)."""
+    LEADER_BADARG (sigma or f outside the supported domain).  host=True: the
+    library's host path (ouro_leader_check_batch_host) instead of the GPU."""
     beta = np.ascontiguousarray(beta_leader, dtype=np.uint8).reshape(-1, 64)
     n = beta.shape[0]
     if len(sigma) != n:
@@ -66,10 +67,11 @@ def check_leader_values(beta_leader: np.ndarray, sigma: Sequence[Fraction],
     verdict = np.zeros(n, dtype=np.uint8)
     if n:
         hi, lo = f.words()
-        rc = _native.load().ouro_leader_check_batch(n, ptr(beta), ptr(num), ptr(den),
-                                                    ctypes.c_int64(hi), ctypes.c_uint64(lo),
-                                                    1 if f.is_one else 0, ptr(verdict))
-        _native.check(rc, "ouro_leader_check_batch")
+        name = "ouro_leader_check_batch" + ("_host" if host else "")
+        rc = getattr(_native.load(), name)(n, ptr(beta), ptr(num), ptr(den), ctypes.c_int64(hi),
+                                           ctypes.c_uint64(lo), 1 if f.is_one else 0,
+                                           ptr(verdict))
+        _native.check(rc, name)
     return verdict
 
 

@@ -173,6 +173,19 @@ def verify_headers(batch: HeaderBatch, nonce: bool = False):
     return (verdict, be, bl, en) if nonce else (verdict, be, bl)
 
 
+def verify_headers_host(batch: HeaderBatch, nonce: bool = False):
+    """verify_headers on the library's host path (ouro_tpraos_verify_batch_host:
+    the kernels' lane routines on the CPU threads); same results."""
+    n = len(batch)
+    verdict, be, bl, en = _outputs(n, nonce)
+    if n:
+        s = batch.c_struct(en)
+        rc = _native.load().ouro_tpraos_verify_batch_host(ctypes.byref(s), ptr(verdict), ptr(be),
+                                                          ptr(bl))
+        _native.check(rc, "ouro_tpraos_verify_batch_host")
+    return (verdict, be, bl, en) if nonce else (verdict, be, bl)
+
+
 def nonce_fold(eta_nonce: np.ndarray, slot: np.ndarray, first_slot_next_epoch: int,
                stability_window: int, eta_v: Optional[bytes], eta_c: Optional[bytes]):
     """The host-side UPDN fold over headers already verified (ouro_nonce_fold):
@@ -266,12 +279,6 @@ class HeaderPlan:
         self._pending = 0
         nonce, self._nonce = getattr(self, "_nonce", None), None
         return tuple(out) + (nonce,) if nonce is not None else out
-
-    def debug_poison(self) -> None:
-        """TEST HOOK (ouro_tpraos_plan_debug_poison): leave the plan's arrival
-        counters as a launch cut off one arrival short of each finish would."""
-        _native.check(self._lib.ouro_tpraos_plan_debug_poison(self._p),
-                      "ouro_tpraos_plan_debug_poison")
 
     def close(self):
         if self._p:

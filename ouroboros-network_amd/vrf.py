@@ -84,8 +84,10 @@ class PraosVRF:
         return None
 
     @staticmethod
-    def verify_batch(vks, alphas, proofs, s_mode: str = "reduce"):
-        """Returns (valid bool array, outputs (n, 64) uint8; zero rows where invalid)."""
+    def verify_batch(vks, alphas, proofs, s_mode: str = "reduce", host: bool = False):
+        """Returns (valid bool array, outputs (n, 64) uint8; zero rows where
+        invalid).  host=True: the library's host path
+        (ouro_vrf03_verify_batch_host) instead of the GPU."""
         flags = _s_flags(s_mode)
         vk = as_rows(vks, SIZE_VERKEY, "vk")
         pf = as_rows(proofs, SIZE_PROOF, "proof")
@@ -96,9 +98,10 @@ class PraosVRF:
         ver = np.zeros(n, dtype=np.uint8)
         beta = np.zeros((n, SIZE_OUTPUT), dtype=np.uint8)
         if n:
-            rc = _native.load().ouro_vrf03_verify_batch_flags(
+            name = "ouro_vrf03_verify_batch_host" if host else "ouro_vrf03_verify_batch_flags"
+            rc = getattr(_native.load(), name)(
                 n, ptr(vk), ptr(pf), ptr(buf), ptr(off), ptr(ln), ptr(beta), ptr(ver), flags)
-            _native.check(rc, "ouro_vrf03_verify_batch_flags")
+            _native.check(rc, name)
         return ver.astype(bool), beta
 
 

@@ -12,6 +12,36 @@ for p in (ROOT, os.path.join(ROOT, "tests")):
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (gfx950) and the built HIP library")
     config.addinivalue_line("markers", "slow: larger CPU-side cases")
+    config.addinivalue_line("markers", "device_error: forces device errors (the host recompute "
+                            "path is expected to run)")
+
+
+def _recomputed(lib):
+    import ctypes
+
+    a, b = ctypes.c_ulonglong(), ctypes.c_ulonglong()
+    lib.ouro_debug_host_path(ctypes.byref(a), ctypes.byref(b))
+    return b.value
+
+
+@pytest.fixture(autouse=True)
+def _no_silent_host_recompute(request):
+    """A GPU test must pass on the GPU: the library recomputes a host-buffer
+    batch on its host path after a device error (include/ouro_verify.h), so
+    every `gpu` test not marked `device_error` fails if that happened while
+    it ran -- a device fault can never hide behind correct host verdicts."""
+    if request.node.get_closest_marker("gpu") is None or \
+            request.node.get_closest_marker("device_error") is not None:
+        yield
+        return
+    from ouroboros_network_amd import _native
+
+    before = _recomputed(_native._lib) if _native._lib is not None else 0
+    yield
+    if _native._lib is not None:
+        after = _recomputed(_native._lib)
+        assert after == before, f"{after - before} batch(es) were recomputed on the host " \
+                                "path after a device error during a GPU test"
 
 
 @pytest.fixture(scope="session")

@@ -155,8 +155,10 @@ else:
 @pytest.mark.parametrize("mode", ["default", "invalid"])
 def test_shim_never_reports_a_device_error_as_an_invalid_proof(mode, which):
     """PraosVRF reads any nonzero as 'invalid proof'.  With no device the
-    product returns an error code; the shim must abort (default) rather than
-    pass it on, or return -1 only when OURO_SHIM_ON_ERROR=invalid says so."""
+    product's GPU route returns an error code; the shim must abort (default)
+    rather than pass it on, or return -1 only when OURO_SHIM_ON_ERROR=invalid
+    says so.  (Single items run on the host path by default since round 4;
+    OURO_SINGLE_ITEM=gpu sends them to the -- here absent -- device.)"""
     import subprocess
     import sys
 
@@ -166,6 +168,7 @@ def test_shim_never_reports_a_device_error_as_an_invalid_proof(mode, which):
         pytest.skip("a GPU is present")
     env = dict(os.environ)
     env.pop("OURO_SHIM_ON_ERROR", None)
+    env["OURO_SINGLE_ITEM"] = "gpu"
     if mode == "invalid":
         env["OURO_SHIM_ON_ERROR"] = "invalid"
     r = subprocess.run([sys.executable, "-c", _SHIM_CALL, LIB,
@@ -179,15 +182,26 @@ def test_shim_never_reports_a_device_error_as_an_invalid_proof(mode, which):
 
 
 def test_no_device_is_an_error_not_an_accept():
+    """A batch call with no device returns OURO_ENODEV -- not a device error,
+    so nothing is recomputed on the host path behind the caller's back -- and
+    leaves the verdicts untouched."""
+    import numpy as np
     import torch
 
     if torch.cuda.is_available():
         pytest.skip("a GPU is present")
     lib = ctypes.CDLL(LIB)
-    lib.ouro_ed25519_verify.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_ulonglong,
-                                        ctypes.c_void_p]
-    rc = lib.ouro_ed25519_verify(bytes(64), b"", 0, bytes(32))
-    assert rc != 0
+    P = ctypes.c_void_p
+    lib.ouro_ed25519_verify_batch.argtypes = [ctypes.c_size_t, P, P, P, P, P, P]
+    off = np.zeros(1, np.uint64)
+    ln = np.zeros(1, np.uint32)
+    v = np.full(1, 7, np.uint8)
+    rc = lib.ouro_ed25519_verify_batch(1, bytes(32), bytes(64), b"\0", off.ctypes.data,
+                                       ln.ctypes.data, v.ctypes.data)
+    assert rc == -4 and v[0] == 7  # OURO_ENODEV
+    single, recomputed = ctypes.c_ulonglong(), ctypes.c_ulonglong()
+    lib.ouro_debug_host_path(ctypes.byref(single), ctypes.byref(recomputed))
+    assert recomputed.value == 0
 
 
 def test_missing_library_fails_loudly(tmp_path):

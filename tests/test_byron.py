@@ -15,7 +15,7 @@ def test_golden_byron_header_slices_to_the_signed_message(kats):
     b = kats["byron"]
     h = parse_byron_header(bytes.fromhex(b["raw"]))
     assert h.magic == b["magic"] == 55550001
-    assert h.message().hex() == b["msg"]
+    assert h.message("header").hex() == b["msg"]
     assert h.delegate_xpub[:32].hex() == b["pk"]
     assert h.sig.hex() == b["sig"]
     assert h.to_sign[0] == 0x85  # ToSign is a 5-element CBOR list
@@ -70,3 +70,33 @@ def test_byron_rules_differ_from_libsodium_where_expected():
     assert not O.ed25519_verify(ident + bytes(32), msg, ident)
     verdicts = np.array([O.ed25519_verify_byron(s, m, p) for p, s, m in cases])
     assert verdicts.any() and not verdicts.all()
+
+
+def test_protocol_magic_is_required_and_the_configured_one_is_used(kats):
+    """the sign tag's magic is the node's configured
+    ProtocolMagicId (Byron/Ledger/PBFT.hs:43-45, DSIGN.hs:111), never
+    silently the peer's header field.  No default; HEADER_MAGIC only by name.
+    A header whose magic field differs from the configured magic is rejected
+    (host path: no GPU needed)."""
+    from ouroboros_network_amd import byron as B
+
+    b = kats["byron"]
+    h = B.parse_byron_header(bytes.fromhex(b["raw"]))
+    raw = bytes.fromhex(b["raw"])
+    with pytest.raises(ValueError):
+        B.pack_byron_cbor([raw], None)
+    with pytest.raises(TypeError):
+        B.verify_byron_cbor([raw])  # pylint: disable=no-value-for-parameter
+    with pytest.raises(ValueError):
+        h.message(None)
+    with pytest.raises(ValueError):
+        B.pack_byron_cbor([raw], "peer")
+    assert h.message(b["magic"]) == h.message(B.HEADER_MAGIC)  # golden: field == configured
+    mainnet = 764824073
+    assert h.magic != mainnet
+    ok = B.ByronDSIGN.verify_batch([h.delegate_xpub[:32]] * 2,
+                                   [h.message(b["magic"]), h.message(mainnet)], [h.sig] * 2,
+                                   host=True)
+    assert ok.tolist() == [True, False]
+    packed = B.pack_byron_cbor([raw], mainnet)
+    assert packed.message(0) == h.message(mainnet)

@@ -12,6 +12,9 @@ Every path -- throughput kernel (one piece and pipelined chunks), latency
 kernels (lane quads and one lane), captured plans (run, submit/wait) and the
 multi-device workers -- against the oracle (oracle/tpraos.c), bit for bit.
 """
+import contextlib
+import os
+
 import numpy as np
 import pytest
 
@@ -129,11 +132,22 @@ def test_nonce_fold_from_device_outputs(gpu_lib, kats):
         assert got == ON.fold(None, b"\x11" * 32, [bytes(r) for r in en], slots, fsne, 7)
 
 
+@contextlib.contextmanager
+def _poisoned_submit():
+    """The plan test hook (kernels.hip plan_poison), reached only through the
+    environment: every submit while it is set first poisons the counters."""
+    os.environ["OURO_TEST_PLAN_POISON"] = "1"
+    try:
+        yield
+    finally:
+        del os.environ["OURO_TEST_PLAN_POISON"]
+
+
 def test_plan_counters_from_cut_off_launch(gpu_lib, kats):
     """A plan whose arrival counters were left mid-count by an earlier launch
-    that never completed (simulated: ouro_tpraos_plan_debug_poison leaves every
-    counter one arrival short of its finish, tagged with the last launch's
-    generation) must still give the oracle's verdicts and outputs on the next
+    that never completed (simulated: with OURO_TEST_PLAN_POISON set,
+    ouro_tpraos_plan_submit first leaves every counter one arrival short of its
+    finish, tagged with the last launch's generation) must still give the oracle's verdicts and outputs on the next
     window: each launch counts in its own generation (wide_cores.h
     arrive_last), so no header finishes early on the stale counts -- and no
     verdict carries an earlier window's result.  The second window holds other
@@ -148,12 +162,12 @@ def test_plan_counters_from_cut_off_launch(gpu_lib, kats):
     try:
         _check(plan.run(first, nonce=True), w1)
         for _ in range(3):
-            plan.debug_poison()
-            _check(plan.run(second, nonce=True), w2)
-            plan.debug_poison()
-            _check(plan.run(first, nonce=True), w1)
+            with _poisoned_submit():
+                _check(plan.run(second, nonce=True), w2)
+            with _poisoned_submit():
+                _check(plan.run(first, nonce=True), w1)
         # and a partial window after a poisoned full one
-        plan.debug_poison()
-        _check(plan.run(second.slice(5, 17), nonce=True), tuple(a[5:17] for a in w2))
+        with _poisoned_submit():
+            _check(plan.run(second.slice(5, 17), nonce=True), tuple(a[5:17] for a in w2))
     finally:
         plan.close()

@@ -17,10 +17,15 @@ EXE = os.path.join(ROOT, "tests", "c", "build", "concurrency")
 pytestmark = pytest.mark.gpu
 
 
-def test_eight_threads_mixed_calls(gpu_lib):
+@pytest.mark.parametrize("single_route", ["host", "gpu"])
+def test_eight_threads_mixed_calls(gpu_lib, single_route):
+    """Single items on the host path (the default since round 4) and on the
+    GPU (OURO_SINGLE_ITEM=gpu), concurrently with batch calls."""
     if not os.path.exists(EXE):
         subprocess.run(["make", "-C", os.path.join(ROOT, "tests", "c")], check=True)
-    r = subprocess.run([EXE, "8", "30", "64"], capture_output=True, text=True, timeout=100)
+    env = dict(os.environ, OURO_SINGLE_ITEM=single_route)
+    r = subprocess.run([EXE, "8", "30", "64"], capture_output=True, text=True, timeout=100,
+                       env=env)
     assert r.returncode == 0, r.stdout + r.stderr
     ok, calls, created = r.stdout.split()
     assert (ok, calls) == ("ok", str(8 * 30))

@@ -456,7 +456,9 @@ def test_byron_golden_header(small_path, gpu_lib, kats):
         == "Verification failed"
     assert ByronDSIGN.verify_dsign((h.magic + 1, h.issuer_xpub), h.delegate_xpub, h.to_sign,
                                    h.sig) == "Verification failed"
-    assert verify_byron_headers([h, h]).tolist() == [True, True]
+    assert verify_byron_headers([h, h], protocol_magic=b["magic"]).tolist() == [True, True]
+    # a header signed for another network's magic fails under the configured one
+    assert verify_byron_headers([h], protocol_magic=764824073).tolist() == [False]
 
 
 def test_byron_batch_matches_oracle(small_path, gpu_lib):
@@ -500,7 +502,7 @@ def test_byron_raw_headers_to_verdicts(small_path, gpu_lib, kats):
             m = bytearray(g)
             m[pos] ^= 0x04
             raws.append(bytes(m))
-    got, status = B.verify_byron_cbor(raws)
+    got, status = B.verify_byron_cbor(raws, B.HEADER_MAGIC)
     want = []
     for r in raws:
         st, h = B.byron_status(r)
@@ -509,7 +511,7 @@ def test_byron_raw_headers_to_verdicts(small_path, gpu_lib, kats):
         elif st != B.PACK_OK:
             want.append(False)
         else:
-            want.append(O.ed25519_verify_byron(h.sig, h.message(), h.delegate_xpub[:32]))
+            want.append(O.ed25519_verify_byron(h.sig, h.message(B.HEADER_MAGIC), h.delegate_xpub[:32]))
         assert status[len(want) - 1] == st
     np.testing.assert_array_equal(got, np.array(want))
     assert got[:len(wires)].all()

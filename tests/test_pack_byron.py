@@ -19,7 +19,7 @@ def wires(kats):
     return [(w["form"], w["kind"], bytes.fromhex(w["raw"])) for w in kats["byron_wire"]]
 
 
-def assert_same(raws, pk, protocol_magic=None):
+def assert_same(raws, pk, protocol_magic=B.HEADER_MAGIC):
     for i, r in enumerate(raws):
         st, h = B.byron_status(r)
         assert pk.status[i] == st, f"header {i}: C status {pk.status[i]}, Python {st}"
@@ -39,7 +39,7 @@ def assert_same(raws, pk, protocol_magic=None):
 def test_golden_wire_forms(kats, wires):
     g = kats["byron"]
     raws = [r for _, _, r in wires]
-    pk = B.pack_byron_cbor(raws, nthreads=1)
+    pk = B.pack_byron_cbor(raws, B.HEADER_MAGIC, nthreads=1)
     assert_same(raws, pk)
     for i, (form, kind, _) in enumerate(wires):
         if kind == "boundary":
@@ -75,7 +75,7 @@ def test_every_byte_corruption_matches_python(wires):
                 m = bytearray(g)
                 m[pos] ^= x
                 raws.append(bytes(m))
-    pk = B.pack_byron_cbor(raws, nthreads=4)
+    pk = B.pack_byron_cbor(raws, B.HEADER_MAGIC, nthreads=4)
     assert_same(raws, pk)
     seen = set(pk.status.tolist())
     assert {B.PACK_OK, B.PACK_ECBOR, B.PACK_ESHAPE, B.PACK_EBB} <= seen, seen
@@ -84,7 +84,7 @@ def test_every_byte_corruption_matches_python(wires):
 def test_every_truncation_rejected(wires):
     for _, _, g in wires[:2] + [w for w in wires if w[0] == "hfc"][:2]:
         raws = [g[:k] for k in range(len(g))]
-        pk = B.pack_byron_cbor(raws)
+        pk = B.pack_byron_cbor(raws, B.HEADER_MAGIC)
         assert (pk.status != B.PACK_OK).all()
         assert_same(raws, pk)
 
@@ -104,7 +104,7 @@ def test_cbor_in_cbor_bounds(wires):
         cases = [pre + enc(ln - 1) + payload, pre + enc(ln + 1) + payload,
                  pre + enc(ln + 1) + payload + b"\x00", g + b"\x00",
                  pre[:-1] + b"\x5f" + b"\x59" + enc(ln) + payload + b"\xff"]
-        pk = B.pack_byron_cbor(cases)
+        pk = B.pack_byron_cbor(cases, B.HEADER_MAGIC)
         assert (pk.status != B.PACK_OK).all(), form
         assert_same(cases, pk)
 
@@ -133,13 +133,13 @@ def test_shape_rules(kats, wires):
         "short_issuer_xpub": short,
     }
     raws = list(cases.values())
-    pk = B.pack_byron_cbor(raws)
+    pk = B.pack_byron_cbor(raws, B.HEADER_MAGIC)
     assert_same(raws, pk)
     got = dict(zip(cases, pk.status.tolist()))
     assert got["shelley_era_1"] == got["shelley_header"] == B.PACK_ESHELLEY
     assert got["era_indefinite"] == B.PACK_ESHAPE
     assert got["byron_v2_unwrapped"] == B.PACK_OK
-    assert pk.message(3) == B.pack_byron_cbor([hfc]).message(0)
+    assert pk.message(3) == B.pack_byron_cbor([hfc], B.HEADER_MAGIC).message(0)
     assert got["v2_kind_2"] == got["v1_kind_3"] == B.PACK_ESHAPE
     assert got["shelley_as_byron_v1"] in (B.PACK_ESHAPE, B.PACK_ECBOR)
     assert got["sig_kind_0"] == B.PACK_ESHAPE
@@ -158,23 +158,23 @@ def test_threads_and_spans_inside_one_buffer(wires):
         ln.append(len(r))
         at += len(pad) + len(r)
     buf = b"".join(parts)
-    one = B.pack_byron_cbor((buf, off, ln), nthreads=1)
-    many = B.pack_byron_cbor((buf, off, ln), nthreads=3)
+    one = B.pack_byron_cbor((buf, off, ln), B.HEADER_MAGIC, nthreads=1)
+    many = B.pack_byron_cbor((buf, off, ln), B.HEADER_MAGIC, nthreads=3)
     assert np.array_equal(one.status, many.status)
     assert set(one.status.tolist()) == {B.PACK_OK, B.PACK_EBB}
     for f in ("pk", "sig", "genesis_vk", "delegate_vk", "magic", "msg_len"):
         assert np.array_equal(getattr(one, f), getattr(many, f)), f
     for i in (0, 1, 4500, 8999):
         assert one.message(i) == many.message(i)
-        assert_same([raws[i]], B.pack_byron_cbor([raws[i]]))
+        assert_same([raws[i]], B.pack_byron_cbor([raws[i]], B.HEADER_MAGIC))
 
 
 def test_bad_arguments_are_einval(wires):
     g = wires[0][2]
     with pytest.raises(ValueError):
-        B.pack_byron_cbor((g, [0], [len(g) + 1]))      # span past the end
+        B.pack_byron_cbor((g, [0], [len(g) + 1]), B.HEADER_MAGIC)  # span past the end
     with pytest.raises(ValueError):
-        B.pack_byron_cbor((g, [2 ** 64 - 1], [4]))     # wrapping offset
+        B.pack_byron_cbor((g, [2 ** 64 - 1], [4]), B.HEADER_MAGIC)  # wrapping offset
     lib = _native.load()
     out = _native.ByronBatch()
     assert lib.ouro_byron_pack_cbor(None, 0, None, None, 0, -1, None, 0, ctypes.byref(out),
@@ -195,7 +195,7 @@ def test_bad_arguments_are_einval(wires):
 
 
 def test_empty_batch():
-    pk = B.pack_byron_cbor([])
+    pk = B.pack_byron_cbor([], B.HEADER_MAGIC)
     assert pk.status.size == 0 and pk.pk.shape == (0, 32)
 
 
