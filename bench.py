@@ -325,6 +325,65 @@ def measure_peak_mac(device) -> float:
     return float(fn())
 
 
+CLOCK_SO = os.path.join(ROOT, "ouroboros-network_amd", "lib", "libouro_verify_clock.so")
+DEVHOST_SO = os.path.join(ROOT, "ouroboros-network_amd", "lib", "libouro_devhost_test.so")
+
+
+def kernel_clock_ghz(hdr, stream, launches: int = 12):
+    """The shader clock k_tpraos_verify itself runs at on THIS box: the
+    diagnostic build lib/libouro_verify_clock.so (-DOURO_CLOCK_STAMPS=1: the
+    same kernel with s_memtime / s_memrealtime stamps at each workgroup's entry
+    and exit, MI355X_MICROARCH.md "DVFS give-back" item 6) run back to back on
+    the same device-resident batch; median over workgroups of the last launch.
+    The timed product launches never execute a stamp."""
+    import torch
+
+    if not os.path.exists(CLOCK_SO):
+        return None, "lib/libouro_verify_clock.so not built"
+    lib = ctypes.CDLL(CLOCK_SO)
+    P = ctypes.c_void_p
+    lib.ouro_tpraos_verify_batch_device.argtypes = [P, P, P, P, P]
+    lib.ouro_debug_clock_stamps.argtypes = [P, ctypes.c_int]
+    lib.ouro_set_device.argtypes = [ctypes.c_int]
+    lib.ouro_set_device(torch.cuda.current_device())
+    t0 = time.perf_counter()
+    for _ in range(launches):
+        rc = lib.ouro_tpraos_verify_batch_device(P(stream.cuda_stream), ctypes.byref(hdr.s),
+                                                 P(hdr.verdict.data_ptr()),
+                                                 P(hdr.beta_eta.data_ptr()),
+                                                 P(hdr.beta_leader.data_ptr()))
+        if rc != 0:
+            return None, f"diagnostic launch failed ({rc})"
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    buf = np.zeros((8192, 4), np.uint64)
+    rows = lib.ouro_debug_clock_stamps(P(buf.ctypes.data), 8192)
+    if rows <= 0:
+        return None, "no stamps"
+    st = buf[:rows].astype(np.float64)
+    ok = (st[:, 3] > st[:, 2]) & (st[:, 1] > st[:, 0])
+    ghz = (st[ok, 1] - st[ok, 0]) / (st[ok, 3] - st[ok, 2]) * 0.1
+    return float(np.median(ghz)), f"median of {int(ok.sum())} workgroups, last of {launches} " \
+                                  f"back-to-back launches ({wall:.2f} s)"
+
+
+def executed_work_per_header():
+    """Field operations the kernels' lane routines execute for one header in
+    the throughput schedule (the host build with operation counters,
+    lib/libouro_devhost_test.so -- the same source), as v_mad_u64_u32 counts:
+    100 per multiply, 55 per squaring (csrc/fe25519.h)."""
+    if not os.path.exists(DEVHOST_SO):
+        return None
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    try:
+        import count_ops
+        r = count_ops.counts(header_only=True)["tpraos_header (throughput schedule)"]
+    except Exception:  # noqa: BLE001
+        return None
+    return {"field_mul": r["mul"], "field_sq": r["sq"],
+            "executed_mads_per_header": 100 * r["mul"] + 55 * r["sq"]}
+
+
 def ed25519_rate(device, n: int, reps: int):
     """Ed25519 verifies/s on n device-resident synthetic signatures; returns
     (result, (pk, sig, msg) device tensors)."""
@@ -871,7 +930,9 @@ def _timed(fn) -> float:
 def load_pmc_traffic():
     """HBM bytes per header of one header-kernel launch from the committed PMC
     run (profiles/pmc_traffic.json, tools/summarize_profile.py), with whether
-    that run measured THIS source (its stamped source_hash)."""
+    that run measured THIS source (its stamped source_hash), and the same
+    run's box-independent counters: VALU lane-instructions per header
+    (SQ_INSTS_VALU) and the clock it ran at (GRBM_GUI_ACTIVE / 8 / wall)."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         with open(path) as f:
@@ -880,7 +941,9 @@ def load_pmc_traffic():
         return None, {}
     return d.get("k_tpraos_verify_bytes_per_launch_per_header"), {
         "traffic_round": d.get("round"), "traffic_source_hash": d.get("source_hash"),
-        "traffic_matches_source": d.get("source_hash") == source_hash()}
+        "traffic_matches_source": d.get("source_hash") == source_hash(),
+        "valu_lane_insts_per_header": d.get("valu_lane_insts_per_header"),
+        "pmc_clock_ghz": d.get("clock_ghz")}
 
 
 def load_component_traffic():
@@ -1160,6 +1223,20 @@ def main():
             print(f"# peak microbench failed: {e}", file=sys.stderr)
         achieved = n * MACS_PER_HEADER / (kern_ms * 1e-3) / 1e12
         traffic_per_header, traffic_meta = load_pmc_traffic()
+        # box-independent companions of frac: the clock
+        # the header kernel itself ran at on this box (diagnostic stamp
+        # build), the INT32 issue ceiling at that clock, the MADs the code
+        # executes, and the committed SQ / traffic counters per header
+        clk, clk_how = None, "not measured (--no-extras: the profiling runs)"
+        if not args.no_extras:
+            try:
+                clk, clk_how = kernel_clock_ghz(hdr, stream)
+            except Exception as e:  # noqa: BLE001
+                clk, clk_how = None, f"clock probe failed: {e}"
+        cus = torch.cuda.get_device_properties(device).multi_processor_count
+        ceiling = cus * 64 * clk * 1e9 / 1e12 if clk else None
+        work = executed_work_per_header()
+        exec_mads = work["executed_mads_per_header"] if work else None
         roof = {
             "bound": "valu",
             "kernel": "k_tpraos_verify",
@@ -1167,9 +1244,23 @@ def main():
             "peak": round(peak, 3) if peak else None,
             "unit": "TMAC/s",
             "frac": round(achieved / peak, 4) if peak else None,
+            "frac_clock": round(achieved / ceiling, 4) if ceiling else None,
+            "clock_ghz": round(clk, 4) if clk else None,
+            "clock_how": clk_how,
+            "int32_ceiling_at_clock": round(ceiling, 3) if ceiling else None,
+            "int32_ceiling_note": f"{cus} CU x 64 lanes x clock_ghz: one 32-bit VALU op "
+                                  "per lane per clock",
+            "executed_mads_per_header": exec_mads,
+            "executed_mad_rate": (round(n * exec_mads / (kern_ms * 1e-3) / 1e12, 3)
+                                  if exec_mads else None),
+            "frac_clock_executed": (round(n * exec_mads / (kern_ms * 1e-3) / 1e12 / ceiling, 4)
+                                    if exec_mads and ceiling else None),
+            "field_ops_per_header": ({"mul": work["field_mul"], "sq": work["field_sq"]}
+                                     if work else None),
             "traffic": (round(traffic_per_header * n) if traffic_per_header else None),
             "traffic_per_header": (round(traffic_per_header, 1) if traffic_per_header else None),
             "algorithmic_bytes_per_header": 1537,
+            "traffic_ratio": (round(traffic_per_header / 1537, 1) if traffic_per_header else None),
             "macs_per_header": MACS_PER_HEADER,
             "kernel_ms_per_launch": round(kern_ms, 3),
             "source_hash": source_hash(),

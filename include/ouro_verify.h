@@ -461,6 +461,14 @@ int ouro_debug_contexts(int device, size_t *created, size_t *idle);
  * Returns the number of stamps written to out, or -1 (the product build). */
 int ouro_debug_lat_stamps(unsigned long long *out);
 
+/* CLOCK PROBE (bench.py roofline.frac_clock): the shader clock the header
+ * kernel ran at, from per-workgroup s_memtime / s_memrealtime stamps at entry
+ * and exit of the last k_tpraos_verify launch (4 values per workgroup, up to
+ * max_slots rows), in a library built with -DOURO_CLOCK_STAMPS=1
+ * (lib/libouro_verify_clock.so).  Returns the rows written, or -1 (the
+ * product build, in which no stamp executes). */
+int ouro_debug_clock_stamps(unsigned long long *out, int max_slots);
+
 /* ---------------------------------------------- leader threshold ----- */
 /* ledger-specs checkLeaderValue (shelley-spec-ledger BlockChain.hs), called by
  * meetsLeaderThreshold, ouroboros-consensus-shelley/src/Ouroboros/Consensus/

@@ -113,6 +113,7 @@ SIGNATURES = {
                                           _P]),
     "ouro_debug_contexts": (_I, [_I, _P, _P]),
     "ouro_debug_lat_stamps": (_I, [_P]),
+    "ouro_debug_clock_stamps": (_I, [_P, _I]),
     "ouro_sum6kes_verify_batch": (_I, [_SZ, _P, _P, _P, _P, _P, _P, _P]),
     "ouro_tpraos_verify_batch": (_I, [ctypes.POINTER(TPraosBatch), _P, _P, _P]),
     "ouro_ed25519_verify_batch_device": (_I, [_P, _SZ, _P, _P, _P, _P, _P, _P]),

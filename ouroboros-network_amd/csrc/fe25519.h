@@ -242,6 +242,22 @@ OURO_FI fe fe_carry(const fe& f) {
 #ifndef OURO_FE_SCAN
 #define OURO_FE_SCAN 1
 #endif
+// 2 v: v_add_u32 v, v on the device.  LLVM writes 2v / 4v as v_lshlrev_b32,
+// which issues at 3.46 SIMD cycles per wave-instruction at two waves per SIMD
+// against 2.52 for v_add_u32 (profiles/r04/valu_costs.json); non-volatile asm,
+// so equal inputs still CSE.  OURO_ADD_SCALE=0: the shifts (A/B).
+#ifndef OURO_ADD_SCALE
+#define OURO_ADD_SCALE 1
+#endif
+OURO_FI uint32_t u32_x2(uint32_t v) {
+#if defined(__HIP_DEVICE_COMPILE__) && OURO_ADD_SCALE
+  uint32_t r;
+  asm("v_add_u32 %0, %1, %1" : "=v"(r) : "v"(v));
+  return r;
+#else
+  return 2u * v;
+#endif
+}
 OURO_FI uint64_t mad_acc(uint32_t a, uint32_t b, uint64_t c) {
   uint64_t r = (uint64_t)a * b + c;
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -312,7 +328,7 @@ OURO_FI fe fe_mul_scan(const fe& f, const fe& g) {
 #pragma unroll
   for (int i = 0; i < 10; i++) {
     g19[i] = 19u * g.v[i];
-    f2[i] = (i & 1) ? 2u * f.v[i] : f.v[i];
+    f2[i] = (i & 1) ? u32_x2(f.v[i]) : f.v[i];
   }
   uint32_t h[10];
   uint64_t cA = 0, cB = 0;
@@ -625,9 +641,9 @@ OURO_FI fe fe_sq_scan(const fe& f) {
   uint32_t fs[10], f2s[10], f4s[10], f19[10];
 #pragma unroll
   for (int i = 0; i < 10; i++) {
-    fs[i] = kScale * f.v[i];
-    f2s[i] = 2u * kScale * f.v[i];
-    f4s[i] = 4u * kScale * f.v[i];
+    fs[i] = kScale == 1 ? f.v[i] : u32_x2(f.v[i]);
+    f2s[i] = u32_x2(fs[i]);
+    f4s[i] = u32_x2(f2s[i]);
     f19[i] = 19u * f.v[i];
   }
   uint32_t h[10];
@@ -828,6 +844,128 @@ OURO_FI fe fe_sq2(const fe& f) {
   OURO_TRK(trk_sq(h, f, 2));
   return h;
 #endif
+}
+
+// ---- independent products in lockstep (round 4) ------------------------------
+// N independent products, each scanned in ONE chain (column k's carry the
+// first addend of column k + 1), their multiply-adds interleaved so a chain's
+// dependent v_mad_u64_u32 sit N instructions apart.  A MAD's result is ready
+// ~14 cycles after it issues while a wave issues one every ~7
+// (tools/microbench/valu_costs.hip, profiles/r04/valu_costs.json), so at two
+// waves per SIMD a chain whose MADs depend back to back stalls; three or four
+// chains in lockstep do not.  The doubling built from these (ge25519.h
+// ge_dbl_lockstep) runs 25.9 vs 29.3 ps per chip-wide doubling
+// (tools/microbench/occupancy.hip, profiles/r04/occupancy_lockstep.json);
+// the same instruction count.
+template <int N>
+OURO_FI void fe_mul_xn(fe* h, const fe* f, const fe* g) {
+  uint32_t g19[N][10], f2[N][10];
+#pragma unroll
+  for (int e = 0; e < N; e++)
+#pragma unroll
+    for (int i = 0; i < 10; i++) {
+      g19[e][i] = 19u * g[e].v[i];
+      f2[e][i] = (i & 1) ? u32_x2(f[e].v[i]) : f[e].v[i];
+    }
+  uint32_t hv[N][10];
+  uint64_t c[N];
+#pragma unroll
+  for (int e = 0; e < N; e++) c[e] = 0;
+#pragma unroll
+  for (int k = 0; k < 10; k++) {
+    uint64_t t[N];
+#pragma unroll
+    for (int e = 0; e < N; e++) t[e] = c[e];
+#pragma unroll
+    for (int i = 0; i < 10; i++) {
+      const int j = (k - i + 10) % 10;
+#pragma unroll
+      for (int e = 0; e < N; e++) {
+        const uint32_t a = ((i & 1) && (j & 1)) ? f2[e][i] : f[e].v[i];
+        const uint32_t b = (i + j >= 10) ? g19[e][j] : g[e].v[j];
+        t[e] = mad_acc(a, b, t[e]);
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < N; e++) {
+      hv[e][k] = (uint32_t)t[e] & limb_mask(k);
+      c[e] = t[e] >> limb_bits(k);
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < N; e++) {
+    OURO_COUNT_MUL();
+    h[e] = scan_finish(hv[e], c[e]);
+    OURO_TRK({
+      unsigned __int128 T[10] = {0};
+      for (int i = 0; i < 10; i++) {
+        if (i & 1) trk_check(2 * f[e].b[i] < (1ull << 32));
+        if (i >= 1) trk_check(19 * g[e].b[i] < (1ull << 32));
+        for (int j = 0; j < 10; j++) {
+          const int k = i + j;
+          unsigned __int128 x = (unsigned __int128)f[e].b[i] * g[e].b[j];
+          if ((i & 1) && (j & 1)) x *= 2;
+          if (k >= 10) x *= 19;
+          T[k % 10] += x;
+        }
+      }
+      trk_scan(h[e], T, 1);
+    })
+  }
+}
+// N independent squarings in lockstep; element e is scaled by kScale[e]
+// (1: f^2, 2: 2 f^2), one chain each as fe_sq_scan
+template <int N>
+OURO_FI void fe_sq_xn(fe* h, const fe* f, const int (&scale)[N]) {
+  uint32_t fs[N][10], f2s[N][10], f4s[N][10], f19[N][10];
+#pragma unroll
+  for (int e = 0; e < N; e++)
+#pragma unroll
+    for (int i = 0; i < 10; i++) {
+      fs[e][i] = scale[e] == 1 ? f[e].v[i] : u32_x2(f[e].v[i]);
+      f2s[e][i] = u32_x2(fs[e][i]);
+      f4s[e][i] = u32_x2(f2s[e][i]);
+      f19[e][i] = 19u * f[e].v[i];
+    }
+  uint32_t hv[N][10];
+  uint64_t c[N];
+#pragma unroll
+  for (int e = 0; e < N; e++) c[e] = 0;
+#pragma unroll
+  for (int k = 0; k < 10; k++) {
+    uint64_t t[N];
+#pragma unroll
+    for (int e = 0; e < N; e++) t[e] = c[e];
+#pragma unroll
+    for (int i = 0; i < 10; i++)
+#pragma unroll
+      for (int j = i; j < 10; j++) {
+        if ((i + j) % 10 != k) continue;
+#pragma unroll
+        for (int e = 0; e < N; e++) {
+          uint32_t a, b;
+          if (i == j) {
+            a = (i & 1) ? f2s[e][i] : fs[e][i];
+            b = (2 * i >= 10) ? f19[e][i] : f[e].v[i];
+          } else {
+            a = ((i & 1) && (j & 1)) ? f4s[e][i] : f2s[e][i];
+            b = (i + j >= 10) ? f19[e][j] : f[e].v[j];
+          }
+          t[e] = mad_acc(a, b, t[e]);
+        }
+      }
+#pragma unroll
+    for (int e = 0; e < N; e++) {
+      hv[e][k] = (uint32_t)t[e] & limb_mask(k);
+      c[e] = t[e] >> limb_bits(k);
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < N; e++) {
+    OURO_COUNT_SQ();
+    h[e] = scan_finish(hv[e], c[e]);
+    OURO_TRK(trk_sq_scan(h[e], f[e], (unsigned)scale[e], 1));
+  }
 }
 
 // ---- encoding -------------------------------------------------------------

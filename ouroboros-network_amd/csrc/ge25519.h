@@ -70,6 +70,28 @@ OURO_FI ge_p1p1 ge_p2_dbl(const ge_p2& p) {
 }
 OURO_FI ge_p1p1 ge_p3_dbl(const ge_p3& p) { return ge_p2_dbl(ge_p3_to_p2(p)); }
 
+// ge_p2_dbl(ge_p1p1_to_p2(t)) -- a doubling of a chain -- with the three
+// products of the p2 conversion in lockstep, then the four squarings in
+// lockstep (fe25519.h fe_mul_xn / fe_sq_xn): the same operations and operand
+// order, so the same bounds, scheduled so no multiply-add waits on the one
+// before it (round 4: 29.3 -> 25.9 ps per chip-wide doubling at two waves per
+// SIMD, profiles/r04/occupancy_lockstep.json).
+OURO_FI ge_p1p1 ge_dbl_lockstep(const ge_p1p1& t) {
+  const fe f[3] = {t.T, t.Z, t.T}, g[3] = {t.X, t.Y, t.Z};
+  fe p[3];
+  fe_mul_xn<3>(p, f, g);  // X = T X, Y = Z Y, Z = T Z
+  const fe in[4] = {p[0], p[1], p[2], fe_add(p[0], p[1])};
+  constexpr int kScale[4] = {1, 1, 2, 1};  // A = X^2, B = Y^2, C = 2 Z^2, S = (X + Y)^2
+  fe o[4];
+  fe_sq_xn<4>(o, in, kScale);
+  ge_p1p1 r;
+  r.Y = fe_carry(fe_add(o[1], o[0]));
+  r.Z = fe_sub(o[1], o[0]);
+  r.X = fe_sub(o[3], r.Y);
+  r.T = fe_sub(fe_add(o[2], o[0]), o[1]);
+  return r;
+}
+
 // P + Q (neg = false) or P - Q (neg = true), Q cached.  The sign is a per-lane
 // select so a wave stays convergent whatever the digits are.  affine_q (wave-
 // uniform): Q has Z = 1 (Z2 = 2), so 2 Z_P Z_Q is a re-normalised addition.

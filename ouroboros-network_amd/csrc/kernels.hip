@@ -111,6 +111,21 @@ __device__ __noinline__ void hdr_finish_item_ni(const ouro_tpraos_batch& b, size
 }
 #endif
 
+// CLOCK PROBE (a separate diagnostic build, lib/libouro_verify_clock.so,
+// -DOURO_CLOCK_STAMPS=1; in the product build no stamp executes): thread 0 of
+// each workgroup stamps s_memtime (shader clock) and s_memrealtime (100 MHz)
+// at entry and exit of k_tpraos_verify, so bench.py reads the clock the
+// header kernel itself ran at (MI355X_MICROARCH.md "DVFS give-back" item 6)
+// for roofline.frac_clock.  Every workgroup of the capped grid lives for the
+// whole launch.
+#ifndef OURO_CLOCK_STAMPS
+#define OURO_CLOCK_STAMPS 0
+#endif
+[[maybe_unused]] constexpr int kClockSlots = 8192;
+#if OURO_CLOCK_STAMPS
+__device__ unsigned long long g_clock_stamps[kClockSlots][4];
+#endif
+
 // Throughput mode: one lane per header runs every core of tpraos.h, sharing
 // the VRF key decode and its table, then the single-inversion finish.
 __global__ void __launch_bounds__(kBlock, OURO_WAVES) k_tpraos_verify(ouro_tpraos_batch b,
@@ -124,6 +139,13 @@ __global__ void __launch_bounds__(kBlock, OURO_WAVES) k_tpraos_verify(ouro_tprao
   const Slot lane = slot_of(scratch, tid, kHdrLaneWords);
   const Slot res = lane + kLaneWords;
   const uint32_t opts = batch_opts(b);
+#if OURO_CLOCK_STAMPS
+  unsigned long long c0 = 0, r0 = 0;
+  if (threadIdx.x == 0) {
+    r0 = __builtin_amdgcn_s_memrealtime();
+    c0 = __builtin_amdgcn_s_memtime();
+  }
+#endif
   for (size_t i = tid; i < b.n; i += nth) {
 #if OURO_HDR_LOOP
     // one copy of the core dispatch, the core chosen at run time
@@ -143,6 +165,17 @@ __global__ void __launch_bounds__(kBlock, OURO_WAVES) k_tpraos_verify(ouro_tprao
     hdr_finish_item(b, i, opts, res, lane, verdict, beta_eta, beta_leader);
 #endif
   }
+#if OURO_CLOCK_STAMPS
+  __syncthreads();  // the whole workgroup's work inside the stamps
+  if (threadIdx.x == 0 && blockIdx.x < kClockSlots) {
+    const unsigned long long c1 = __builtin_amdgcn_s_memtime();
+    const unsigned long long r1 = __builtin_amdgcn_s_memrealtime();
+    g_clock_stamps[blockIdx.x][0] = c0;
+    g_clock_stamps[blockIdx.x][1] = c1;
+    g_clock_stamps[blockIdx.x][2] = r0;
+    g_clock_stamps[blockIdx.x][3] = r1;
+  }
+#endif
 }
 
 // Latency mode (k_tpraos_cores, k_tpraos_finish): kernels_lat.hip, its own
@@ -1702,6 +1735,26 @@ void ouro_tpraos_plan_destroy(ouro_tpraos_plan* p) { plan_free(p); }
 // library built with -DOURO_LAT_STAMPS=1 and run with OURO_LAT_STAMPS set;
 // returns the count, or -1 in the product build.
 int ouro_debug_lat_stamps(unsigned long long* out) { return lat_stamps_read(out); }
+
+// CLOCK PROBE (bench.py roofline.frac_clock): the last k_tpraos_verify
+// launch's per-workgroup {s_memtime, s_memtime, s_memrealtime, s_memrealtime}
+// at entry / exit, min(grid, max_slots) rows, from a -DOURO_CLOCK_STAMPS=1
+// build (lib/libouro_verify_clock.so); -1 in the product build.
+int ouro_debug_clock_stamps(unsigned long long* out, int max_slots) {
+#if OURO_CLOCK_STAMPS
+  if (!out || max_slots <= 0) return fail(OURO_EINVAL, "null buffer");
+  const int n = std::min(max_slots, kClockSlots);
+  if (hipDeviceSynchronize() != hipSuccess) return fail(OURO_EDEVICE, "sync");
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_clock_stamps), sizeof(unsigned long long) * 4 * n) !=
+      hipSuccess)
+    return fail(OURO_EDEVICE, "hipMemcpyFromSymbol");
+  return n;
+#else
+  (void)out;
+  (void)max_slots;
+  return -1;
+#endif
+}
 
 // ---- the host path, called explicitly (host_path.h) ----
 int ouro_ed25519_verify_batch_host(size_t n, const uint8_t* pk, const uint8_t* sig,

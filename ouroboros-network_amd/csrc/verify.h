@@ -370,6 +370,16 @@ constexpr uint32_t dsm_cfg(int nw1, int nw2, bool useB, int tab1 = 0, int tab2 =
 #ifndef OURO_PF_AT
 #define OURO_PF_AT 3
 #endif
+// A doubling of the lane chain: its products in lockstep (ge25519.h
+// ge_dbl_lockstep, 1, the default since round 4) or as written in ge_p2_dbl
+// (0, A/B).
+#ifndef OURO_DBL_LOCKSTEP
+#define OURO_DBL_LOCKSTEP 1
+#endif
+OURO_FI ge_p1p1 dsm_dbl(const ge_p1p1& t) {
+  if constexpr (OURO_DBL_LOCKSTEP) return ge_dbl_lockstep(t);
+  else return ge_p2_dbl(ge_p1p1_to_p2(t));
+}
 template <bool kQuad>
 OURO_FI void dsm_body(Slot lane, const int32_t* btab, uint32_t cfg) {
   const int nw1 = (int)(cfg & 0x7f), nw2 = (int)((cfg >> 8) & 0x7f);
@@ -447,12 +457,12 @@ OURO_FI void dsm_body(Slot lane, const int32_t* btab, uint32_t cfg) {
         for (int k = 0; k < 4; k++) t = ge_dbl_from_p1p1_quad(t);
       } else if (OURO_PF_AT == 0) {
 #pragma unroll OURO_DBL_UNROLL
-        for (int k = 0; k < 4; k++) t = ge_p2_dbl(ge_p1p1_to_p2(t));
+        for (int k = 0; k < 4; k++) t = dsm_dbl(t);
       } else {
 #pragma unroll 1
-        for (int k = 0; k < 3; k++) t = ge_p2_dbl(ge_p1p1_to_p2(t));
+        for (int k = 0; k < 3; k++) t = dsm_dbl(t);
         OURO_TOUCH_ENTRIES();
-        t = ge_p2_dbl(ge_p1p1_to_p2(t));
+        t = dsm_dbl(t);
       }
     }
 #undef OURO_TOUCH_ENTRIES

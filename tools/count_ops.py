@@ -14,12 +14,16 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tests"))
 
-import oracle_ffi as O  # noqa: E402
-
 SO = os.path.join(ROOT, "ouroboros-network_amd", "lib", "libouro_devhost_test.so")
 
 
 def main():
+    print(json.dumps(counts(), indent=1))
+
+
+def counts(header_only: bool = False):
+    """header_only: just the golden header through the throughput schedule
+    (no oracle-synthesised inputs; what bench.py reports)."""
     d = ctypes.CDLL(SO)
     nm, ns = ctypes.c_ulonglong(), ctypes.c_ulonglong()
 
@@ -28,6 +32,26 @@ def main():
         fn()
         d.dh_count_get(ctypes.byref(nm), ctypes.byref(ns))
         return {"mul": nm.value, "sq": ns.value, "M": nm.value + ns.value}
+
+    kats = json.load(open(os.path.join(ROOT, "tests", "golden", "reference_kats.json")))
+    from ouroboros_network_amd import header as H
+    import numpy as np
+
+    hd = H.parse_header(bytes.fromhex(kats["headers"][0]["raw"]))
+    # one golden header through tpraos.h's throughput schedule (shared key table,
+    # single-inversion finish)
+    batch = H.pack([hd], [bytes.fromhex(kats["headers"][0]["eta_alpha"])],
+                   [bytes.fromhex(kats["headers"][0]["leader_alpha"])], slots_per_kes_period=100)
+    st = batch.c_struct()
+    v, be, bl = np.zeros(1, np.uint8), np.zeros((1, 64), np.uint8), np.zeros((1, 64), np.uint8)
+    d.dh_tpraos_verify.argtypes = [ctypes.c_void_p, ctypes.c_int] + [ctypes.c_void_p] * 3
+    d.dh_tpraos_verify(ctypes.addressof(st), 0, v.ctypes.data, be.ctypes.data, bl.ctypes.data)
+    hdr = measure(lambda: d.dh_tpraos_verify(ctypes.addressof(st), 0, v.ctypes.data,
+                                             be.ctypes.data, bl.ctypes.data))
+    assert int(v[0]) & 0x0F == 15
+    if header_only:
+        return {"tpraos_header (throughput schedule)": hdr}
+    import oracle_ffi as O
 
     pk, sig, msg = O.synth_ed25519(1, first=0)
     # build the host copy of the fixed-base table outside the counted region
@@ -41,21 +65,9 @@ def main():
 
     hd = H.parse_header(bytes.fromhex(kats["headers"][0]["raw"]))
     kes = measure(lambda: d.dh_sum6kes_verify(hd.hot_vk, 0, hd.body, len(hd.body), hd.kes_sig))
-    # one golden header through tpraos.h's throughput schedule (shared key table,
-    # single-inversion finish)
-    batch = H.pack([hd], [bytes.fromhex(kats["headers"][0]["eta_alpha"])],
-                   [bytes.fromhex(kats["headers"][0]["leader_alpha"])], slots_per_kes_period=100)
-    st = batch.c_struct()
-    import numpy as np
-
-    v, be, bl = np.zeros(1, np.uint8), np.zeros((1, 64), np.uint8), np.zeros((1, 64), np.uint8)
-    d.dh_tpraos_verify.argtypes = [ctypes.c_void_p, ctypes.c_int] + [ctypes.c_void_p] * 3
-    hdr = measure(lambda: d.dh_tpraos_verify(ctypes.addressof(st), 0, O.p(v), O.p(be), O.p(bl)))
-    assert int(v[0]) & 0x0F == 15
-    res = {"ed25519_verify": ed, "vrf03_verify": vrf, "sum6kes_verify": kes,
-           "tpraos_header (throughput schedule)": hdr,
-           "canonical_M (SURVEY.md §8(d))": {"ed25519": 2983, "vrf": 7325, "header": 20616}}
-    print(json.dumps(res, indent=1))
+    return {"ed25519_verify": ed, "vrf03_verify": vrf, "sum6kes_verify": kes,
+            "tpraos_header (throughput schedule)": hdr,
+            "canonical_M (SURVEY.md §8(d))": {"ed25519": 2983, "vrf": 7325, "header": 20616}}
 
 
 if __name__ == "__main__":

@@ -31,6 +31,18 @@ def counters(path, kernel="k_tpraos_verify"):
     return dict(agg), len(n)
 
 
+def clock_ghz(path, kernel="k_tpraos_verify"):
+    """GRBM_GUI_ACTIVE / 8 (rocprofv3 sums the 8 XCDs) / dispatch wall time:
+    the clock the kernel ran at (MI355X_MICROARCH.md "DVFS give-back"; within
+    3 % of the in-kernel clock for dispatches of 10 ms or more)."""
+    with open(path) as f:
+        for r in csv.DictReader(f):
+            if kernel in r["Kernel_Name"] and r["Counter_Name"] == "GRBM_GUI_ACTIVE":
+                ns = float(r["End_Timestamp"]) - float(r["Start_Timestamp"])
+                return float(r["Counter_Value"]) / 8 / ns
+    return None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("round")
@@ -64,6 +76,9 @@ def main():
                                                    "SQ_ACTIVE_INST_ANY", "SQ_ACTIVE_INST_VALU")
                             if k in sq}
         out["valu_insts_per_header"] = sq.get("SQ_INSTS_VALU", 0) * 64 / args.pmc_headers / 64
+        out["valu_lane_insts_per_header"] = sq.get("SQ_INSTS_VALU", 0) * 64 / args.pmc_headers
+    if os.path.exists(os.path.join(d, "pmc_sq.csv")):
+        out["clock_ghz"] = clock_ghz(os.path.join(d, "pmc_sq.csv"))
     # the source the PMC passes measured: bench.py stamps it into its JSON line
     src = None
     bj = os.path.join(d, "bench_under_rocprof.json")
@@ -77,7 +92,9 @@ def main():
         json.dump(out, f, indent=1, sort_keys=True)
     with open(os.path.join(ROOT, "profiles", "pmc_traffic.json"), "w") as f:
         json.dump({"round": args.round, "source_hash": src,
-                   "k_tpraos_verify_bytes_per_launch_per_header": hbm / args.pmc_headers}, f, indent=1)
+                   "k_tpraos_verify_bytes_per_launch_per_header": hbm / args.pmc_headers,
+                   "valu_lane_insts_per_header": out.get("valu_lane_insts_per_header"),
+                   "clock_ghz": out.get("clock_ghz")}, f, indent=1)
     print(json.dumps(out, indent=1, sort_keys=True))
 
 
