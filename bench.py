@@ -329,7 +329,7 @@ CLOCK_SO = os.path.join(ROOT, "ouroboros-network_amd", "lib", "libouro_verify_cl
 DEVHOST_SO = os.path.join(ROOT, "ouroboros-network_amd", "lib", "libouro_devhost_test.so")
 
 
-def kernel_clock_ghz(hdr, stream, launches: int = 12):
+def kernel_clock_ghz(hdr, stream, launches: int = 36):
     """The shader clock k_tpraos_verify itself runs at on THIS box: the
     diagnostic build lib/libouro_verify_clock.so (-DOURO_CLOCK_STAMPS=1: the
     same kernel with s_memtime / s_memrealtime stamps at each workgroup's entry
@@ -964,10 +964,11 @@ def load_component_traffic():
 
 
 def single_item_leg(ed, hdr, iters: int = 300):
-    """Per-call wall latency of the ABI-identical single-item symbols (each a
-    one-item GPU batch: H2D, launch, D2H) next to the reference's own
-    libsodium call on the host -- the number a per-item Haskell FFI caller
-    would see (INTEGRATION.md steers such callers to batches)."""
+    """Per-call wall latency of the ABI-identical single-item symbols -- the
+    number a per-item Haskell FFI caller sees -- on both routes: the library's
+    host path (the default since round 4: the kernels' lane routines compiled
+    for the CPU) and the GPU (OURO_SINGLE_ITEM=gpu: a one-item batch, H2D,
+    one wave, D2H), next to the reference's own libsodium call on the host."""
     from ouroboros_network_amd import _native
 
     lib = _native.load()
@@ -995,17 +996,31 @@ def single_item_leg(ed, hdr, iters: int = 300):
                 "p99_us": round(float(np.percentile(t, 99)) * 1e6, 1)}
 
     shim = _native.load_shim()
+
+    def route(r):
+        old = os.environ.get("OURO_SINGLE_ITEM")
+        os.environ["OURO_SINGLE_ITEM"] = r
+        try:
+            return {
+                "ouro_ed25519_verify": lat(lambda i: lib.ouro_ed25519_verify(
+                    items[i][0], items[i][1], 32, items[i][2])),
+                "ouro_vrf03_verify": lat(lambda i: lib.ouro_vrf03_verify(
+                    out, vitems[i][0], vitems[i][1], vitems[i][2], 32)),
+                "crypto_vrf_ietfdraft03_verify (opt-in shim)": lat(
+                    lambda i: shim.crypto_vrf_ietfdraft03_verify(out, vitems[i][0], vitems[i][1],
+                                                                 vitems[i][2], 32))}
+        finally:
+            if old is None:
+                os.environ.pop("OURO_SINGLE_ITEM", None)
+            else:
+                os.environ["OURO_SINGLE_ITEM"] = old
+
     res = {"workload": f"{iters} single-item calls, valid synthetic items, one thread",
-           "routing": "each single-item symbol is one GPU round trip (H2D, one wave, D2H); "
-                      "include/ouro_verify.h routes per-item callers (n = 1) to "
-                      "libsodium / the fork and windows of >= 64 headers to plans",
-           "ouro_ed25519_verify": lat(lambda i: lib.ouro_ed25519_verify(
-               items[i][0], items[i][1], 32, items[i][2])),
-           "ouro_vrf03_verify": lat(lambda i: lib.ouro_vrf03_verify(
-               out, vitems[i][0], vitems[i][1], vitems[i][2], 32)),
-           "crypto_vrf_ietfdraft03_verify (opt-in shim)": lat(
-               lambda i: shim.crypto_vrf_ietfdraft03_verify(out, vitems[i][0], vitems[i][1],
-                                                            vitems[i][2], 32))}
+           "routing": "single items run on the library's host path by default "
+                      "(include/ouro_verify.h); OURO_SINGLE_ITEM=gpu sends them to the device",
+           "host_path": route("host"), "gpu": route("gpu")}
+    # the default route's figures at the top level (the names the ABI exports)
+    res.update(res["host_path"])
     if os.path.exists(SODIUM_SO):
         so = ctypes.CDLL(SODIUM_SO)
         so.sodium_init()
@@ -1258,6 +1273,10 @@ def main():
             "field_ops_per_header": ({"mul": work["field_mul"], "sq": work["field_sq"]}
                                      if work else None),
             "traffic": (round(traffic_per_header * n) if traffic_per_header else None),
+            "traffic_note": "HBM bytes per launch from the committed PMC pass named by "
+                            "traffic_round (FETCH_SIZE x 2 + WRITE_SIZE per the guide's gfx950 "
+                            "correction); traffic_matches_source says whether it measured this "
+                            "source",
             "traffic_per_header": (round(traffic_per_header, 1) if traffic_per_header else None),
             "algorithmic_bytes_per_header": 1537,
             "traffic_ratio": (round(traffic_per_header / 1537, 1) if traffic_per_header else None),
