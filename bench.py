@@ -588,6 +588,62 @@ def _plan_latency(hb, iters: int, nonce: bool):
     return lat, out
 
 
+def _plan_phases(hb, iters: int, nonce: bool):
+    """Where a window's wall time goes, to explain the latency tail (VERDICT
+    r03 item 5): the plan's submit (copy into pinned staging + graph launch)
+    and wait (until the results are in the caller's buffers) timed on the
+    host, and the GPU time of the graph (H2D, kernel, D2H) from events the
+    plan records around its launch (OURO_PLAN_TIMING; a separate pass, so the
+    headline windows carry no events).  host_gap = wall - gpu: launch latency
+    + completion wake-up + the host copies."""
+    from ouroboros_network_amd.tpraos import HeaderPlan
+
+    body_bytes = int(hb.body_len.astype(np.int64).sum())
+    plan = HeaderPlan(len(hb), body_bytes)
+    old = os.environ.get("OURO_PLAN_TIMING")
+    os.environ["OURO_PLAN_TIMING"] = "1"
+    try:
+        out = plan.run(hb, nonce=nonce)
+        s = hb.c_struct(out[3] if nonce else None)
+        P = lambda a: a.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
+        lib = plan._lib
+        sub, wait = lib.ouro_tpraos_plan_submit, lib.ouro_tpraos_plan_wait
+        gms = ctypes.c_float()
+        for _ in range(min(50, iters)):
+            assert sub(plan._p, ctypes.byref(s)) == 0
+            assert wait(plan._p, P(out[0]), P(out[1]), P(out[2])) == 0
+        ph = np.empty((iters, 3))
+        for k in range(iters):
+            t0 = time.perf_counter()
+            assert sub(plan._p, ctypes.byref(s)) == 0
+            t1 = time.perf_counter()
+            assert wait(plan._p, P(out[0]), P(out[1]), P(out[2])) == 0
+            t2 = time.perf_counter()
+            lib.ouro_debug_plan_gpu_ms(plan._p, ctypes.byref(gms))
+            ph[k] = (t1 - t0, t2 - t1, gms.value * 1e-3)
+    finally:
+        if old is None:
+            os.environ.pop("OURO_PLAN_TIMING", None)
+        else:
+            os.environ["OURO_PLAN_TIMING"] = old
+        plan.close()
+    wall = ph[:, 0] + ph[:, 1]
+    gap = wall - ph[:, 2]
+    us = lambda a, q: round(float(np.percentile(a, q)) * 1e6, 1)  # noqa: E731
+    pc = lambda a: {"p50_us": us(a, 50), "p99_us": us(a, 99), "p99_9_us": us(a, 99.9),  # noqa: E731
+                    "max_us": us(a, 100)}
+    worst = np.argsort(wall)[-5:][::-1]
+    return {"iters": iters, "wall": pc(wall), "submit": pc(ph[:, 0]), "wait": pc(ph[:, 1]),
+            "gpu_graph": pc(ph[:, 2]), "host_gap": pc(gap),
+            "slowest_windows_us": [{"wall": round(wall[i] * 1e6, 1),
+                                    "submit": round(ph[i, 0] * 1e6, 1),
+                                    "wait": round(ph[i, 1] * 1e6, 1),
+                                    "gpu_graph": round(ph[i, 2] * 1e6, 1)} for i in worst],
+            "note": "events around the graph launch (OURO_PLAN_TIMING) in a separate pass; "
+                    "host_gap = wall - gpu_graph (launch latency, completion wake-up, "
+                    "host copies)"}
+
+
 def _pcts(lat):
     ms = lambda q: round(float(np.percentile(lat, q)) * 1e3, 4)  # noqa: E731
     return {"p50_ms": ms(50), "p99_ms": ms(99), "p99_9_ms": ms(99.9), "max_ms": ms(100)}
@@ -659,7 +715,8 @@ def latency_leg(hdr, batch: int, iters: int, cpu_threads: int, cpu_iters: int, n
                         "(*_CLAIM_OK), VRF inputs from (slot, eta0) by mkSeed on the device, "
                         "eta nonce output requested",
             "iters": iters, **_pcts(nlat),
-            "all_strict_ok": bool((nout[0] == HDR_STRICT_OK).all()),
+            "phases": _plan_phases(nb, iters, nonce=True),
+            "all_strict_ok": bool(((nout[0] & HDR_STRICT_OK) == HDR_STRICT_OK).all()),
             "gpu_equals_cpu": bool((nout[0] == wv).all() and (nout[1] == wbe).all()
                                    and (nout[2] == wbl).all() and (nout[3] == wen).all())}
     return res
@@ -883,6 +940,73 @@ def raw_leg(n: int, npools: int, device, threads: int, chunk: int = 0, reps: int
     return res
 
 
+def integrity_leg(n: int, npools: int, device, reps: int = 3):
+    """Storage integrity straight from raw CBOR: the
+    KES-only verifyHeaderIntegrity
+    (ouroboros-consensus-shelley/src/Ouroboros/Consensus/Shelley/Ledger/Integrity.hs:20-44)
+    that the VolatileDB parser runs on every block at open (Storage/VolatileDB/
+    Impl/Parser.hs:66-85) and ImmutableDB chunk validation on every block of a
+    chunk (Storage/ImmutableDB/Impl/Validation.hs:358-365), over n synthetic
+    raw headers: HBM-resident (ouro_integrity_verify_cbor_device: device
+    slicer + Sum6KES kernel) and from pageable host memory in one call
+    (ouro_integrity_verify_cbor: host slicer, H2D, kernel, D2H).  Never `value`."""
+    import torch
+
+    from ouroboros_network_amd import _native
+
+    t, raw, rl = synth_raw_headers(n, npools, device)
+    lib = _native.load()
+    V = ctypes.c_void_p
+    st = torch.cuda.current_stream()
+    S = V(st.cuda_stream)
+    doff = torch.arange(n, dtype=torch.int64, device=device) * rl
+    dlen = torch.full((n,), rl, dtype=torch.int32, device=device)
+    nb = int(lib.ouro_tpraos_pack_bytes(n))
+    arena = torch.empty(nb, dtype=torch.uint8, device=device)
+    status = torch.empty(n, dtype=torch.uint8, device=device)
+    ver = torch.empty(n, dtype=torch.uint8, device=device)
+
+    def go():
+        _native.check(lib.ouro_integrity_verify_cbor_device(
+            S, V(raw.data_ptr()), raw.numel(), V(doff.data_ptr()), V(dlen.data_ptr()), n, 129600,
+            V(arena.data_ptr()), nb, V(status.data_ptr()), V(ver.data_ptr())),
+            "ouro_integrity_verify_cbor_device")
+
+    go()
+    torch.cuda.synchronize()
+    ts = []
+    for _ in range(reps):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(st)
+        go()
+        e1.record(st)
+        torch.cuda.synchronize()
+        ts.append(e0.elapsed_time(e1))
+    dms = min(ts)
+    all_ok = bool((ver == 1).all().item()) and bool((status == 0).all().item())
+    hraw = raw.cpu().numpy()
+    hoff = doff.cpu().numpy().astype(np.uint64)
+    hlen = dlen.cpu().numpy().astype(np.uint32)
+    hst = np.zeros(n, np.uint8)
+    hv = np.zeros(n, np.uint8)
+    P = lambda a: a.ctypes.data_as(V)  # noqa: E731
+
+    def host():
+        _native.check(lib.ouro_integrity_verify_cbor(P(hraw), hraw.size, P(hoff), P(hlen), n,
+                                                     129600, P(hst), P(hv)),
+                      "ouro_integrity_verify_cbor")
+
+    host()
+    th = min(_timed(host) for _ in range(reps))
+    return {"workload": f"{n} synthetic raw Shelley headers ({rl} B each), KES-only "
+                        "verifyHeaderIntegrity from raw CBOR",
+            "device_resident": {"headers_per_s": round(n / (dms * 1e-3), 1),
+                                "ms": round(dms, 3), "all_valid": all_ok},
+            "host_buffers_one_call": {"headers_per_s": round(n / th, 1), "ms": round(th * 1e3, 2),
+                                      "equals_device": bool((hv == ver.cpu().numpy()).all()),
+                                      "note": "host slicer + PCIe + kernel + D2H"}}
+
+
 def byron_leg(n: int, threads: int, reps: int = 3):
     """Raw Byron header CBOR -> verdicts: the golden
     Byron headers (tests/golden/reference_kats.json "byron_wire": N2N v1 and
@@ -1097,6 +1221,9 @@ def main():
     from ouroboros_network_amd import _native
 
     _native.load().ouro_set_device(gpu)
+    # this rank's host side on its GPU's NUMA node: threads
+    # created from here on inherit the binding; -1 = unknown (left alone)
+    numa_node = _native.load().ouro_bind_thread_to_device(gpu)
     if world > 1:
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
         if args.dist_backend == "nccl":
@@ -1203,7 +1330,8 @@ def main():
         # what the process group itself reports, and every rank's kernel time
         per_rank = [None] * world
         dist.all_gather_object(per_rank, {"rank": rank, "device": gpu, "headers": n,
-                                          "kernel_ms": round(kern_ms, 3)})
+                                          "kernel_ms": round(kern_ms, 3),
+                                          "numa_node": numa_node})
         dist_info = {"world_size_seen": dist.get_world_size(), "backend": dist.get_backend(),
                      "per_rank": per_rank}
         if strong:
@@ -1303,6 +1431,7 @@ def main():
                        "pools": args.pools, "body_bytes": blen,
                        "parallelism": f"shard{world}"},
             "all_valid": all_ok,
+            "numa_node": numa_node,
             "synth_s": round(syn_s, 2),
             "roofline": roof,
         }
@@ -1352,6 +1481,11 @@ def main():
                 out["raw_cbor"] = raw_leg(n, args.pools, device, cpu["usable"])
             except Exception as e:  # noqa: BLE001
                 out["raw_cbor"] = {"error": str(e)}
+        if not args.no_e2e and world == 1:
+            try:
+                out["integrity_cbor"] = integrity_leg(n, args.pools, device)
+            except Exception as e:  # noqa: BLE001
+                out["integrity_cbor"] = {"error": str(e)}
         if not args.no_e2e and world == 1:
             try:
                 out["byron_cbor"] = byron_leg(1 << 18, cpu["usable"])

@@ -300,6 +300,31 @@ int ouro_tpraos_pack_cbor_device(void *stream, const uint8_t *raw, size_t raw_by
                                  ouro_tpraos_batch *out, uint64_t *slot, uint8_t *era,
                                  uint8_t *status);
 
+/* Storage integrity, KES only, straight from raw header CBOR: replaces
+ * verifyHeaderIntegrity (ouroboros-consensus-shelley/src/Ouroboros/Consensus/
+ * Shelley/Ledger/Integrity.hs:20-44) as the storage layer runs it on every
+ * block -- the VolatileDB parser at open
+ * (ouroboros-consensus/src/Ouroboros/Consensus/Storage/VolatileDB/Impl/Parser.hs:66-85)
+ * and ImmutableDB chunk validation
+ * (.../Storage/ImmutableDB/Impl/Validation.hs:358-365).  Headers as for
+ * ouro_tpraos_pack_cbor; verdict[i] = 1 iff header i slices (status
+ * OURO_PACK_OK) and its Sum6KES signature verifies over the raw header body
+ * under the opcert's hot key at t = kesPeriod(slot) - c0 (0 when the slot's
+ * period is below c0; Integrity.hs:38-44).  The host slicer, then the Sum6KES
+ * kernel (host buffers, synchronous; a device error recomputes on the host
+ * path).  OURO_EINVAL for a span outside raw_bytes, NULLs or a zero period. */
+int ouro_integrity_verify_cbor(const uint8_t *raw, size_t raw_bytes, const uint64_t *off,
+                               const uint32_t *len, size_t n, uint64_t slots_per_kes_period,
+                               uint8_t *status, uint8_t *verdict);
+/* The same on raw headers already in device memory (device pointers; arena
+ * of ouro_tpraos_pack_bytes(n) bytes): the device slicer and the Sum6KES
+ * kernel enqueued on `stream`, not synchronised.  A rejected header's row is
+ * zeroed by the slicer, so its verdict is 0. */
+int ouro_integrity_verify_cbor_device(void *stream, const uint8_t *raw, size_t raw_bytes,
+                                      const uint64_t *off, const uint32_t *len, size_t n,
+                                      uint64_t slots_per_kes_period, void *arena,
+                                      size_t arena_bytes, uint8_t *status, uint8_t *verdict);
+
 /* Raw Byron header CBOR -> the inputs of its PBFT block-signature check
  * (SURVEY.md §8(f) row 4).  Replaces the per-header decode + message assembly
  * in front of ByronDSIGN.verifyDSIGN: Byron/Ledger/PBFT.hs:47-73 builds
@@ -383,6 +408,24 @@ int ouro_tpraos_verify_batch_lowlat(const ouro_tpraos_batch *b, uint8_t *verdict
  * serialised process-wide; the first shard error is returned after every
  * shard has finished.  Same results as ouro_tpraos_verify_batch. */
 int ouro_device_count(void);
+/* NUMA placement (each GPU's pinned staging NUMA-local).
+ * ouro_device_numa_node: the node of the device's PCI function in sysfs
+ * (-1 unknown; OURO_ENODEV for a bad index).  ouro_bind_thread_to_device:
+ * restricts the calling thread to that node's CPUs (within the process's
+ * cpuset) and prefers its memory, so the pinned staging the thread allocates
+ * afterwards lands there; returns the node or -1 (left alone).  The workers of
+ * ouro_tpraos_verify_batch_multi bind themselves to their device's node; all
+ * pinned staging is allocated with hipHostMallocNumaUser (the allocating
+ * thread's policy).  ouro_debug_multi_workers: per worker its device, node and
+ * the CPUs it is bound to (0 = unbound); returns the worker count. */
+int ouro_device_numa_node(int device);
+int ouro_bind_thread_to_device(int device);
+int ouro_debug_multi_workers(int *devices, int *nodes, int *cpus, int max);
+/* (test/diagnostic, no device: bind the calling thread to a PCI bus id's node
+ * as read from OURO_SYSFS_ROOT (default /sys); returns the node, *ncpus the
+ * CPUs bound.  ouro_debug_thread_cpus: the CPUs the caller may run on.) */
+int ouro_debug_numa_bind_pci(const char *busid, int *ncpus);
+int ouro_debug_thread_cpus(int *cpus, int max);
 int ouro_tpraos_verify_batch_multi(const ouro_tpraos_batch *b, const int *devices, int ndev,
                                    uint8_t *verdict, uint8_t *beta_eta, uint8_t *beta_leader);
 
@@ -448,6 +491,12 @@ int ouro_leader_check_batch_host(size_t n, const uint8_t *beta, const uint64_t *
  * device error.  Host-only. */
 int ouro_debug_host_path(unsigned long long *single_items,
                          unsigned long long *recomputed_batches);
+
+/* TIMING PROBE (bench.py latency phases): the GPU time in ms of the plan's
+ * last waited-for window -- events recorded around its graph launch (H2D,
+ * the latency kernel, D2H) when OURO_PLAN_TIMING was set in the environment
+ * at its submit; -1 otherwise. */
+int ouro_debug_plan_gpu_ms(ouro_tpraos_plan *plan, float *ms);
 
 /* Diagnostics: per-thread contexts (stream, scratch, staging) are pooled per
  * device; a thread borrows one on its first call and returns it when it

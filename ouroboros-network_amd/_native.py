@@ -114,6 +114,15 @@ SIGNATURES = {
     "ouro_debug_contexts": (_I, [_I, _P, _P]),
     "ouro_debug_lat_stamps": (_I, [_P]),
     "ouro_debug_clock_stamps": (_I, [_P, _I]),
+    "ouro_debug_plan_gpu_ms": (_I, [_P, _P]),
+    "ouro_device_numa_node": (_I, [_I]),
+    "ouro_bind_thread_to_device": (_I, [_I]),
+    "ouro_debug_multi_workers": (_I, [_P, _P, _P, _I]),
+    "ouro_debug_numa_bind_pci": (_I, [ctypes.c_char_p, _P]),
+    "ouro_debug_thread_cpus": (_I, [_P, _I]),
+    "ouro_integrity_verify_cbor": (_I, [_P, _SZ, _P, _P, _SZ, ctypes.c_uint64, _P, _P]),
+    "ouro_integrity_verify_cbor_device": (_I, [_P, _P, _SZ, _P, _P, _SZ, ctypes.c_uint64, _P,
+                                               _SZ, _P, _P]),
     "ouro_sum6kes_verify_batch": (_I, [_SZ, _P, _P, _P, _P, _P, _P, _P]),
     "ouro_tpraos_verify_batch": (_I, [ctypes.POINTER(TPraosBatch), _P, _P, _P]),
     "ouro_ed25519_verify_batch_device": (_I, [_P, _SZ, _P, _P, _P, _P, _P, _P]),

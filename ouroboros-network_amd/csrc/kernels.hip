@@ -27,6 +27,12 @@
 
 using namespace ouro;
 
+// numa.cpp: NUMA placement of a device's host side
+namespace ouro_numa {
+int node_of_pci(const char* busid);
+int bind_thread(int node);
+}  // namespace ouro_numa
+
 
 // ---------------------------------------------------------------- kernels ----
 
@@ -322,6 +328,14 @@ const void* kernel_ptr(int id) {
     case kLeader: return reinterpret_cast<const void*>(&k_leader_check);
     default: return reinterpret_cast<const void*>(&k_vrf03_proof_to_hash);
   }
+}
+
+// ---- NUMA placement (numa.cpp) ----
+// the NUMA node of device `dev` (sysfs numa_node of its PCI function), -1 if unknown
+int device_numa_node(int dev) {
+  char busid[64] = {0};
+  if (hipDeviceGetPCIBusId(busid, (int)sizeof(busid), dev) != hipSuccess) return -1;
+  return ouro_numa::node_of_pci(busid);
 }
 
 int current_device(int* dev) {
@@ -1057,7 +1071,9 @@ int pipe_chunk(PipeSlot& p, const ouro_tpraos_batch* b, size_t lo, size_t m, con
     if (p.h_out) OURO_HIP(hipHostFree(p.h_out));
     p.h_out = nullptr;
     p.h_cap = 0;
-    OURO_HIP(hipHostMalloc(reinterpret_cast<void**>(&p.h_out), kOutRow * m, hipHostMallocDefault));
+    // (hipHostMallocNumaUser: on the calling thread's NUMA policy -- a
+    // multi-device worker is bound to its GPU's node, numa.cpp)
+    OURO_HIP(hipHostMalloc(reinterpret_cast<void**>(&p.h_out), kOutRow * m, hipHostMallocNumaUser));
     p.h_cap = kOutRow * m;
   }
   OURO_HIP(hipMemcpyAsync(p.h_out, s.ver, m, hipMemcpyDeviceToHost, p.st));
@@ -1427,6 +1443,56 @@ int ouro_tpraos_pack_cbor_device(void* stream, const uint8_t* raw, size_t raw_by
   return launch_check();
 }
 
+// ---- storage integrity (KES only) over raw headers ----
+// verifyHeaderIntegrity (ouroboros-consensus-shelley/src/Ouroboros/Consensus/
+// Shelley/Ledger/Integrity.hs:20-44): Sum6KES of the raw header body under the
+// opcert's hot key at t = kesPeriod(slot) - c0 (0 below c0) -- the check the
+// VolatileDB parser runs on every block at open
+// (ouroboros-consensus/src/Ouroboros/Consensus/Storage/VolatileDB/Impl/Parser.hs:66-85)
+// and ImmutableDB chunk validation on every block of a chunk
+// (.../ImmutableDB/Impl/Validation.hs:358-365).  One call: the slicer (cbor.h,
+// kes_t_of = Integrity.hs:38-44), then the Sum6KES kernel on its rows; a header
+// the slicer rejects is 0 (its zeroed row cannot verify, and is masked too).
+int ouro_integrity_verify_cbor(const uint8_t* raw, size_t raw_bytes, const uint64_t* off,
+                               const uint32_t* len, size_t n, uint64_t slots_per_kes_period,
+                               uint8_t* status, uint8_t* verdict) {
+  if (n == 0) return OURO_OK;
+  if (!status || !verdict || !len || slots_per_kes_period == 0)
+    return fail(OURO_EINVAL, "null argument / zero period");
+  const size_t nb = ouro_tpraos_pack_bytes(n);
+  std::unique_ptr<uint8_t[]> arena(new (std::nothrow) uint8_t[nb]);
+  if (!arena) return fail(OURO_EDEVICE, "ouro_integrity_verify_cbor: out of host memory");
+  ouro_tpraos_batch b;
+  int rc = ouro_tpraos_pack_cbor(raw, raw_bytes, off, len, n, slots_per_kes_period, arena.get(),
+                                 nb, &b, nullptr, nullptr, status, 0);
+  if (rc) return fail(rc, "ouro_tpraos_pack_cbor: bad arguments");
+  // (host-buffer Sum6KES batch: a device error recomputes on the host path)
+  if ((rc = ouro_sum6kes_verify_batch(n, b.hot_vk, b.kes_t, b.body, b.body_off, b.body_len,
+                                      b.kes_sig, verdict)))
+    return rc;
+  for (size_t i = 0; i < n; i++) verdict[i] = status[i] == OURO_PACK_OK && verdict[i];
+  return OURO_OK;
+}
+
+// The same on raw headers already in device memory (raw, off, len, arena,
+// status, verdict: device pointers; arena >= ouro_tpraos_pack_bytes(n)):
+// the device slicer and the Sum6KES kernel enqueued on `stream`, not
+// synchronised.  A rejected header's zeroed row (OURO_PACK_*) cannot verify.
+int ouro_integrity_verify_cbor_device(void* stream, const uint8_t* raw, size_t raw_bytes,
+                                      const uint64_t* off, const uint32_t* len, size_t n,
+                                      uint64_t slots_per_kes_period, void* arena,
+                                      size_t arena_bytes, uint8_t* status, uint8_t* verdict) {
+  if (n == 0) return OURO_OK;
+  if (!verdict) return fail(OURO_EINVAL, "null verdict");
+  ouro_tpraos_batch b;
+  int rc = ouro_tpraos_pack_cbor_device(stream, raw, raw_bytes, off, len, n,
+                                        slots_per_kes_period, arena, arena_bytes, &b, nullptr,
+                                        nullptr, status);
+  if (rc) return rc;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  return launch_kes(st, n, b.hot_vk, b.kes_t, b.body, b.body_off, b.body_len, b.kes_sig, verdict);
+}
+
 int ouro_leader_check_batch_device(void* stream, size_t n, const uint8_t* beta,
                                    const uint64_t* sigma_num, const uint64_t* sigma_den,
                                    int64_t act_log_hi, uint64_t act_log_lo, int f_is_one,
@@ -1471,12 +1537,19 @@ struct ouro_tpraos_plan {
   uint32_t opts = 0;             // that batch's option bits (tpraos.h kOpt*)
   bool inflight = false;
   bool failed = false;           // its launch failed: wait recomputes it on the host path
+  // TIMING PROBE (OURO_PLAN_TIMING set at submit; bench.py latency phases):
+  // events around the graph launch on the plan's stream
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  bool timed = false;
+  float last_gpu_ms = -1.0f;
 };
 
 namespace {
 void plan_free(ouro_tpraos_plan* p) {
   if (!p) return;
   if (p->inflight && p->st) (void)hipStreamSynchronize(p->st);  // no DMA into freed staging
+  if (p->ev0) (void)hipEventDestroy(p->ev0);
+  if (p->ev1) (void)hipEventDestroy(p->ev1);
   if (p->exec) (void)hipGraphExecDestroy(p->exec);
   if (p->graph) (void)hipGraphDestroy(p->graph);
   if (p->h_in) (void)hipHostFree(p->h_in);
@@ -1507,8 +1580,8 @@ int plan_build(ouro_tpraos_plan* p) {
   }
   p->in_bytes = o;
   p->out_bytes = align16(p->cap) + 160 * p->cap;
-  OURO_HIP(hipHostMalloc(&p->h_in, p->in_bytes, hipHostMallocDefault));
-  OURO_HIP(hipHostMalloc(&p->h_out, p->out_bytes, hipHostMallocDefault));
+  OURO_HIP(hipHostMalloc(&p->h_in, p->in_bytes, hipHostMallocNumaUser));
+  OURO_HIP(hipHostMalloc(&p->h_out, p->out_bytes, hipHostMallocNumaUser));
   OURO_HIP(hipMalloc(&p->d_in, p->in_bytes));
   OURO_HIP(hipMalloc(&p->d_out, p->out_bytes));
   OURO_HIP(hipMalloc(&p->res, sizeof(int32_t) * slot_region_words(p->cap, kLatResWords)));
@@ -1677,7 +1750,14 @@ int ouro_tpraos_plan_submit(ouro_tpraos_plan* p, const ouro_tpraos_batch* b) {
   p->failed = false;
   const bool injected = injected_device_error();
   hipError_t e = hipSetDevice(p->dev);
+  p->timed = getenv("OURO_PLAN_TIMING") != nullptr;
+  if (p->timed && !p->ev0 && e == hipSuccess) {
+    e = hipEventCreate(&p->ev0);
+    if (e == hipSuccess) e = hipEventCreate(&p->ev1);
+  }
+  if (p->timed && e == hipSuccess) e = hipEventRecord(p->ev0, p->st);
   if (e == hipSuccess && !injected) e = hipGraphLaunch(p->exec, p->st);
+  if (p->timed && e == hipSuccess) e = hipEventRecord(p->ev1, p->st);
   if (e != hipSuccess || injected) {
     fail(OURO_EDEVICE, std::string("plan launch: ") +
                            (e != hipSuccess ? hipGetErrorString(e) : "injected device error"));
@@ -1710,6 +1790,8 @@ int ouro_tpraos_plan_wait(ouro_tpraos_plan* p, uint8_t* verdict, uint8_t* beta_e
     p->failed = false;
     return or_host(rc, [&] { return ouro_host::hdr_batch(&hb, verdict, beta_eta, beta_leader); });
   }
+  p->last_gpu_ms = -1.0f;
+  if (p->timed) (void)hipEventElapsedTime(&p->last_gpu_ms, p->ev0, p->ev1);
   const uint8_t* o = p->h_out + align16(p->cap);
   memcpy(verdict, p->h_out, n);
   if (beta_eta) memcpy(beta_eta, o, 64 * n);
@@ -1805,6 +1887,15 @@ int ouro_leader_check_batch_host(size_t n, const uint8_t* beta, const uint64_t* 
                                  verdict);
 }
 
+// TIMING PROBE: the GPU time of the plan's last waited-for window (events
+// around its graph launch: H2D, the latency kernel, D2H), recorded when
+// OURO_PLAN_TIMING was set at its submit; -1 otherwise.
+int ouro_debug_plan_gpu_ms(ouro_tpraos_plan* p, float* ms) {
+  if (!p || !ms) return fail(OURO_EINVAL, "null argument");
+  *ms = p->last_gpu_ms;
+  return OURO_OK;
+}
+
 // Items the host path has verified: single items routed there, and host-
 // buffer batches recomputed there after a device error.
 int ouro_debug_host_path(unsigned long long* single_items, unsigned long long* recomputed_batches) {
@@ -1838,11 +1929,16 @@ struct Worker {
   std::condition_variable cv;
   bool has_job = false, done = false;
   int dev = 0, rc = OURO_OK;
+  int numa_node = -1, bound_cpus = 0;
   std::string err;
   ouro_tpraos_batch shard{};
   uint8_t *verdict = nullptr, *be = nullptr, *bl = nullptr;
 
   void loop() {
+    // this worker's host side -- its copies, its pinned staging (allocated
+    // below with hipHostMallocNumaUser), its callbacks -- on the GPU's node
+    numa_node = device_numa_node(dev);
+    if (numa_node >= 0) bound_cpus = ouro_numa::bind_thread(numa_node);
     for (;;) {
       std::unique_lock<std::mutex> lk(mu);
       cv.wait(lk, [&] { return has_job; });
@@ -1904,6 +2000,32 @@ int ouro_device_count(void) {
   int count = 0;
   if (hipGetDeviceCount(&count) != hipSuccess) return 0;
   return count;
+}
+
+int ouro_device_numa_node(int device) {
+  const int count = ouro_device_count();
+  if (device < 0 || device >= count) return fail(OURO_ENODEV, "no such device");
+  return device_numa_node(device);
+}
+
+int ouro_bind_thread_to_device(int device) {
+  const int node = ouro_device_numa_node(device);
+  if (node >= 0) ouro_numa::bind_thread(node);
+  return node;
+}
+
+int ouro_debug_multi_workers(int* devices, int* nodes, int* cpus, int max) {
+  std::lock_guard<std::mutex> guard(g_multi_mu);
+  int k = 0;
+  for (auto& kv : g_workers) {
+    if (k < max) {
+      if (devices) devices[k] = kv.second->dev;
+      if (nodes) nodes[k] = kv.second->numa_node;
+      if (cpus) cpus[k] = kv.second->bound_cpus;
+    }
+    k++;
+  }
+  return k;
 }
 
 int ouro_tpraos_verify_batch_multi(const ouro_tpraos_batch* b, const int* devices, int ndev,

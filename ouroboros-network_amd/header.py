@@ -385,3 +385,49 @@ def mk_seed(universal_nonce: Optional[bytes], slot: int, epoch_nonce: Optional[b
     if universal_nonce is None:
         return h
     return bytes(a ^ b for a, b in zip(h, universal_nonce))
+
+
+def verify_integrity_cbor(raw_headers, slots_per_kes_period: int, host: bool = False):
+    """verifyHeaderIntegrity over raw headers (KES only; the storage layer's
+    check, ouroboros-consensus-shelley/src/Ouroboros/Consensus/Shelley/Ledger/
+    Integrity.hs:20-44): returns (valid bool array, slicer status array).
+    Default: ouro_integrity_verify_cbor (host slicer + the Sum6KES kernel).
+    host=True: the same slicer, then the library's host path
+    (ouro_sum6kes_verify_batch_host) -- no device touched."""
+    import ctypes
+
+    from . import _native
+    if isinstance(raw_headers, tuple) and len(raw_headers) == 3:
+        buf, off, ln = raw_headers
+        buf = np.frombuffer(buf, np.uint8) if isinstance(buf, (bytes, bytearray)) else \
+            np.ascontiguousarray(buf, np.uint8).reshape(-1)
+        off = np.ascontiguousarray(off, np.uint64)
+        ln = np.ascontiguousarray(ln, np.uint32)
+    else:
+        items = [bytes(r) for r in raw_headers]
+        ln = np.array([len(r) for r in items], np.uint32)
+        off = np.zeros(len(items), np.uint64)
+        if len(items) > 1:
+            off[1:] = np.cumsum(ln[:-1], dtype=np.uint64)
+        buf = np.frombuffer(b"".join(items) or b"\0", np.uint8)
+    n = int(off.size)
+    status = np.zeros(max(n, 1), np.uint8)
+    verdict = np.zeros(max(n, 1), np.uint8)
+    if n == 0:
+        return verdict[:0].astype(bool), status[:0]
+    ptr = lambda a: a.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
+    lib = _native.load()
+    if not host:
+        rc = lib.ouro_integrity_verify_cbor(ptr(buf), buf.size, ptr(off), ptr(ln), n,
+                                            slots_per_kes_period, ptr(status), ptr(verdict))
+        _native.check(rc, "ouro_integrity_verify_cbor")
+        return verdict[:n].astype(bool), status[:n]
+    p = pack_cbor((buf, off, ln), slots_per_kes_period=slots_per_kes_period, seeds=True,
+                  claimed=False)
+    b = p.batch
+    rc = lib.ouro_sum6kes_verify_batch_host(n, ptr(b.hot_vk), ptr(b.kes_t), ptr(b.body),
+                                            ptr(b.body_off), ptr(b.body_len), ptr(b.kes_sig),
+                                            ptr(verdict))
+    _native.check(rc, "ouro_sum6kes_verify_batch_host")
+    ok = (verdict[:n] != 0) & (p.status == PACK_OK)
+    return ok, p.status.copy()
