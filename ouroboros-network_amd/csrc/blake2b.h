@@ -22,7 +22,30 @@ constexpr uint8_t kB2bSigma[12][16] = {
     {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15},
     {14, 10, 4, 8, 9, 15, 13, 6, 1, 12, 0, 2, 11, 7, 5, 3}};
 
-OURO_FI uint64_t b2b_rotr(uint64_t x, int n) { return (x >> n) | (x << (64 - n)); }
+// G's rotations (32, 24, 16, 63; compile-time n).  On the device two
+// v_alignbit_b32 per rotation (a half swap for 32): LLVM writes the shift form
+// as a 64-bit shift pair and two ORs, four instructions (OURO_B2B_ALIGNBIT=0:
+// that form, for A/B)
+#ifndef OURO_B2B_ALIGNBIT
+#define OURO_B2B_ALIGNBIT 1
+#endif
+OURO_FI uint64_t b2b_rotr(uint64_t x, int n) {
+#if defined(__HIP_DEVICE_COMPILE__) && OURO_B2B_ALIGNBIT
+  const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+  if (n == 32) return ((uint64_t)lo << 32) | hi;
+  uint32_t rl, rh;
+  if (n < 32) {
+    rl = __builtin_amdgcn_alignbit(hi, lo, n);
+    rh = __builtin_amdgcn_alignbit(lo, hi, n);
+  } else {
+    rl = __builtin_amdgcn_alignbit(lo, hi, n - 32);
+    rh = __builtin_amdgcn_alignbit(hi, lo, n - 32);
+  }
+  return ((uint64_t)rh << 32) | rl;
+#else
+  return (x >> n) | (x << (64 - n));
+#endif
+}
 
 // out = Blake2b-256 of the first `len` <= 64 bytes of in (16 little-endian
 // 32-bit words; bytes past len must be zero).  One final compression with

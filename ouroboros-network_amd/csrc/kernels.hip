@@ -1139,7 +1139,8 @@ int hdr_batch_once(const ouro_tpraos_batch* b, const HdrOut& o, bool lowlat) {
     int32_t* res = sg.out<int32_t>(slot_region_words(n, kLatResWords));
     int32_t* scr = sg.out<int32_t>(lowlat_scratch_words(ds, n));
     if (sg.rc) return sg.rc;
-    // the fused launch's arrival counters start at zero (its tails reset them)
+    // the arrival records are generation-tagged (generation 1 here) and never
+    // reset by the kernel: this one-shot buffer starts from zero
     OURO_HIP(hipMemsetAsync(res, 0, sizeof(int32_t) * slot_region_words(n, kLatResWords), st));
     // (nw is read by the H2D above; this frame outlives the sync below)
     if ((rc = launch_lowlat(st, s.d, d_n, n, res, scr, s.ver, s.be, s.bl))) return rc;
@@ -1585,7 +1586,8 @@ int plan_build(ouro_tpraos_plan* p) {
   OURO_HIP(hipMalloc(&p->d_in, p->in_bytes));
   OURO_HIP(hipMalloc(&p->d_out, p->out_bytes));
   OURO_HIP(hipMalloc(&p->res, sizeof(int32_t) * slot_region_words(p->cap, kLatResWords)));
-  // the fused launch's arrival counters start at zero (its tails reset them)
+  // the arrival records are generation-tagged (each submit bumps the plan's
+  // generation) and never reset by the kernel; they start from zero once here
   OURO_HIP(hipMemset(p->res, 0, sizeof(int32_t) * slot_region_words(p->cap, kLatResWords)));
   OURO_HIP(hipMalloc(&p->scratch, sizeof(int32_t) * lowlat_scratch_words(ds, p->cap)));
   memset(p->h_in, 0, p->in_bytes);

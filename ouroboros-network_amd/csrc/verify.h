@@ -523,7 +523,9 @@ OURO_FI void dsm_body(Slot lane, const int32_t* btab, uint32_t cfg) {
   st_fe(lane + kSlotOut, r.X);
   st_fe(lane + kSlotOut + 12, r.Y);
   st_fe(lane + kSlotOut + 24, r.Z);
-  // keeps the prefetch loads alive; limbs are < 2^27, so this never stores
+  // keeps the prefetch loads alive.  The XOR can equal the guard (packed
+  // table entries make word 0 full-width), and then this store happens on
+  // purpose: it lands on Z's padding word kSlotOut+35, which nothing reads
   if (prefetch == 0xffffffffu) stg1(lane.word(kSlotOut + 35), (int32_t)prefetch);
 }
 OURO_NI void dsm_lane(Slot lane, const int32_t* btab, uint32_t cfg) {
