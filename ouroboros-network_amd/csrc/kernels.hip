@@ -1506,6 +1506,15 @@ int ouro_leader_check_batch_device(void* stream, size_t n, const uint8_t* beta,
 
 }  // extern "C"
 
+// A plan's window read straight from its pinned input block by a copy kernel
+// (OURO_PLAN_STAGE >= 1; A/B against the DMA copy node): one 16-B load per
+// thread, every load of the window in flight at once.
+__global__ void __launch_bounds__(256) k_plan_stage(const uint4* __restrict__ src,
+                                                    uint4* __restrict__ dst, size_t n16) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n16) dst[i] = src[i];
+}
+
 // ---- captured plans: pinned staging + hipGraph (H2D, 2 kernels, D2H) --------
 // The packed input block: 16 bytes {n, option bits (tpraos.h kOpt*), the
 // launch's generation (wide_cores.h arrive_last), 0}, then
@@ -1543,6 +1552,8 @@ struct ouro_tpraos_plan {
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   bool timed = false;
   float last_gpu_ms = -1.0f;
+  int stage = 0;  // OURO_PLAN_STAGE at capture (plan_build)
+  int spin = 0;   // OURO_PLAN_SPIN at capture: wait spins on hipStreamQuery
 };
 
 namespace {
@@ -1617,8 +1628,29 @@ int plan_build(ouro_tpraos_plan* p) {
   uint8_t* dbe = dver + align16(p->cap);
   uint8_t* dbl = dbe + 64 * p->cap;
   b.eta_nonce = dbl + 64 * p->cap;  // written only when the option bit says so
+  // OURO_PLAN_STAGE (A/B of the window's copies, read here once): 0 = DMA
+  // copy nodes in and out; 1 = a copy kernel reads the pinned input block;
+  // 2 = that, and the results written straight into the pinned output block
+  if (const char* e = getenv("OURO_PLAN_STAGE")) p->stage = atoi(e);
+  if (const char* e = getenv("OURO_PLAN_SPIN")) p->spin = atoi(e);
+  if (p->stage >= 2) {
+    void* hout = nullptr;
+    OURO_HIP(hipHostGetDevicePointer(&hout, p->h_out, 0));
+    dver = static_cast<uint8_t*>(hout);
+    dbe = dver + align16(p->cap);
+    dbl = dbe + 64 * p->cap;
+    b.eta_nonce = dbl + 64 * p->cap;
+  }
   OURO_HIP(hipStreamBeginCapture(p->st, hipStreamCaptureModeThreadLocal));
-  OURO_HIP(hipMemcpyAsync(p->d_in, p->h_in, p->in_bytes, hipMemcpyHostToDevice, p->st));
+  if (p->stage >= 1) {
+    void* hin = nullptr;
+    OURO_HIP(hipHostGetDevicePointer(&hin, p->h_in, 0));
+    const size_t n16 = p->in_bytes / 16;  // in_bytes is a multiple of 16
+    hipLaunchKernelGGL(k_plan_stage, dim3((unsigned)((n16 + 255) / 256)), dim3(256), 0, p->st,
+                       static_cast<const uint4*>(hin), reinterpret_cast<uint4*>(p->d_in), n16);
+  } else {
+    OURO_HIP(hipMemcpyAsync(p->d_in, p->h_in, p->in_bytes, hipMemcpyHostToDevice, p->st));
+  }
   rc = launch_lowlat(p->st, b, reinterpret_cast<const uint32_t*>(p->d_in), p->cap, p->res,
                      p->scratch, dver, dbe, dbl);
   if (rc) {
@@ -1626,7 +1658,8 @@ int plan_build(ouro_tpraos_plan* p) {
     (void)hipStreamEndCapture(p->st, &g);
     return rc;
   }
-  OURO_HIP(hipMemcpyAsync(p->h_out, p->d_out, p->out_bytes, hipMemcpyDeviceToHost, p->st));
+  if (p->stage < 2)
+    OURO_HIP(hipMemcpyAsync(p->h_out, p->d_out, p->out_bytes, hipMemcpyDeviceToHost, p->st));
   OURO_HIP(hipStreamEndCapture(p->st, &p->graph));
   OURO_HIP(hipGraphInstantiate(&p->exec, p->graph, nullptr, nullptr, 0));
   return OURO_OK;
@@ -1781,6 +1814,11 @@ int ouro_tpraos_plan_wait(ouro_tpraos_plan* p, uint8_t* verdict, uint8_t* beta_e
   int rc = OURO_OK;
   if (!p->failed) {
     hipError_t e = hipSetDevice(p->dev);
+    if (e == hipSuccess && p->spin) {
+      // poll the stream instead of the runtime's wait, which may sleep on the
+      // completion interrupt
+      while ((e = hipStreamQuery(p->st)) == hipErrorNotReady) __builtin_ia32_pause();
+    }
     if (e == hipSuccess) e = hipStreamSynchronize(p->st);
     if (e != hipSuccess) rc = fail(OURO_EDEVICE, std::string("plan wait: ") + hipGetErrorString(e));
   } else {
