@@ -608,19 +608,20 @@ def _plan_phases(hb, iters: int, nonce: bool):
         P = lambda a: a.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
         lib = plan._lib
         sub, wait = lib.ouro_tpraos_plan_submit, lib.ouro_tpraos_plan_wait
-        gms = ctypes.c_float()
+        gms, cus, lus = ctypes.c_float(), ctypes.c_float(), ctypes.c_float()
         for _ in range(min(50, iters)):
             assert sub(plan._p, ctypes.byref(s)) == 0
             assert wait(plan._p, P(out[0]), P(out[1]), P(out[2])) == 0
-        ph = np.empty((iters, 3))
+        ph = np.empty((iters, 5))
         for k in range(iters):
             t0 = time.perf_counter()
             assert sub(plan._p, ctypes.byref(s)) == 0
             t1 = time.perf_counter()
             assert wait(plan._p, P(out[0]), P(out[1]), P(out[2])) == 0
             t2 = time.perf_counter()
-            lib.ouro_debug_plan_gpu_ms(plan._p, ctypes.byref(gms))
-            ph[k] = (t1 - t0, t2 - t1, gms.value * 1e-3)
+            lib.ouro_debug_plan_timing(plan._p, ctypes.byref(gms), ctypes.byref(cus),
+                                       ctypes.byref(lus))
+            ph[k] = (t1 - t0, t2 - t1, gms.value * 1e-3, cus.value * 1e-6, lus.value * 1e-6)
     finally:
         if old is None:
             os.environ.pop("OURO_PLAN_TIMING", None)
@@ -633,7 +634,8 @@ def _plan_phases(hb, iters: int, nonce: bool):
     pc = lambda a: {"p50_us": us(a, 50), "p99_us": us(a, 99), "p99_9_us": us(a, 99.9),  # noqa: E731
                     "max_us": us(a, 100)}
     worst = np.argsort(wall)[-5:][::-1]
-    return {"iters": iters, "wall": pc(wall), "submit": pc(ph[:, 0]), "wait": pc(ph[:, 1]),
+    return {"iters": iters, "wall": pc(wall), "submit": pc(ph[:, 0]),
+            "submit_copy": pc(ph[:, 3]), "submit_graph_launch": pc(ph[:, 4]), "wait": pc(ph[:, 1]),
             "gpu_graph": pc(ph[:, 2]), "host_gap": pc(gap),
             "slowest_windows_us": [{"wall": round(wall[i] * 1e6, 1),
                                     "submit": round(ph[i, 0] * 1e6, 1),

@@ -492,11 +492,13 @@ int ouro_leader_check_batch_host(size_t n, const uint8_t *beta, const uint64_t *
 int ouro_debug_host_path(unsigned long long *single_items,
                          unsigned long long *recomputed_batches);
 
-/* TIMING PROBE (bench.py latency phases): the GPU time in ms of the plan's
- * last waited-for window -- events recorded around its graph launch (H2D,
- * the latency kernel, D2H) when OURO_PLAN_TIMING was set in the environment
- * at its submit; -1 otherwise. */
-int ouro_debug_plan_gpu_ms(ouro_tpraos_plan *plan, float *ms);
+/* TIMING PROBE (bench.py latency phases) of the plan's last waited-for
+ * window, when OURO_PLAN_TIMING was set in the environment at its submit (-1
+ * otherwise): gpu_ms = events recorded around its graph launch (H2D, the
+ * latency kernel, D2H); copy_us / launch_us = host time of submit's copy into
+ * the pinned block and of the graph launch call.  Any pointer may be NULL. */
+int ouro_debug_plan_timing(ouro_tpraos_plan *plan, float *gpu_ms, float *copy_us,
+                           float *launch_us);
 
 /* Diagnostics: per-thread contexts (stream, scratch, staging) are pooled per
  * device; a thread borrows one on its first call and returns it when it

@@ -114,7 +114,7 @@ SIGNATURES = {
     "ouro_debug_contexts": (_I, [_I, _P, _P]),
     "ouro_debug_lat_stamps": (_I, [_P]),
     "ouro_debug_clock_stamps": (_I, [_P, _I]),
-    "ouro_debug_plan_gpu_ms": (_I, [_P, _P]),
+    "ouro_debug_plan_timing": (_I, [_P, _P, _P, _P]),
     "ouro_device_numa_node": (_I, [_I]),
     "ouro_bind_thread_to_device": (_I, [_I]),
     "ouro_debug_multi_workers": (_I, [_P, _P, _P, _I]),

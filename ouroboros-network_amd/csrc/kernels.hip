@@ -7,6 +7,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <cstdio>
 #include <cstring>
@@ -1552,7 +1553,8 @@ struct ouro_tpraos_plan {
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   bool timed = false;
   float last_gpu_ms = -1.0f;
-  int stage = 0;  // OURO_PLAN_STAGE at capture (plan_build)
+  float copy_us = -1.0f, launch_us = -1.0f;  // host side of its last submit
+  int stage = 2;  // OURO_PLAN_STAGE at capture (plan_build)
   int spin = 0;   // OURO_PLAN_SPIN at capture: wait spins on hipStreamQuery
 };
 
@@ -1628,9 +1630,12 @@ int plan_build(ouro_tpraos_plan* p) {
   uint8_t* dbe = dver + align16(p->cap);
   uint8_t* dbl = dbe + 64 * p->cap;
   b.eta_nonce = dbl + 64 * p->cap;  // written only when the option bit says so
-  // OURO_PLAN_STAGE (A/B of the window's copies, read here once): 0 = DMA
-  // copy nodes in and out; 1 = a copy kernel reads the pinned input block;
-  // 2 = that, and the results written straight into the pinned output block
+  // OURO_PLAN_STAGE (the window's copies, read here once): 0 = copy nodes in
+  // and out; 1 = a copy kernel reads the pinned input block; 2 (default) =
+  // that, and the latency kernel writes the results straight into the pinned
+  // output block -- one node fewer, 2-3 us of the window (profiles/r04c:
+  // ablat_plan_stage.json, lat_phases.json; the copy nodes' own time is
+  // ~5 us each, the rest is the graph's node-to-node dispatch)
   if (const char* e = getenv("OURO_PLAN_STAGE")) p->stage = atoi(e);
   if (const char* e = getenv("OURO_PLAN_SPIN")) p->spin = atoi(e);
   if (p->stage >= 2) {
@@ -1766,6 +1771,8 @@ int ouro_tpraos_plan_submit(ouro_tpraos_plan* p, const ouro_tpraos_batch* b) {
       b->ocert_sigma, b->kes_t,           b->kes_sig,     w.span() ? b->body + w.lo : nullptr,
       w.off.data(),  b->body_len,         b->eta_output,  b->leader_output, b->slot,
       b->epoch_nonce};
+  p->timed = getenv("OURO_PLAN_TIMING") != nullptr;
+  const auto tc0 = std::chrono::steady_clock::now();
   if (b->slot) src[kFEtaAlpha] = src[kFLeaderAlpha] = nullptr;  // derived on the device
   else src[kFEpochNonce] = nullptr;
   for (int f = 0; f < kPlanFields; f++) {
@@ -1773,6 +1780,8 @@ int ouro_tpraos_plan_submit(ouro_tpraos_plan* p, const ouro_tpraos_batch* b) {
                                             : (kFieldBytes[f] == 0 ? w.span() : 32);
     if (bytes && src[f]) memcpy(p->h_in + p->off[f], src[f], bytes);
   }
+  if (p->timed)
+    p->copy_us = std::chrono::duration<float, std::micro>(std::chrono::steady_clock::now() - tc0).count();
   if (p->gen && getenv("OURO_TEST_PLAN_POISON") && (rc = plan_poison(p))) return rc;
   // every launch a new generation, so no counter an earlier launch left
   // behind (one that never completed) is ever counted again
@@ -1785,13 +1794,15 @@ int ouro_tpraos_plan_submit(ouro_tpraos_plan* p, const ouro_tpraos_batch* b) {
   p->failed = false;
   const bool injected = injected_device_error();
   hipError_t e = hipSetDevice(p->dev);
-  p->timed = getenv("OURO_PLAN_TIMING") != nullptr;
   if (p->timed && !p->ev0 && e == hipSuccess) {
     e = hipEventCreate(&p->ev0);
     if (e == hipSuccess) e = hipEventCreate(&p->ev1);
   }
   if (p->timed && e == hipSuccess) e = hipEventRecord(p->ev0, p->st);
+  const auto tl0 = std::chrono::steady_clock::now();
   if (e == hipSuccess && !injected) e = hipGraphLaunch(p->exec, p->st);
+  if (p->timed)
+    p->launch_us = std::chrono::duration<float, std::micro>(std::chrono::steady_clock::now() - tl0).count();
   if (p->timed && e == hipSuccess) e = hipEventRecord(p->ev1, p->st);
   if (e != hipSuccess || injected) {
     fail(OURO_EDEVICE, std::string("plan launch: ") +
@@ -1930,9 +1941,11 @@ int ouro_leader_check_batch_host(size_t n, const uint8_t* beta, const uint64_t* 
 // TIMING PROBE: the GPU time of the plan's last waited-for window (events
 // around its graph launch: H2D, the latency kernel, D2H), recorded when
 // OURO_PLAN_TIMING was set at its submit; -1 otherwise.
-int ouro_debug_plan_gpu_ms(ouro_tpraos_plan* p, float* ms) {
-  if (!p || !ms) return fail(OURO_EINVAL, "null argument");
-  *ms = p->last_gpu_ms;
+int ouro_debug_plan_timing(ouro_tpraos_plan* p, float* gpu_ms, float* copy_us, float* launch_us) {
+  if (!p) return fail(OURO_EINVAL, "null plan");
+  if (gpu_ms) *gpu_ms = p->last_gpu_ms;
+  if (copy_us) *copy_us = p->timed ? p->copy_us : -1.0f;
+  if (launch_us) *launch_us = p->timed ? p->launch_us : -1.0f;
   return OURO_OK;
 }
 
