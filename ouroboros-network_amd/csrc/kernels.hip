@@ -185,6 +185,76 @@ __global__ void __launch_bounds__(kBlock, OURO_WAVES) k_tpraos_verify(ouro_tprao
 #endif
 }
 
+// ---- the split header kernel (OURO_HDR_SPLIT, round 4) -----------------------
+// The same cores as k_tpraos_verify in three launches per chunk of headers, so
+// the double-scalar multiplications -- ~70 % of a header's time, and code
+// whose chains fit in 128 VGPRs -- run at OURO_DSM_WAVES waves per SIMD while
+// the decodes, hashes, table builds and the finish keep the 2-wave budget they
+// need (3 waves spill there: +2.7 %, profiles/r04b/ab_waves_w2_vs_w3.json):
+//   k_hdr_pre   header li of the chunk: every core's kPhasePre into its own
+//               task slot (core * chunk + li), flags into the header's record;
+//   k_hdr_dsm   task t: dsm_lane with the cfg the pre phase left in the slot
+//               (t = core * chunk + li: a wave's 64 tasks are one core of 64
+//               consecutive headers, the same grouping the pre phase's
+//               wave_max_small saw, so the window count is wave-uniform);
+//   k_hdr_post  header li: every core's kPhasePost, then the finish.
+#ifndef OURO_DSM_WAVES
+#define OURO_DSM_WAVES 4
+#endif
+constexpr int kHdrResWords = round_slot(kResWords);
+__global__ void __launch_bounds__(kBlock, OURO_WAVES) k_hdr_pre(ouro_tpraos_batch b, size_t base,
+                                                               size_t count, size_t chunk,
+                                                               int32_t* tasks, int32_t* res_buf,
+                                                               const int32_t* __restrict__ btab) {
+  const size_t nth = (size_t)gridDim.x * blockDim.x;
+  const uint32_t opts = batch_opts(b);
+  for (size_t li = (size_t)blockIdx.x * blockDim.x + threadIdx.x; li < count; li += nth) {
+    const size_t i = base + li;
+    const Slot res = slot_of(res_buf, li, kHdrResWords);
+    const Slot ukey = slot_of(tasks, (size_t)kCoreUe * chunk + li, kSlotWords);
+#pragma unroll 1
+    for (int c = kCoreOcert; c <= kCoreVl; c++)
+      hdr_core(b, i, opts, c, slot_of(tasks, (size_t)c * chunk + li, kSlotWords), res, btab, true,
+               false, false, kPhasePre, ukey);
+  }
+}
+__global__ void __launch_bounds__(kBlock, OURO_DSM_WAVES) k_hdr_dsm(size_t count, size_t chunk,
+                                                                   int32_t* tasks,
+                                                                   const int32_t* __restrict__ btab) {
+  const size_t nth = (size_t)gridDim.x * blockDim.x;
+  const size_t ntasks = (size_t)kHdrCores * chunk;
+  for (size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x; t < ntasks; t += nth) {
+    if (t % chunk >= count) continue;  // the last chunk's unused headers
+    const Slot s = slot_of(tasks, t, kSlotWords);
+    dsm_lane_dsm_launch(s, btab, (uint32_t)ldg1(s.word(kSlotCfg)));
+  }
+}
+__global__ void __launch_bounds__(kBlock, OURO_WAVES) k_hdr_post(ouro_tpraos_batch b, size_t base,
+                                                                size_t count, size_t chunk,
+                                                                int32_t* tasks, int32_t* res_buf,
+                                                                uint8_t* __restrict__ verdict,
+                                                                uint8_t* __restrict__ beta_eta,
+                                                                uint8_t* __restrict__ beta_leader) {
+  const size_t nth = (size_t)gridDim.x * blockDim.x;
+  const uint32_t opts = batch_opts(b);
+  for (size_t li = (size_t)blockIdx.x * blockDim.x + threadIdx.x; li < count; li += nth) {
+    const size_t i = base + li;
+    const Slot res = slot_of(res_buf, li, kHdrResWords);
+#pragma unroll 1
+    for (int c = kCoreOcert; c <= kCoreVl; c++)
+      hdr_core(b, i, opts, c, slot_of(tasks, (size_t)c * chunk + li, kSlotWords), res, nullptr,
+               true, false, false, kPhasePost);
+    // the finish's 8 x 12 scratch words: the header's (spent) OCERT task slot
+#if OURO_HDR_FINISH_NI
+    hdr_finish_item_ni(b, i, opts, res, slot_of(tasks, li, kSlotWords), verdict, beta_eta,
+                       beta_leader);
+#else
+    hdr_finish_item(b, i, opts, res, slot_of(tasks, li, kSlotWords), verdict, beta_eta,
+                    beta_leader);
+#endif
+  }
+}
+
 // Latency mode (k_tpraos_cores, k_tpraos_finish): kernels_lat.hip, its own
 // translation unit built with the row-order field products (lane quads issue
 // one product per lane, whose dependent column-scan chains would stall: A/B
@@ -309,14 +379,14 @@ struct DeviceState {
   std::string err_msg;
   int32_t* btab = nullptr;
   int cus = 0;
-  int max_blocks[8] = {0};  // per KernelId (kNumKernels <= 8)
+  int max_blocks[12] = {0};  // per KernelId (kNumKernels <= 12)
 };
 
 std::mutex g_dev_mu;
 std::map<int, DeviceState> g_dev;
 
 enum KernelId { kEd = 0, kVrf = 1, kKes = 2, kHdr = 3, kP2H = 4, kCores = 5, kFinish = 6,
-                kLeader = 7, kNumKernels = 8 };
+                kLeader = 7, kHdrPre = 8, kHdrDsm = 9, kHdrPost = 10, kNumKernels = 11 };
 
 const void* kernel_ptr(int id) {
   switch (id) {
@@ -327,6 +397,9 @@ const void* kernel_ptr(int id) {
     case kCores: return reinterpret_cast<const void*>(&k_tpraos_cores);
     case kFinish: return reinterpret_cast<const void*>(&k_tpraos_finish);
     case kLeader: return reinterpret_cast<const void*>(&k_leader_check);
+    case kHdrPre: return reinterpret_cast<const void*>(&k_hdr_pre);
+    case kHdrDsm: return reinterpret_cast<const void*>(&k_hdr_dsm);
+    case kHdrPost: return reinterpret_cast<const void*>(&k_hdr_post);
     default: return reinterpret_cast<const void*>(&k_vrf03_proof_to_hash);
   }
 }
@@ -632,6 +705,17 @@ int launch_kes(hipStream_t st, size_t n, const uint8_t* vk, const uint32_t* t, c
   return launch_check();
 }
 
+// The split header kernel (k_hdr_pre / k_hdr_dsm / k_hdr_post) instead of
+// k_tpraos_verify: OURO_HDR_SPLIT=0/1 in the environment, read per launch
+// (default OURO_HDR_SPLIT_DEFAULT).
+#ifndef OURO_HDR_SPLIT_DEFAULT
+#define OURO_HDR_SPLIT_DEFAULT 0
+#endif
+bool hdr_split() {
+  if (const char* e = getenv("OURO_HDR_SPLIT")) return atoi(e) != 0;
+  return OURO_HDR_SPLIT_DEFAULT != 0;
+}
+
 int launch_hdr(hipStream_t st, const ouro_tpraos_batch& b, uint8_t* verdict, uint8_t* be,
                uint8_t* bl) {
   DeviceState* ds;
@@ -639,6 +723,32 @@ int launch_hdr(hipStream_t st, const ouro_tpraos_batch& b, uint8_t* verdict, uin
   if (rc) return rc;
   int grid;
   int32_t* scr;
+  if (hdr_split()) {
+    // chunks of one resident grid of the pre / post kernels; per chunk the
+    // six task slots of each header and its result record
+    const size_t chunk = std::min<size_t>((b.n + kBlock - 1) / kBlock * kBlock,
+                                          (size_t)ds->max_blocks[kHdrPre] * kBlock);
+    const size_t words = (size_t)kHdrCores * slot_region_words(chunk, kSlotWords) +
+                         slot_region_words(chunk, kHdrResWords);
+    Buf& sb = ctx().scratch[st];
+    if ((rc = ensure(sb, words * sizeof(int32_t)))) return rc;
+    int32_t* tasks = static_cast<int32_t*>(sb.p);
+    int32_t* res = tasks + (size_t)kHdrCores * slot_region_words(chunk, kSlotWords);
+    const int gpp = (int)std::min<size_t>(chunk / kBlock, (size_t)ds->max_blocks[kHdrPre]);
+    const int gpo = (int)std::min<size_t>(chunk / kBlock, (size_t)ds->max_blocks[kHdrPost]);
+    const int gd = (int)std::min<size_t>((size_t)kHdrCores * chunk / kBlock,
+                                         (size_t)ds->max_blocks[kHdrDsm]);
+    for (size_t base = 0; base < b.n; base += chunk) {
+      const size_t count = std::min(chunk, b.n - base);
+      hipLaunchKernelGGL(k_hdr_pre, dim3(gpp), dim3(kBlock), 0, st, b, base, count, chunk, tasks,
+                         res, ds->btab);
+      hipLaunchKernelGGL(k_hdr_dsm, dim3(gd), dim3(kBlock), 0, st, count, chunk, tasks, ds->btab);
+      hipLaunchKernelGGL(k_hdr_post, dim3(gpo), dim3(kBlock), 0, st, b, base, count, chunk, tasks,
+                         res, verdict, be, bl);
+      if ((rc = launch_check())) return rc;
+    }
+    return OURO_OK;
+  }
   if ((rc = plan(ds, kHdr, b.n, st, &grid, &scr, kHdrLaneWords))) return rc;
   hipLaunchKernelGGL(k_tpraos_verify, dim3(grid), dim3(kBlock), 0, st, b, verdict, be, bl, scr,
                      ds->btab);

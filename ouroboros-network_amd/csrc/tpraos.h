@@ -128,7 +128,7 @@ OURO_HD inline void ocert_msg(OcertMsg& m, const uint32_t hot_vk[8], uint64_t ct
 // reused (throughput mode: both VRFs of a header share the key).
 OURO_HD inline bool vrf_u_core(const uint32_t pk[8], const uint32_t pi[20], bool build_y,
                                int yslot, Slot lane, const int32_t* btab,
-                               bool quad = false) {
+                               bool quad = false, int phase = kPhaseAll) {
   bool ok = true;
   if (build_y) {
     ge_p3 Y;
@@ -147,7 +147,7 @@ OURO_HD inline bool vrf_u_core(const uint32_t pk[8], const uint32_t pi[20], bool
   st_words8(lane + kSlotB, s);
   st_carry(lane, 0, sc_recode_carries<4, 33>(c));
   st_carry(lane, 2, sc_recode_b(s));
-  dsm(lane, btab, dsm_cfg(33, 0, true, yslot, 1), quad);
+  dsm_or_defer(lane, btab, dsm_cfg(33, 0, true, yslot, 1), quad, phase);
   return ok;
 }
 
@@ -160,7 +160,7 @@ template <class Tail>
 OURO_HD inline int32_t vrf_v_core(const uint32_t pk[8], const uint32_t pi[20], const Tail& alpha,
                                   uint32_t alen, Slot lane, const int32_t* btab,
                                   Slot res, int ptH, int ptV, int ptG8, int part,
-                                  Slot partial, bool quad = false) {
+                                  Slot partial, bool quad = false, int phase = kPhaseAll) {
   uint32_t G[8], c[8], s_raw[8], s[8];
 #pragma unroll
   for (int i = 0; i < 8; i++) {
@@ -217,11 +217,11 @@ OURO_HD inline int32_t vrf_v_core(const uint32_t pk[8], const uint32_t pi[20], c
       build_table(lane + kSlotTab2, ge_p3_neg(Gamma), quad);
       st_words8(lane + kSlotA2, c);
       st_carry(lane, 1, sc_recode_carries<4, 33>(c));
-      dsm(lane, btab, dsm_cfg(64, 33, false, 0, 1), quad);
+      dsm_or_defer(lane, btab, dsm_cfg(64, 33, false, 0, 1), quad, phase);
     } else {
       dsm(lane, btab, dsm_cfg(64, 0, false, 0, 1), quad);
     }
-    st_point_from_dsm(res, ptV, lane);
+    if (phase != kPhasePre) st_point_from_dsm(res, ptV, lane);
     if (part == 1) return kFlagOk;
   }
   ge_p3 G8 = ge_mul8(Gamma);
@@ -453,9 +453,25 @@ OURO_HD inline void hdr_seed(SeedMsg& a, const ouro_tpraos_batch& b, size_t i, b
 // One core of header i (tpraos.h); throughput mode reuses the VRF key table
 // built by the eta U core (table slot 2) for the leader U core.
 // opts: the batch's optional members (batch_opts / the latency launches' word).
+// phase (the split header kernel, throughput mode only): kPhasePre runs
+// every step before the core's dsm, leaving its inputs in `lane` (the core's
+// own task slot) and its flag in res; kPhasePost, after the dsm launch, stores
+// the dsm's point or clears the Ed25519 core's flag unless its result is the
+// identity.  The leader U core's pre copies the shared key table from the eta
+// U core's task slot `ukey` instead of decoding the key again.
 OURO_HD inline void hdr_core(const ouro_tpraos_batch& b, size_t i, uint32_t opts, int core,
                              Slot lane, Slot res, const int32_t* btab,
-                             bool share_key = true, bool split = false, bool quad = false) {
+                             bool share_key = true, bool split = false, bool quad = false,
+                             int phase = kPhaseAll, Slot ukey = Slot{nullptr}) {
+  if (phase == kPhasePost) {
+    if (core == kCoreOcert || core == kCoreKes) {
+      if (!dsm_result_is_identity(lane)) stg1(res.word(kResFlags + core), 0);
+    } else {
+      st_point_from_dsm(res, core == kCoreUe ? kPtUe : core == kCoreUl ? kPtUl
+                                             : core == kCoreVe ? kPtVe : kPtVl, lane);
+    }
+    return;
+  }
   int32_t flag = 0;
   switch (core) {
     case kCoreOcert: {
@@ -465,7 +481,7 @@ OURO_HD inline void hdr_core(const ouro_tpraos_batch& b, size_t i, uint32_t opts
       ld_words(hv, b.hot_vk + 32 * i, 2);
       OcertMsg m;
       ocert_msg(m, hv, b.ocert_counter[i], b.ocert_kes_period[i]);
-      flag = ed25519_verify_lane(s, p, m, 48, lane, btab, false, quad) ? kFlagOk : 0;
+      flag = ed25519_verify_lane(s, p, m, 48, lane, btab, false, quad, phase) ? kFlagOk : 0;
       break;
     }
     case kCoreKes: {
@@ -473,7 +489,7 @@ OURO_HD inline void hdr_core(const ouro_tpraos_batch& b, size_t i, uint32_t opts
       ld_words(hv, b.hot_vk + 32 * i, 2);
       const uint32_t* sw = reinterpret_cast<const uint32_t*>(b.kes_sig + 448 * i);
       flag = sum6kes_verify_lane(hv, b.kes_t[i], sw, ShaGlobalTail{b.body + b.body_off[i]},
-                                 b.body_len[i], lane, btab, quad) ? kFlagOk : 0;
+                                 b.body_len[i], lane, btab, quad, phase) ? kFlagOk : 0;
       break;
     }
     case kCoreUe:
@@ -483,9 +499,15 @@ OURO_HD inline void hdr_core(const ouro_tpraos_batch& b, size_t i, uint32_t opts
       ld_words(p, b.vrf_vk + 32 * i, 2);
       ld_words(pi, (leader ? b.leader_proof : b.eta_proof) + 80 * i, 5);
       const bool build = !(share_key && leader);
-      const bool ok = vrf_u_core(p, pi, build, 2, lane, btab, quad);
+      if (!build && phase == kPhasePre) {
+        // the eta core's [1..8](-Y) into this core's own task slot
+#pragma unroll 1
+        for (int k = 0; k < kTabWords / 4; k++)
+          stg4((lane + kSlotTab3).chunk(k), ldg4((ukey + kSlotTab3).chunk(k)));
+      }
+      const bool ok = vrf_u_core(p, pi, build, 2, lane, btab, quad, phase);
       flag = build ? (ok ? kFlagOk : 0) : (ldg1(res.word(kResFlags + kCoreUe)) & kFlagOk);
-      st_point_from_dsm(res, leader ? kPtUl : kPtUe, lane);
+      if (phase != kPhasePre) st_point_from_dsm(res, leader ? kPtUl : kPtUe, lane);
       break;
     }
     default: {  // kCoreVe / kCoreVl, and in latency mode kCoreGe / kCoreGl
@@ -505,7 +527,7 @@ OURO_HD inline void hdr_core(const ouro_tpraos_batch& b, size_t i, uint32_t opts
       flag = vrf_v_core(p, pi, SlotTail{lane + kSlotOut}, 32, lane, btab, res,
                         leader ? kPtHl : kPtHe, leader ? kPtVl : kPtVe,
                         leader ? kPtG8l : kPtG8e, gamma ? 2 : (split ? 1 : 0),
-                        res + kLatPart + (leader ? kPtWords : 0), quad);
+                        res + kLatPart + (leader ? kPtWords : 0), quad, phase);
       break;
     }
   }

@@ -531,6 +531,15 @@ OURO_FI void dsm_body(Slot lane, const int32_t* btab, uint32_t cfg) {
 OURO_NI void dsm_lane(Slot lane, const int32_t* btab, uint32_t cfg) {
   dsm_body<false>(lane, btab, cfg);
 }
+#if defined(__HIPCC__)
+// The same for the split header kernel's dsm launch (k_hdr_dsm), a function
+// of its own: an out-of-line function gets ONE register allocation, the
+// tightest any caller allows, and k_hdr_dsm runs at 4 waves / SIMD (128
+// VGPRs) while every other caller has 256.
+__device__ __noinline__ void dsm_lane_dsm_launch(Slot lane, const int32_t* btab, uint32_t cfg) {
+  dsm_body<false>(lane, btab, cfg);
+}
+#endif
 // latency mode: the four lanes of a quad run one chain (same inputs, same
 // slot), splitting each group operation's products
 OURO_NI void dsm_quad(Slot lane, const int32_t* btab, uint32_t cfg) {
@@ -545,6 +554,27 @@ OURO_FI void dsm(Slot lane, const int32_t* btab, uint32_t cfg, bool quad = false
 
 OURO_FI ge_p2 dsm_result(Slot lane) {
   return ge_p2{ld_fe(lane + kSlotOut), ld_fe(lane + kSlotOut + 12), ld_fe(lane + kSlotOut + 24)};
+}
+
+// Phases of a core around its double-scalar multiplication (the split header
+// kernel, kernels.hip OURO_HDR_SPLIT): kPhasePre stops once the dsm's inputs
+// -- tables, scalars, recoding carries -- and its cfg word (kSlotCfg, the
+// carry region's spare words) are in the slot; the dsm then runs in a launch
+// of its own at a higher occupancy (k_hdr_dsm), and kPhasePost finishes the
+// core from the result the dsm left at kSlotOut.  kPhaseAll: all of it.
+enum Phase { kPhaseAll = 0, kPhasePre = 1, kPhasePost = 2 };
+constexpr int kSlotCfg = kSlotCarry + 6;
+OURO_FI void dsm_or_defer(Slot lane, const int32_t* btab, uint32_t cfg, bool quad, int phase) {
+  if (phase == kPhasePre) {
+    stg1(lane.word(kSlotCfg), (int32_t)cfg);
+    return;
+  }
+  dsm(lane, btab, cfg, quad);
+}
+// an Ed25519 core's verdict from its dsm result: Q == O, projectively
+OURO_FI bool dsm_result_is_identity(Slot lane) {
+  const ge_p2 Q = dsm_result(lane);
+  return fe_iszero(Q.X) && fe_iszero(fe_sub(Q.Y, Q.Z));
 }
 
 // ---- Ed25519 ------------------------------------------------------------------
@@ -634,11 +664,14 @@ OURO_FI bool ed25519_precheck(const uint32_t R[8], const uint32_t S[8], const ui
 // with h = SHA-512(R || A || M) mod L.  The doubling chain is ~130 bits
 // instead of 253, and no inversion is needed: the result is compared to the
 // identity projectively.
+// phase (kPhasePre / kPhasePost, the split header kernel): Pre returns the
+// checks before the dsm, Post whether its result is the identity.
 template <class Tail>
 OURO_HD inline bool ed25519_verify_lane(const uint32_t sig[16], const uint32_t pk[8],
                                         const Tail& msg, uint32_t mlen, Slot lane,
                                         const int32_t* btab, bool byron = false,
-                                        bool quad = false) {
+                                        bool quad = false, int phase = kPhaseAll) {
+  if (phase == kPhasePost) return dsm_result_is_identity(lane);
   uint32_t R[8], S[8];
 #pragma unroll
   for (int i = 0; i < 8; i++) {
@@ -673,10 +706,9 @@ OURO_HD inline bool ed25519_verify_lane(const uint32_t sig[16], const uint32_t p
   // windows so that every scalar is < 2^(4 nw - 1) (top carry zero), <= 64
   int nw = wave_max_small((hs.bits + 4) >> 2);
   nw = nw < 1 ? 1 : (nw > 64 ? 64 : nw);
-  dsm(lane, btab, dsm_cfg(nw, nw, true, 0, 1), quad);
-  const ge_p2 Q = dsm_result(lane);
-  const bool ident = fe_iszero(Q.X) && fe_iszero(fe_sub(Q.Y, Q.Z));
-  return ok && ident;
+  dsm_or_defer(lane, btab, dsm_cfg(nw, nw, true, 0, 1), quad, phase);
+  if (phase == kPhasePre) return ok;
+  return ok && dsm_result_is_identity(lane);
 }
 
 // ---- ECVRF-ED25519-SHA512-Elligator2 (draft-03) -------------------------------
@@ -940,10 +972,12 @@ OURO_HD inline bool sum6kes_walk(uint32_t cur[8], uint32_t sig[16], const uint32
 template <class Tail>
 OURO_HD inline bool sum6kes_verify_lane(const uint32_t vk[8], uint32_t t, const uint32_t* sigw,
                                         const Tail& msg, uint32_t mlen, Slot lane,
-                                        const int32_t* btab, bool quad = false) {
+                                        const int32_t* btab, bool quad = false,
+                                        int phase = kPhaseAll) {
+  if (phase == kPhasePost) return dsm_result_is_identity(lane);
   uint32_t cur[8], sig[16];
   const bool ok = sum6kes_walk(cur, sig, vk, t, sigw);
-  const bool leaf = ed25519_verify_lane(sig, cur, msg, mlen, lane, btab, false, quad);
+  const bool leaf = ed25519_verify_lane(sig, cur, msg, mlen, lane, btab, false, quad, phase);
   return ok && leaf;
 }
 
