@@ -254,6 +254,20 @@ int dh_tpraos_verify(const ouro_tpraos_batch* b, int mode, uint8_t* verdict, uin
   const uint32_t opts = batch_opts(*b);
   for (size_t i = 0; i < b->n; i++) {
     std::fill(rr.buf.begin(), rr.buf.end(), 0);
+    if (mode == 3) {
+      // the split header kernel's phases (k_hdr_pre / k_hdr_dsm / k_hdr_post):
+      // each core in its own task slot, the dsm from the cfg word the pre
+      // phase left there
+      for (int core = 0; core < kHdrCores; core++)
+        hdr_core(*b, i, opts, core, lanes[core].s, r, host_btab(), true, false, false, kPhasePre,
+                 lanes[kCoreUe].s);
+      for (int core = 0; core < kHdrCores; core++)
+        dsm_lane(lanes[core].s, host_btab(), (uint32_t)*lanes[core].s.word(kSlotCfg));
+      for (int core = 0; core < kHdrCores; core++)
+        hdr_core(*b, i, opts, core, lanes[core].s, r, nullptr, true, false, false, kPhasePost);
+      hdr_finish_item(*b, i, opts, r, lanes[0].s, verdict, beta_eta, beta_leader);
+      continue;
+    }
     const int cores = mode ? kLatCores : kHdrCores;
     for (int core = 0; core < cores; core++)
       hdr_core(*b, i, opts, core, lanes[mode ? core : 0].s, r, host_btab(), mode == 0, mode != 0,

@@ -247,7 +247,8 @@ def _oracle(batch, nonce=False):
     return verdict, be, bl, en
 
 
-MODES = pytest.mark.parametrize("mode", [0, 1, 2], ids=["throughput", "latency", "latency_quad"])
+MODES = pytest.mark.parametrize("mode", [0, 1, 2, 3],
+                                ids=["throughput", "latency", "latency_quad", "split_phases"])
 
 
 @MODES
