@@ -185,7 +185,7 @@ __global__ void __launch_bounds__(kBlock, OURO_WAVES) k_tpraos_verify(ouro_tprao
 #endif
 }
 
-// ---- the split header kernel (OURO_HDR_SPLIT, round 4) -----------------------
+// ---- the split header kernel (OURO_SPLIT, round 4) ---------------------------
 // The same cores as k_tpraos_verify in three launches per chunk of headers, so
 // the double-scalar multiplications -- ~70 % of a header's time, and code
 // whose chains fit in 128 VGPRs -- run at OURO_DSM_WAVES waves per SIMD while
@@ -219,10 +219,10 @@ __global__ void __launch_bounds__(kBlock, OURO_WAVES) k_hdr_pre(ouro_tpraos_batc
   }
 }
 __global__ void __launch_bounds__(kBlock, OURO_DSM_WAVES) k_hdr_dsm(size_t count, size_t chunk,
-                                                                   int32_t* tasks,
+                                                                   int ncores, int32_t* tasks,
                                                                    const int32_t* __restrict__ btab) {
   const size_t nth = (size_t)gridDim.x * blockDim.x;
-  const size_t ntasks = (size_t)kHdrCores * chunk;
+  const size_t ntasks = (size_t)ncores * chunk;
   for (size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x; t < ntasks; t += nth) {
     if (t % chunk >= count) continue;  // the last chunk's unused headers
     const Slot s = slot_of(tasks, t, kSlotWords);
@@ -252,6 +252,53 @@ __global__ void __launch_bounds__(kBlock, OURO_WAVES) k_hdr_post(ouro_tpraos_bat
     hdr_finish_item(b, i, opts, res, slot_of(tasks, li, kSlotWords), verdict, beta_eta,
                     beta_leader);
 #endif
+  }
+}
+
+// The standalone Ed25519 / Sum6KES kernels split the same way (one task per
+// item; the checks before the dsm in the slot's spare word kSlotCfg + 1).
+constexpr int kSlotPreOk = kSlotCfg + 1;
+__global__ void __launch_bounds__(kBlock, OURO_WAVES) k_ed25519_pre(
+    size_t base, size_t count, const uint8_t* __restrict__ pk, const uint8_t* __restrict__ sig,
+    const uint8_t* __restrict__ msg, const uint64_t* __restrict__ msg_off,
+    const uint32_t* __restrict__ msg_len, int32_t* tasks, const int32_t* __restrict__ btab,
+    uint32_t byron) {
+  const size_t nth = (size_t)gridDim.x * blockDim.x;
+  for (size_t li = (size_t)blockIdx.x * blockDim.x + threadIdx.x; li < count; li += nth) {
+    const size_t i = base + li;
+    const Slot s = slot_of(tasks, li, kSlotWords);
+    uint32_t sg[16], p[8];
+    load_words(sg, sig + 64 * i, 4);
+    load_words(p, pk + 32 * i, 2);
+    const bool ok = ed25519_verify_lane(sg, p, ShaGlobalTail{msg + msg_off[i]}, msg_len[i], s, btab,
+                                        byron != 0, false, kPhasePre);
+    stg1(s.word(kSlotPreOk), ok ? 1 : 0);
+  }
+}
+__global__ void __launch_bounds__(kBlock, OURO_WAVES) k_sum6kes_pre(
+    size_t base, size_t count, const uint8_t* __restrict__ vk, const uint32_t* __restrict__ t,
+    const uint8_t* __restrict__ msg, const uint64_t* __restrict__ msg_off,
+    const uint32_t* __restrict__ msg_len, const uint8_t* __restrict__ sig, int32_t* tasks,
+    const int32_t* __restrict__ btab) {
+  const size_t nth = (size_t)gridDim.x * blockDim.x;
+  for (size_t li = (size_t)blockIdx.x * blockDim.x + threadIdx.x; li < count; li += nth) {
+    const size_t i = base + li;
+    const Slot s = slot_of(tasks, li, kSlotWords);
+    uint32_t v[8];
+    load_words(v, vk + 32 * i, 2);
+    const uint32_t* sw = reinterpret_cast<const uint32_t*>(sig + 448 * i);
+    const bool ok = sum6kes_verify_lane(v, t[i], sw, ShaGlobalTail{msg + msg_off[i]}, msg_len[i], s,
+                                        btab, false, kPhasePre);
+    stg1(s.word(kSlotPreOk), ok ? 1 : 0);
+  }
+}
+// verdict = the pre checks and [the dsm's result] == O
+__global__ void __launch_bounds__(kBlock) k_ed_post(size_t base, size_t count, int32_t* tasks,
+                                                    uint8_t* __restrict__ verdict) {
+  const size_t nth = (size_t)gridDim.x * blockDim.x;
+  for (size_t li = (size_t)blockIdx.x * blockDim.x + threadIdx.x; li < count; li += nth) {
+    const Slot s = slot_of(tasks, li, kSlotWords);
+    verdict[base + li] = (ldg1(s.word(kSlotPreOk)) && dsm_result_is_identity(s)) ? 1 : 0;
   }
 }
 
@@ -379,14 +426,15 @@ struct DeviceState {
   std::string err_msg;
   int32_t* btab = nullptr;
   int cus = 0;
-  int max_blocks[12] = {0};  // per KernelId (kNumKernels <= 12)
+  int max_blocks[16] = {0};  // per KernelId (kNumKernels <= 16)
 };
 
 std::mutex g_dev_mu;
 std::map<int, DeviceState> g_dev;
 
 enum KernelId { kEd = 0, kVrf = 1, kKes = 2, kHdr = 3, kP2H = 4, kCores = 5, kFinish = 6,
-                kLeader = 7, kHdrPre = 8, kHdrDsm = 9, kHdrPost = 10, kNumKernels = 11 };
+                kLeader = 7, kHdrPre = 8, kHdrDsm = 9, kHdrPost = 10, kEdPre = 11, kKesPre = 12,
+                kNumKernels = 13 };
 
 const void* kernel_ptr(int id) {
   switch (id) {
@@ -400,6 +448,8 @@ const void* kernel_ptr(int id) {
     case kHdrPre: return reinterpret_cast<const void*>(&k_hdr_pre);
     case kHdrDsm: return reinterpret_cast<const void*>(&k_hdr_dsm);
     case kHdrPost: return reinterpret_cast<const void*>(&k_hdr_post);
+    case kEdPre: return reinterpret_cast<const void*>(&k_ed25519_pre);
+    case kKesPre: return reinterpret_cast<const void*>(&k_sum6kes_pre);
     default: return reinterpret_cast<const void*>(&k_vrf03_proof_to_hash);
   }
 }
@@ -654,6 +704,39 @@ size_t wide_small_max() {
 int wide_grid(size_t n) { return (int)std::min<size_t>(n, 8192); }
 
 // ---- device-pointer launches (shared by the host-buffer and device APIs) ----
+// The split kernels (pre / dsm at OURO_DSM_WAVES / post) instead of the
+// one-pass k_tpraos_verify, k_ed25519_verify and k_sum6kes_verify:
+// OURO_SPLIT=0/1 in the environment, read per launch (default
+// OURO_SPLIT_DEFAULT).
+#ifndef OURO_SPLIT_DEFAULT
+#define OURO_SPLIT_DEFAULT 0
+#endif
+bool split_launch() {
+  if (const char* e = getenv("OURO_SPLIT")) return atoi(e) != 0;
+  return OURO_SPLIT_DEFAULT != 0;
+}
+// One Ed25519-shaped item per task: chunks of 4 resident grids of the pre
+// kernel, so the 4-wave dsm launch has 2 grids of tasks to spread.
+template <class LaunchPre>
+int launch_split_items(DeviceState* ds, hipStream_t st, size_t n, int pre_id, uint8_t* verdict,
+                       LaunchPre&& launch_pre) {
+  const size_t cap = (size_t)ds->max_blocks[pre_id] * kBlock;
+  const size_t chunk = std::min<size_t>((n + kBlock - 1) / kBlock * kBlock, 4 * cap);
+  Buf& sb = ctx().scratch[st];
+  int rc = ensure(sb, slot_region_words(chunk, kSlotWords) * sizeof(int32_t));
+  if (rc) return rc;
+  int32_t* tasks = static_cast<int32_t*>(sb.p);
+  const int gp = (int)std::min<size_t>(chunk / kBlock, (size_t)ds->max_blocks[pre_id]);
+  const int gd = (int)std::min<size_t>(chunk / kBlock, (size_t)ds->max_blocks[kHdrDsm]);
+  for (size_t base = 0; base < n; base += chunk) {
+    const size_t count = std::min(chunk, n - base);
+    launch_pre(gp, base, count, tasks);
+    hipLaunchKernelGGL(k_hdr_dsm, dim3(gd), dim3(kBlock), 0, st, count, chunk, 1, tasks, ds->btab);
+    hipLaunchKernelGGL(k_ed_post, dim3(gp), dim3(kBlock), 0, st, base, count, tasks, verdict);
+    if ((rc = launch_check())) return rc;
+  }
+  return OURO_OK;
+}
 // byron = 1: ByronDSIGN acceptance (cardano-crypto)
 int launch_ed(hipStream_t st, size_t n, const uint8_t* pk, const uint8_t* sig, const uint8_t* msg,
               const uint64_t* off, const uint32_t* len, uint8_t* verdict, uint32_t byron = 0) {
@@ -665,6 +748,12 @@ int launch_ed(hipStream_t st, size_t n, const uint8_t* pk, const uint8_t* sig, c
                        len, verdict, ds->btab, byron);
     return launch_check();
   }
+  if (split_launch())
+    return launch_split_items(ds, st, n, kEdPre, verdict, [&](int g, size_t base, size_t count,
+                                                               int32_t* tasks) {
+      hipLaunchKernelGGL(k_ed25519_pre, dim3(g), dim3(kBlock), 0, st, base, count, pk, sig, msg,
+                         off, len, tasks, ds->btab, byron);
+    });
   int grid;
   int32_t* scr;
   if ((rc = plan(ds, kEd, n, st, &grid, &scr))) return rc;
@@ -697,6 +786,12 @@ int launch_kes(hipStream_t st, size_t n, const uint8_t* vk, const uint32_t* t, c
   DeviceState* ds;
   int rc = device_state(&ds);
   if (rc) return rc;
+  if (split_launch())
+    return launch_split_items(ds, st, n, kKesPre, verdict, [&](int g, size_t base, size_t count,
+                                                                int32_t* tasks) {
+      hipLaunchKernelGGL(k_sum6kes_pre, dim3(g), dim3(kBlock), 0, st, base, count, vk, t, msg, off,
+                         len, sig, tasks, ds->btab);
+    });
   int grid;
   int32_t* scr;
   if ((rc = plan(ds, kKes, n, st, &grid, &scr))) return rc;
@@ -705,16 +800,6 @@ int launch_kes(hipStream_t st, size_t n, const uint8_t* vk, const uint32_t* t, c
   return launch_check();
 }
 
-// The split header kernel (k_hdr_pre / k_hdr_dsm / k_hdr_post) instead of
-// k_tpraos_verify: OURO_HDR_SPLIT=0/1 in the environment, read per launch
-// (default OURO_HDR_SPLIT_DEFAULT).
-#ifndef OURO_HDR_SPLIT_DEFAULT
-#define OURO_HDR_SPLIT_DEFAULT 0
-#endif
-bool hdr_split() {
-  if (const char* e = getenv("OURO_HDR_SPLIT")) return atoi(e) != 0;
-  return OURO_HDR_SPLIT_DEFAULT != 0;
-}
 
 int launch_hdr(hipStream_t st, const ouro_tpraos_batch& b, uint8_t* verdict, uint8_t* be,
                uint8_t* bl) {
@@ -723,7 +808,7 @@ int launch_hdr(hipStream_t st, const ouro_tpraos_batch& b, uint8_t* verdict, uin
   if (rc) return rc;
   int grid;
   int32_t* scr;
-  if (hdr_split()) {
+  if (split_launch()) {
     // chunks of one resident grid of the pre / post kernels; per chunk the
     // six task slots of each header and its result record
     const size_t chunk = std::min<size_t>((b.n + kBlock - 1) / kBlock * kBlock,
@@ -742,7 +827,8 @@ int launch_hdr(hipStream_t st, const ouro_tpraos_batch& b, uint8_t* verdict, uin
       const size_t count = std::min(chunk, b.n - base);
       hipLaunchKernelGGL(k_hdr_pre, dim3(gpp), dim3(kBlock), 0, st, b, base, count, chunk, tasks,
                          res, ds->btab);
-      hipLaunchKernelGGL(k_hdr_dsm, dim3(gd), dim3(kBlock), 0, st, count, chunk, tasks, ds->btab);
+      hipLaunchKernelGGL(k_hdr_dsm, dim3(gd), dim3(kBlock), 0, st, count, chunk, (int)kHdrCores,
+                         tasks, ds->btab);
       hipLaunchKernelGGL(k_hdr_post, dim3(gpo), dim3(kBlock), 0, st, b, base, count, chunk, tasks,
                          res, verdict, be, bl);
       if ((rc = launch_check())) return rc;

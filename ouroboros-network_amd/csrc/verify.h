@@ -557,7 +557,7 @@ OURO_FI ge_p2 dsm_result(Slot lane) {
 }
 
 // Phases of a core around its double-scalar multiplication (the split header
-// kernel, kernels.hip OURO_HDR_SPLIT): kPhasePre stops once the dsm's inputs
+// kernel, kernels.hip OURO_SPLIT): kPhasePre stops once the dsm's inputs
 // -- tables, scalars, recoding carries -- and its cfg word (kSlotCfg, the
 // carry region's spare words) are in the slot; the dsm then runs in a launch
 // of its own at a higher occupancy (k_hdr_dsm), and kPhasePost finishes the
