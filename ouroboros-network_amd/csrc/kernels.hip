@@ -201,8 +201,14 @@ __global__ void __launch_bounds__(kBlock, OURO_WAVES) k_tpraos_verify(ouro_tprao
 #ifndef OURO_DSM_WAVES
 #define OURO_DSM_WAVES 4
 #endif
+#ifndef OURO_PRE_WAVES
+#define OURO_PRE_WAVES OURO_WAVES  // the pre / post kernels' own budgets (A/B)
+#endif
+#ifndef OURO_POST_WAVES
+#define OURO_POST_WAVES OURO_WAVES
+#endif
 constexpr int kHdrResWords = round_slot(kResWords);
-__global__ void __launch_bounds__(kBlock, OURO_WAVES) k_hdr_pre(ouro_tpraos_batch b, size_t base,
+__global__ void __launch_bounds__(kBlock, OURO_PRE_WAVES) k_hdr_pre(ouro_tpraos_batch b, size_t base,
                                                                size_t count, size_t chunk,
                                                                int32_t* tasks, int32_t* res_buf,
                                                                const int32_t* __restrict__ btab) {
@@ -229,7 +235,7 @@ __global__ void __launch_bounds__(kBlock, OURO_DSM_WAVES) k_hdr_dsm(size_t count
     dsm_lane_dsm_launch(s, btab, (uint32_t)ldg1(s.word(kSlotCfg)));
   }
 }
-__global__ void __launch_bounds__(kBlock, OURO_WAVES) k_hdr_post(ouro_tpraos_batch b, size_t base,
+__global__ void __launch_bounds__(kBlock, OURO_POST_WAVES) k_hdr_post(ouro_tpraos_batch b, size_t base,
                                                                 size_t count, size_t chunk,
                                                                 int32_t* tasks, int32_t* res_buf,
                                                                 uint8_t* __restrict__ verdict,
@@ -258,7 +264,7 @@ __global__ void __launch_bounds__(kBlock, OURO_WAVES) k_hdr_post(ouro_tpraos_bat
 // The standalone Ed25519 / Sum6KES kernels split the same way (one task per
 // item; the checks before the dsm in the slot's spare word kSlotCfg + 1).
 constexpr int kSlotPreOk = kSlotCfg + 1;
-__global__ void __launch_bounds__(kBlock, OURO_WAVES) k_ed25519_pre(
+__global__ void __launch_bounds__(kBlock, OURO_PRE_WAVES) k_ed25519_pre(
     size_t base, size_t count, const uint8_t* __restrict__ pk, const uint8_t* __restrict__ sig,
     const uint8_t* __restrict__ msg, const uint64_t* __restrict__ msg_off,
     const uint32_t* __restrict__ msg_len, int32_t* tasks, const int32_t* __restrict__ btab,
@@ -275,7 +281,7 @@ __global__ void __launch_bounds__(kBlock, OURO_WAVES) k_ed25519_pre(
     stg1(s.word(kSlotPreOk), ok ? 1 : 0);
   }
 }
-__global__ void __launch_bounds__(kBlock, OURO_WAVES) k_sum6kes_pre(
+__global__ void __launch_bounds__(kBlock, OURO_PRE_WAVES) k_sum6kes_pre(
     size_t base, size_t count, const uint8_t* __restrict__ vk, const uint32_t* __restrict__ t,
     const uint8_t* __restrict__ msg, const uint64_t* __restrict__ msg_off,
     const uint32_t* __restrict__ msg_len, const uint8_t* __restrict__ sig, int32_t* tasks,
