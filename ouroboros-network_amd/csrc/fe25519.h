@@ -1048,9 +1048,28 @@ OURO_FI bool fe_isnegative(const fe& f) {
 #ifndef OURO_SQN_UNROLL
 #define OURO_SQN_UNROLL 1  // A/B switch: squarings per loop trip in the chains
 #endif
+// The squarings of the exponentiation chains in one scan chain (1) or two
+// interleaved ones (2, fe_sq_scan2): a chain's squarings depend on each
+// other, so the one-chain form issues dependent multiply-adds back to back
+// (6.9 SIMD cycles each at 2 waves against 4.4 for two chains,
+// profiles/r04/valu_costs.json).  A/B switch for the chains only (the
+// doublings' squarings are already interleaved, ge_dbl_lockstep).
+#ifndef OURO_POW_SQ_CHAINS
+#define OURO_POW_SQ_CHAINS 1
+#endif
+OURO_FI fe fe_sq_pow(const fe& f) {
+  if constexpr (OURO_POW_SQ_CHAINS == 2) {
+    OURO_COUNT_SQ();
+    fe h = fe_sq_scan2<1>(f);
+    OURO_TRK(trk_sq_scan(h, f, 1, 2));
+    return h;
+  } else {
+    return fe_sq(f);
+  }
+}
 OURO_FI fe fe_sqn(fe t, int n) {
 #pragma unroll OURO_SQN_UNROLL
-  for (int i = 0; i < n; i++) t = fe_sq(t);
+  for (int i = 0; i < n; i++) t = fe_sq_pow(t);
   return t;
 }
 
