@@ -1806,7 +1806,18 @@ int plan_build(ouro_tpraos_plan* p) {
   OURO_HIP(hipMemset(p->res, 0, sizeof(int32_t) * slot_region_words(p->cap, kLatResWords)));
   OURO_HIP(hipMalloc(&p->scratch, sizeof(int32_t) * lowlat_scratch_words(ds, p->cap)));
   memset(p->h_in, 0, p->in_bytes);
-  uint8_t* d = p->d_in;
+  // OURO_PLAN_STAGE (the window's copies, read here once): 0 = copy nodes in
+  // and out; 1 = a copy kernel reads the pinned input block; 2 (default) =
+  // that, and the latency kernel writes the results straight into the pinned
+  // output block -- one node fewer, 2-3 us of the window (profiles/r04c:
+  // ablat_plan_stage.json, lat_phases.json; the copy nodes' own time is
+  // ~5 us each, the rest is the graph's node-to-node dispatch); 3 = no input
+  // copy either: the latency kernel reads the pinned block over PCIe (A/B)
+  if (const char* e = getenv("OURO_PLAN_STAGE")) p->stage = atoi(e);
+  if (const char* e = getenv("OURO_PLAN_SPIN")) p->spin = atoi(e);
+  void* hin = nullptr;
+  if (p->stage >= 1) OURO_HIP(hipHostGetDevicePointer(&hin, p->h_in, 0));
+  uint8_t* d = p->stage >= 3 ? static_cast<uint8_t*>(hin) : p->d_in;
   ouro_tpraos_batch& b = p->dev_batch;
   b.n = p->cap;
   b.issuer_vk = d + p->off[0];
@@ -1832,14 +1843,6 @@ int plan_build(ouro_tpraos_plan* p) {
   uint8_t* dbe = dver + align16(p->cap);
   uint8_t* dbl = dbe + 64 * p->cap;
   b.eta_nonce = dbl + 64 * p->cap;  // written only when the option bit says so
-  // OURO_PLAN_STAGE (the window's copies, read here once): 0 = copy nodes in
-  // and out; 1 = a copy kernel reads the pinned input block; 2 (default) =
-  // that, and the latency kernel writes the results straight into the pinned
-  // output block -- one node fewer, 2-3 us of the window (profiles/r04c:
-  // ablat_plan_stage.json, lat_phases.json; the copy nodes' own time is
-  // ~5 us each, the rest is the graph's node-to-node dispatch)
-  if (const char* e = getenv("OURO_PLAN_STAGE")) p->stage = atoi(e);
-  if (const char* e = getenv("OURO_PLAN_SPIN")) p->spin = atoi(e);
   if (p->stage >= 2) {
     void* hout = nullptr;
     OURO_HIP(hipHostGetDevicePointer(&hout, p->h_out, 0));
@@ -1849,17 +1852,15 @@ int plan_build(ouro_tpraos_plan* p) {
     b.eta_nonce = dbl + 64 * p->cap;
   }
   OURO_HIP(hipStreamBeginCapture(p->st, hipStreamCaptureModeThreadLocal));
-  if (p->stage >= 1) {
-    void* hin = nullptr;
-    OURO_HIP(hipHostGetDevicePointer(&hin, p->h_in, 0));
+  if (p->stage == 1 || p->stage == 2) {
     const size_t n16 = p->in_bytes / 16;  // in_bytes is a multiple of 16
     hipLaunchKernelGGL(k_plan_stage, dim3((unsigned)((n16 + 255) / 256)), dim3(256), 0, p->st,
                        static_cast<const uint4*>(hin), reinterpret_cast<uint4*>(p->d_in), n16);
-  } else {
+  } else if (p->stage <= 0) {
     OURO_HIP(hipMemcpyAsync(p->d_in, p->h_in, p->in_bytes, hipMemcpyHostToDevice, p->st));
   }
-  rc = launch_lowlat(p->st, b, reinterpret_cast<const uint32_t*>(p->d_in), p->cap, p->res,
-                     p->scratch, dver, dbe, dbl);
+  rc = launch_lowlat(p->st, b, reinterpret_cast<const uint32_t*>(d), p->cap, p->res, p->scratch,
+                     dver, dbe, dbl);
   if (rc) {
     hipGraph_t g;
     (void)hipStreamEndCapture(p->st, &g);

@@ -3,7 +3,7 @@ the GPU (their measurements: DESIGN.md §4 "Measured design alternatives"):
 
 * OURO_SPLIT=1 -- the split kernels (pre / dsm at 4 waves per SIMD / post)
   for headers, Ed25519 and Sum6KES (rejected on time, kept bit-exact);
-* OURO_PLAN_STAGE=0 / 1 / 2 -- a latency plan's window copies (2, the
+* OURO_PLAN_STAGE=0 / 1 / 2 / 3 -- a latency plan's window copies (2, the
   default: copy kernel in, results written by the latency kernel straight
   into the pinned block), with and without the eta nonce output.
 
@@ -80,7 +80,7 @@ def test_split_ed25519_and_kes_match_oracle(gpu_lib, monkeypatch):
     np.testing.assert_array_equal(got, want)
 
 
-@pytest.mark.parametrize("stage", ["0", "1", "2"])
+@pytest.mark.parametrize("stage", ["0", "1", "2", "3"])
 def test_plan_stage_forms_match_oracle(gpu_lib, kats, monkeypatch, stage):
     from ouroboros_network_amd.tpraos import HeaderPlan
 
