@@ -51,6 +51,7 @@ struct SgcdMat { int32_t u, v, q, r; };
 // (f, g) to (u f + v g, q f + r g) / 2^30.
 OURO_FI int32_t sgcd_divsteps30(int32_t eta, uint32_t f, uint32_t g, SgcdMat& t) {
   uint32_t u = 1, v = 0, q = 0, r = 1;
+  uint32_t nfi = 0u - sgcd_inv32(f);  // -1 / f mod 2^32, recomputed when f changes
   int i = 30;
 #pragma unroll 1
   for (;;) {
@@ -69,11 +70,12 @@ OURO_FI int32_t sgcd_divsteps30(int32_t eta, uint32_t f, uint32_t g, SgcdMat& t)
       tmp = f; f = g; g = 0u - tmp;
       tmp = u; u = q; q = 0u - tmp;
       tmp = v; v = r; r = 0u - tmp;
+      nfi = 0u - sgcd_inv32(f);
     }
     // then g <- (g + w f) / 2^k steps: cancel limit low bits of g at once
     const int limit = (eta + 1) > i ? i : (eta + 1);
     const uint32_t m = 0xffffffffu >> (32 - limit);
-    const uint32_t w = (g * (0u - sgcd_inv32(f))) & m;
+    const uint32_t w = (g * nfi) & m;
     g += f * w;
     q += u * w;
     r += v * w;

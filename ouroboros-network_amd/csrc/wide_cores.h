@@ -8,6 +8,7 @@
 #pragma once
 #include "tpraos.h"
 #include "wide.h"
+#include "wide_inv.h"
 
 namespace ouro {
 // the latency probe's stamp table (lstamp below; host and device passes both
@@ -408,14 +409,23 @@ __device__ __forceinline__ bool vrf03_verify_wide(uint32_t beta[16], const uint3
 }
 
 // ---- fused mode: each core encodes the points it makes ----------------------
-// Z^-1 on the wave (z^(p-2): ~265 wave-wide products, 12 us less than the
-// lane's divsteps inversion, OURO_WIDE_INV=0)
+// Z^-1 on the wave: 2 (the default since round 4) = the divsteps with the
+// operand updates spread over the lanes (wide_inv.h fe_invert_wave): configs[4]
+// p50 0.2137 -> 0.2060 ms against 1 = z^(p-2) (~265 wave-wide products,
+// profiles/r04k/ablat_wave_inversion.json), which was itself 12 us faster
+// than the lane's divsteps inversion (0)
 #ifndef OURO_WIDE_INV
-#define OURO_WIDE_INV 1
+#define OURO_WIDE_INV 2
 #endif
 __device__ __forceinline__ fe invert_wide(const fe& z) {
+  if (OURO_WIDE_INV == 2) return fe_invert_wave(z);
   if (OURO_WIDE_INV) return fw_to_fe(fw_invert(fe_to_fw(z, lanes())));
   return fe_invert_vartime(z);
+}
+// the same for a wave-wide element (replicated rows)
+__device__ __forceinline__ int32_t fw_invert_sel(int32_t z, const Lanes& L) {
+  if (OURO_WIDE_INV == 2) return fe_to_fw(fe_invert_wave(fw_to_fe(z)), L);
+  return fw_invert(z);
 }
 // canonical encoding of a p2 point (one inversion)
 __device__ __forceinline__ void encode_p2(uint32_t enc[8], const ge_p2& P) {
@@ -483,7 +493,7 @@ __device__ __forceinline__ void enc_from_rows(uint32_t out[8], int32_t c, int rx
 // layer of row products (rows 0 / 1)
 __device__ __forceinline__ void encode1_wide(uint32_t enc[8], const pw& P) {
   const Lanes L = lanes();
-  const int32_t zi = fw_invert(P.Z);
+  const int32_t zi = fw_invert_sel(P.Z, L);
   const int32_t c = fw_mul(L.odd ? P.Y : P.X, zi, L);
   enc_from_rows(enc, c, 0, 1);
 }
@@ -492,7 +502,7 @@ __device__ __forceinline__ void encode1_wide(uint32_t enc[8], const pw& P) {
 __device__ __forceinline__ void encode2_wide(uint32_t Henc[8], uint32_t Venc[8], const pw& H,
                                              const pw& V) {
   const Lanes L = lanes();
-  const int32_t inv = fw_invert(fw_mul_rep(H.Z, V.Z, L));
+  const int32_t inv = fw_invert_sel(fw_mul_rep(H.Z, V.Z, L), L);
   lstamp(6);
   const fw4 zi = fw_gather(fw_mul(inv, L.odd ? H.Z : V.Z, L));  // r0 = 1/ZH, r1 = 1/ZV
   const int32_t c = fw_mul(sel4(H.X, H.Y, V.X, V.Y, L), L.high ? zi.r1 : zi.r0, L);
