@@ -50,7 +50,7 @@ for r in range(%d):
     torch.cuda.synchronize()
     assert lib.ouro_debug_lat_stamps(buf) == 16 * 24
     rows.append(list(buf))
-assert os.environ.get("OURO_LAT_SKIP") or (out[0] == 15).all()
+assert os.environ.get("OURO_LAT_SKIP") or ((out[0] & 15) == 15).all()
 plan.close()
 print(json.dumps(rows))
 """
