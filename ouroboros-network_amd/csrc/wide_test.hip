@@ -106,8 +106,22 @@ __global__ void __launch_bounds__(WT_BOUNDS) k_wide_selftest(uint64_t seed, int3
   res[2] = ok && same_fe(fw_to_fe(sq), sq_ref);
   // 3: z^(2^252 - 3)
   // (and z^(p - 2), the wave-wide inversion)
+  // (and the inversion by divsteps with lane-parallel updates, wide_inv.h,
+  // on a, b and the edges 0, 1, p - 1 and 2^255 - 1 = p + 18, unreduced)
+  uint32_t ew[4][8] = {{0}, {1}, {0xffffffecu}, {0xffffffffu}};
+#pragma unroll
+  for (int k = 1; k < 8; k++) {
+    ew[2][k] = k == 7 ? 0x7fffffffu : 0xffffffffu;
+    ew[3][k] = k == 7 ? 0x7fffffffu : 0xffffffffu;
+  }
+  bool inv_ok = same_fe(fe_invert_wave(a), fe_invert(a)) && same_fe(fe_invert_wave(b), fe_invert(b));
+#pragma unroll 1
+  for (int k = 0; k < 4; k++) {
+    const fe z = fe_from_words(ew[k]);
+    inv_ok = inv_ok && same_fe(fe_invert_wave(z), fe_invert(z));
+  }
   res[3] = same_fe(fw_to_fe(fw_pow22523(fe_to_fw(a, L))), fe_pow22523(a)) &&
-           same_fe(fw_to_fe(fw_invert(fe_to_fw(b, L))), fe_invert(b));
+           same_fe(fw_to_fe(fw_invert(fe_to_fw(b, L))), fe_invert(b)) && inv_ok;
   // points: Elligator2 images
   const ge_p3 P = elligator2_h(wa), Q = elligator2_h(wb);
   const pw Pw = pw_from_p3(P, L), Qw = pw_from_p3(Q, L);
