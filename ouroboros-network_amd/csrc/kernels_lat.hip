@@ -19,6 +19,7 @@
 #include "launch.h"
 
 #include "wide_cores.h"
+#include "wide_blake2b.h"
 
 // A/B switch: 1 = the V core computes the whole V = [s]H - [c]Gamma (Gamma
 // decoded on its other rows); 0 = -[c]Gamma on the Gamma core and the second
@@ -39,6 +40,18 @@
 #endif
 
 using namespace ouro;
+
+// mkSeed's Blake2b on the lane quads (wide_blake2b.h, 1) or on one lane
+// (tpraos.h hdr_seed, 0) in the V / V2 items (node configuration)
+#ifndef OURO_SEED_QUAD
+#define OURO_SEED_QUAD 1
+#endif
+__device__ __forceinline__ void lat_seed(SeedMsg& a, const ouro_tpraos_batch& b, size_t i,
+                                         bool leader, uint32_t opts) {
+  if (OURO_SEED_QUAD) hdr_seed_wave(a, b, i, leader, opts);
+  else hdr_seed(a, b, i, leader, opts);
+}
+
 
 // One core of header i on one wave (wide_cores.h): the same checks and the
 // same record fields (lane 0 stores) as hdr_core with split V on a lane or
@@ -101,7 +114,7 @@ __device__ __noinline__ void hdr_core_wide(const ouro_tpraos_batch& b, size_t i,
       ld_words(p, b.vrf_vk + 32 * i, 2);
       ld_words(pi, (leader ? b.leader_proof : b.eta_proof) + 80 * i, 5);
       SeedMsg alpha;
-      hdr_seed(alpha, b, i, leader, opts);
+      lat_seed(alpha, b, i, leader, opts);
       if (fused && OURO_V_WHOLE) {
         uint32_t Henc[8], Venc[8];
         vrf_v_full_wide(Henc, Venc, p, pi, alpha);
@@ -305,7 +318,7 @@ __device__ __noinline__ void hdr_item_fused(const ouro_tpraos_batch& b, size_t i
       ld_words(p, b.vrf_vk + 32 * i, 2);
       ld_words(pi, (which ? b.leader_proof : b.eta_proof) + 80 * i, 5);
       SeedMsg alpha;
-      hdr_seed(alpha, b, i, which != 0, opts);
+      lat_seed(alpha, b, i, which != 0, opts);
       vrf_sh_split(res + kLatVsplit + 4 * kPwWords * which, p, pi, alpha, true);
     }
     if (!arrive_last(res.word(kLatCtr + 1 + which), gen, 3)) {

@@ -31,6 +31,9 @@ def main():
                          "list of VAR=value set while that plan is created")
     ap.add_argument("--nonce", action="store_true",
                     help="(--libs) request the eta nonce output as a node would")
+    ap.add_argument("--node", action="store_true",
+                    help="the node configuration: claimed outputs, VRF inputs from (slot, eta0) "
+                         "by mkSeed on the device (bench.synth_node_config)")
     ap.add_argument("--libs", nargs="*", default=None,
                     help="A/B build variants of libouro_verify.so instead of an env variable")
     args = ap.parse_args()
@@ -41,9 +44,14 @@ def main():
 
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(0)
-    t, _ = bench.synth_headers(4096, 1024, dev)
-    hdr = bench.DeviceHeaders(t, 4096, dev)
-    hb = hdr.host_sample(args.batch)
+    if args.node:
+        t, _, pool = bench.synth_headers(args.batch, 1024, dev, keep_pool=True)
+        bench.synth_node_config(t, args.batch, 1024, pool, bytes(range(7, 39)), dev)
+        hb = bench.DeviceHeaders(t, args.batch, dev).host_sample(args.batch)
+    else:
+        t, _ = bench.synth_headers(4096, 1024, dev)
+        hdr = bench.DeviceHeaders(t, 4096, dev)
+        hb = hdr.host_sample(args.batch)
     body = int(hb.body_len.astype(np.int64).sum())
     plans, ref = {}, None
     if args.libs:
