@@ -590,10 +590,11 @@ def _plan_latency(hb, iters: int, nonce: bool):
 
 def _plan_phases(hb, iters: int, nonce: bool):
     """Where a window's wall time goes, to explain the latency tail (VERDICT
-    r03 item 5): the plan's submit (copy into pinned staging + graph launch)
-    and wait (until the results are in the caller's buffers) timed on the
-    host, and the GPU time of the graph (H2D, kernel, D2H) from events the
-    plan records around its launch (OURO_PLAN_TIMING; a separate pass, so the
+    r03 item 5): the plan's submit (copy into pinned staging + the launch
+    calls) and wait (until the results are in the caller's buffers) timed on
+    the host, and the GPU time of the window (input copy kernel, latency
+    kernel; "gpu_graph" keeps its round-4 name) from events the plan records
+    around its launches (OURO_PLAN_TIMING; a separate pass, so the
     headline windows carry no events).  host_gap = wall - gpu: launch latency
     + completion wake-up + the host copies."""
     from ouroboros_network_amd.tpraos import HeaderPlan
@@ -641,7 +642,7 @@ def _plan_phases(hb, iters: int, nonce: bool):
                                     "submit": round(ph[i, 0] * 1e6, 1),
                                     "wait": round(ph[i, 1] * 1e6, 1),
                                     "gpu_graph": round(ph[i, 2] * 1e6, 1)} for i in worst],
-            "note": "events around the graph launch (OURO_PLAN_TIMING) in a separate pass; "
+            "note": "events around the window's launches (OURO_PLAN_TIMING) in a separate pass; "
                     "host_gap = wall - gpu_graph (launch latency, completion wake-up, "
                     "host copies)"}
 
@@ -653,8 +654,8 @@ def _pcts(lat):
 
 def latency_leg(hdr, batch: int, iters: int, cpu_threads: int, cpu_iters: int, node=None):
     """configs[4]: ChainSync small-batch path.  `batch` headers from host
-    memory through the captured hipGraph plan (H2D, the fused latency kernel,
-    D2H), wall-clock per call over `iters` windows (p50 / p99 / p99.9); next to
+    memory through a plan (pinned staging, its input copy kernel and the fused
+    latency kernel writing into pinned memory), wall-clock per call over `iters` windows (p50 / p99 / p99.9); next to
     the CPU oracle on the same batch on 1 core and on `cpu_threads` cores.
     `node` (a DeviceHeaders in the node's configuration, synth_node_config):
     the same timing with claimed outputs, (slot, eta0) seeds derived on the
@@ -699,7 +700,7 @@ def latency_leg(hdr, batch: int, iters: int, cpu_threads: int, cpu_iters: int, n
 
     c1, cn = cpu_lat(1), cpu_lat(cpu_threads)
     ms = lambda a, q: round(float(np.percentile(a, q)) * 1e3, 3)  # noqa: E731
-    res = {"workload": f"configs[4]: {batch}-header batches from host memory, hipGraph plan "
+    res = {"workload": f"configs[4]: {batch}-header batches from host memory, plan "
                        "(minimal configuration: caller alphas, no claimed outputs, no nonce)",
            "iters": iters, **_pcts(lat),
            "headers_per_s_at_p50": round(batch / (np.percentile(lat, 50)), 1),

@@ -429,9 +429,12 @@ int ouro_debug_thread_cpus(int *cpus, int max);
 int ouro_tpraos_verify_batch_multi(const ouro_tpraos_batch *b, const int *devices, int ndev,
                                    uint8_t *verdict, uint8_t *beta_eta, uint8_t *beta_leader);
 
-/* A captured plan for repeated fixed-capacity batches: pinned staging and one
- * hipGraph (H2D, the two latency-mode kernels, D2H) replayed per call.  A plan
- * is used by one thread at a time; any n <= max_headers per run. */
+/* A plan for repeated fixed-capacity batches: pinned staging, device buffers
+ * and the latency kernel's launch shape fixed at create; each run issues the
+ * window's input copy kernel and the fused latency kernel on the plan's own
+ * stream (OURO_PLAN_GRAPH=1 at create: replayed from one captured hipGraph
+ * instead).  A plan is used by one thread at a time; any n <= max_headers per
+ * run. */
 typedef struct ouro_tpraos_plan ouro_tpraos_plan;
 ouro_tpraos_plan *ouro_tpraos_plan_create(size_t max_headers, size_t max_body_bytes);
 int ouro_tpraos_plan_run(ouro_tpraos_plan *plan, const ouro_tpraos_batch *b, uint8_t *verdict,
@@ -444,7 +447,7 @@ void ouro_tpraos_plan_destroy(ouro_tpraos_plan *plan);
  * validates each window as its headers arrive,
  * ouroboros-consensus/src/Ouroboros/Consensus/MiniProtocol/ChainSync/Client.hs:792).
  * submit copies the batch into the plan's pinned staging and launches its
- * graph, returning at once (the caller's input buffers are free again on
+ * kernels, returning at once (the caller's input buffers are free again on
  * return); wait blocks until that batch's results are in the caller's buffers.
  * One batch in flight per plan: a second submit before wait, or a wait with
  * nothing submitted, returns OURO_EINVAL.  Several plans = several windows in
@@ -494,9 +497,9 @@ int ouro_debug_host_path(unsigned long long *single_items,
 
 /* TIMING PROBE (bench.py latency phases) of the plan's last waited-for
  * window, when OURO_PLAN_TIMING was set in the environment at its submit (-1
- * otherwise): gpu_ms = events recorded around its graph launch (H2D, the
- * latency kernel, D2H); copy_us / launch_us = host time of submit's copy into
- * the pinned block and of the graph launch call.  Any pointer may be NULL. */
+ * otherwise): gpu_ms = events recorded around its launches (input copy, the
+ * latency kernel, output); copy_us / launch_us = host time of submit's copy
+ * into the pinned block and of the launch calls.  Any pointer may be NULL. */
 int ouro_debug_plan_timing(ouro_tpraos_plan *plan, float *gpu_ms, float *copy_us,
                            float *launch_us);
 

@@ -895,9 +895,17 @@ int lat_fuse() {
 // latency mode: eight cores per header (x4 lanes in quad mode), then the
 // finish; n and the option bits read from d_n[0..1].
 // Lanes used <= the kBlock-rounded count lowlat_scratch_words provides for.
-int launch_lowlat(hipStream_t st, const ouro_tpraos_batch& b, const uint32_t* d_n, size_t n_cap,
-                  int32_t* res_buf, int32_t* scratch, uint8_t* verdict, uint8_t* be,
-                  uint8_t* bl) {
+// The launch shape (grids, option bits: the OURO_LAT_* switches) is fixed per
+// capacity; a plan computes it once at build (lat_shape) and issues it per
+// window (lat_issue) when it launches without a graph.
+struct LatShape {
+  int g1 = 0, g2 = 0, blk = 0, quad = 0, wide_lanes = 0;
+  bool fused = false;
+  uint32_t flags = 0;
+  const int32_t* btab = nullptr;
+};
+
+int lat_shape(size_t n_cap, LatShape* s) {
   DeviceState* ds;
   int rc = device_state(&ds);
   if (rc) return rc;
@@ -919,19 +927,37 @@ int launch_lowlat(hipStream_t st, const ouro_tpraos_batch& b, const uint32_t* d_
   const size_t wide_waves = (size_t)(fused ? lat_fused_items_host() : nwide) * n_cap;
   const size_t wide_blocks = (wide_waves * 64 + blk - 1) / blk;
   const size_t quad_items = (size_t)(kLatCores - nwide) * n_cap;
-  const int g1 = (int)wide_blocks + grid(quad_items << (quad ? 2 : 0), kCores);
-  const int g2 = grid(n_cap << (quad ? 2 : 0), kFinish);
   // timing probe: OURO_LAT_SKIP = mask of cores left out (verdicts then wrong)
   const char* skip_env = getenv("OURO_LAT_SKIP");
   const int skip = skip_env ? (int)(strtol(skip_env, nullptr, 0) & 0xff) : 0;
-  hipLaunchKernelGGL(k_tpraos_cores, dim3(g1), dim3(blk), 0, st, b, d_n, res_buf, scratch,
-                     ds->btab, quad | (skip << 8) | (wmask << 16) | (fused ? 1 << 24 : 0) |
-                                   (getenv("OURO_LAT_STAMPS") ? 1 << 25 : 0),
-                     (int)(wide_blocks * blk / 64), verdict, be, bl);
-  if ((rc = launch_check())) return rc;
-  if (fused) return OURO_OK;
-  hipLaunchKernelGGL(k_tpraos_finish, dim3(g2), dim3(blk), 0, st, b, d_n, res_buf, verdict, be,
-                     bl, scratch, quad);
+  s->g1 = (int)wide_blocks + grid(quad_items << (quad ? 2 : 0), kCores);
+  s->g2 = grid(n_cap << (quad ? 2 : 0), kFinish);
+  s->blk = blk;
+  s->quad = quad;
+  s->wide_lanes = (int)(wide_blocks * blk / 64);
+  s->fused = fused;
+  s->flags = (uint32_t)(quad | (skip << 8) | (wmask << 16) | (fused ? 1 << 24 : 0) |
+                        (getenv("OURO_LAT_STAMPS") ? 1 << 25 : 0));
+  s->btab = ds->btab;
+  return OURO_OK;
+}
+
+void lat_issue(hipStream_t st, const LatShape& s, const ouro_tpraos_batch& b, const uint32_t* d_n,
+               int32_t* res_buf, int32_t* scratch, uint8_t* verdict, uint8_t* be, uint8_t* bl) {
+  hipLaunchKernelGGL(k_tpraos_cores, dim3(s.g1), dim3(s.blk), 0, st, b, d_n, res_buf, scratch,
+                     s.btab, (int)s.flags, s.wide_lanes, verdict, be, bl);
+  if (s.fused) return;
+  hipLaunchKernelGGL(k_tpraos_finish, dim3(s.g2), dim3(s.blk), 0, st, b, d_n, res_buf, verdict, be,
+                     bl, scratch, s.quad);
+}
+
+int launch_lowlat(hipStream_t st, const ouro_tpraos_batch& b, const uint32_t* d_n, size_t n_cap,
+                  int32_t* res_buf, int32_t* scratch, uint8_t* verdict, uint8_t* be,
+                  uint8_t* bl) {
+  LatShape s;
+  int rc = lat_shape(n_cap, &s);
+  if (rc) return rc;
+  lat_issue(st, s, b, d_n, res_buf, scratch, verdict, be, bl);
   return launch_check();
 }
 
@@ -1718,7 +1744,11 @@ __global__ void __launch_bounds__(256) k_plan_stage(const uint4* __restrict__ sr
   if (i < n16) dst[i] = src[i];
 }
 
-// ---- captured plans: pinned staging + hipGraph (H2D, 2 kernels, D2H) --------
+// ---- plans: pinned staging, the window's copy kernel + latency kernel -------
+// issued straight on the plan's stream per window (default), or replayed from
+// one captured hipGraph (OURO_PLAN_GRAPH=1, A/B): the graph's GPU-side
+// dispatch of its two kernel nodes cost 8-10 us more per window than two
+// stream launches (profiles/r04m/ablat_plan_graph.json, lat_phases_graph.json).
 // The packed input block: 16 bytes {n, option bits (tpraos.h kOpt*), the
 // launch's generation (wide_cores.h arrive_last), 0}, then
 // every member of ouro_tpraos_batch in order, each 16-byte aligned at
@@ -1751,13 +1781,17 @@ struct ouro_tpraos_plan {
   bool inflight = false;
   bool failed = false;           // its launch failed: wait recomputes it on the host path
   // TIMING PROBE (OURO_PLAN_TIMING set at submit; bench.py latency phases):
-  // events around the graph launch on the plan's stream
+  // events around the window's launches on the plan's stream
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   bool timed = false;
   float last_gpu_ms = -1.0f;
   float copy_us = -1.0f, launch_us = -1.0f;  // host side of its last submit
   int stage = 2;  // OURO_PLAN_STAGE at capture (plan_build)
   int spin = 0;   // OURO_PLAN_SPIN at capture: wait spins on hipStreamQuery
+  int use_graph = 0;  // OURO_PLAN_GRAPH at build: 1 = the launches captured into one hipGraph
+  void* hin = nullptr;  // device view of h_in (stage >= 1)
+  uint8_t *dver = nullptr, *dbe = nullptr, *dbl = nullptr;  // the latency kernel's outputs
+  LatShape shape;  // the latency launch at capacity (lat_shape, once)
 };
 
 namespace {
@@ -1776,6 +1810,25 @@ void plan_free(ouro_tpraos_plan* p) {
   if (p->scratch) (void)hipFree(p->scratch);
   if (p->st) (void)hipStreamDestroy(p->st);
   delete p;
+}
+
+// the window's launches on the plan's stream: issued per submit (the
+// default), or captured once into the graph (OURO_PLAN_GRAPH=1, A/B)
+int plan_enqueue(ouro_tpraos_plan* p) {
+  if (p->stage == 1 || p->stage == 2) {
+    const size_t n16 = p->in_bytes / 16;  // in_bytes is a multiple of 16
+    hipLaunchKernelGGL(k_plan_stage, dim3((unsigned)((n16 + 255) / 256)), dim3(256), 0, p->st,
+                       static_cast<const uint4*>(p->hin), reinterpret_cast<uint4*>(p->d_in), n16);
+  } else if (p->stage <= 0) {
+    OURO_HIP(hipMemcpyAsync(p->d_in, p->h_in, p->in_bytes, hipMemcpyHostToDevice, p->st));
+  }
+  const uint8_t* d = p->stage >= 3 ? static_cast<const uint8_t*>(p->hin) : p->d_in;
+  lat_issue(p->st, p->shape, p->dev_batch, reinterpret_cast<const uint32_t*>(d), p->res,
+            p->scratch, p->dver, p->dbe, p->dbl);
+  OURO_HIP(hipGetLastError());
+  if (p->stage < 2)
+    OURO_HIP(hipMemcpyAsync(p->h_out, p->d_out, p->out_bytes, hipMemcpyDeviceToHost, p->st));
+  return OURO_OK;
 }
 
 size_t field_cap_bytes(const ouro_tpraos_plan* p, int f) {
@@ -1806,18 +1859,19 @@ int plan_build(ouro_tpraos_plan* p) {
   OURO_HIP(hipMemset(p->res, 0, sizeof(int32_t) * slot_region_words(p->cap, kLatResWords)));
   OURO_HIP(hipMalloc(&p->scratch, sizeof(int32_t) * lowlat_scratch_words(ds, p->cap)));
   memset(p->h_in, 0, p->in_bytes);
-  // OURO_PLAN_STAGE (the window's copies, read here once): 0 = copy nodes in
+  // OURO_PLAN_STAGE (the window's copies, read here once): 0 = DMA copies in
   // and out; 1 = a copy kernel reads the pinned input block; 2 (default) =
   // that, and the latency kernel writes the results straight into the pinned
   // output block -- one node fewer, 2-3 us of the window (profiles/r04c:
   // ablat_plan_stage.json, lat_phases.json; the copy nodes' own time is
   // ~5 us each, the rest is the graph's node-to-node dispatch); 3 = no input
-  // copy either: the latency kernel reads the pinned block over PCIe (A/B)
+  // copy either: the latency kernel reads the pinned block over PCIe (A/B).
+  // OURO_PLAN_GRAPH=1: capture them into a hipGraph (the form before r04m).
   if (const char* e = getenv("OURO_PLAN_STAGE")) p->stage = atoi(e);
   if (const char* e = getenv("OURO_PLAN_SPIN")) p->spin = atoi(e);
-  void* hin = nullptr;
-  if (p->stage >= 1) OURO_HIP(hipHostGetDevicePointer(&hin, p->h_in, 0));
-  uint8_t* d = p->stage >= 3 ? static_cast<uint8_t*>(hin) : p->d_in;
+  if (const char* e = getenv("OURO_PLAN_GRAPH")) p->use_graph = atoi(e) != 0;
+  if (p->stage >= 1) OURO_HIP(hipHostGetDevicePointer(&p->hin, p->h_in, 0));
+  uint8_t* d = p->stage >= 3 ? static_cast<uint8_t*>(p->hin) : p->d_in;
   ouro_tpraos_batch& b = p->dev_batch;
   b.n = p->cap;
   b.issuer_vk = d + p->off[0];
@@ -1851,23 +1905,18 @@ int plan_build(ouro_tpraos_plan* p) {
     dbl = dbe + 64 * p->cap;
     b.eta_nonce = dbl + 64 * p->cap;
   }
+  p->dver = dver;
+  p->dbe = dbe;
+  p->dbl = dbl;
+  if ((rc = lat_shape(p->cap, &p->shape))) return rc;
+  if (!p->use_graph) return OURO_OK;
   OURO_HIP(hipStreamBeginCapture(p->st, hipStreamCaptureModeThreadLocal));
-  if (p->stage == 1 || p->stage == 2) {
-    const size_t n16 = p->in_bytes / 16;  // in_bytes is a multiple of 16
-    hipLaunchKernelGGL(k_plan_stage, dim3((unsigned)((n16 + 255) / 256)), dim3(256), 0, p->st,
-                       static_cast<const uint4*>(hin), reinterpret_cast<uint4*>(p->d_in), n16);
-  } else if (p->stage <= 0) {
-    OURO_HIP(hipMemcpyAsync(p->d_in, p->h_in, p->in_bytes, hipMemcpyHostToDevice, p->st));
-  }
-  rc = launch_lowlat(p->st, b, reinterpret_cast<const uint32_t*>(d), p->cap, p->res, p->scratch,
-                     dver, dbe, dbl);
-  if (rc) {
-    hipGraph_t g;
+  if ((rc = plan_enqueue(p))) {
+    hipGraph_t g = nullptr;
     (void)hipStreamEndCapture(p->st, &g);
+    if (g) (void)hipGraphDestroy(g);
     return rc;
   }
-  if (p->stage < 2)
-    OURO_HIP(hipMemcpyAsync(p->h_out, p->d_out, p->out_bytes, hipMemcpyDeviceToHost, p->st));
   OURO_HIP(hipStreamEndCapture(p->st, &p->graph));
   OURO_HIP(hipGraphInstantiate(&p->exec, p->graph, nullptr, nullptr, 0));
   return OURO_OK;
@@ -2003,7 +2052,10 @@ int ouro_tpraos_plan_submit(ouro_tpraos_plan* p, const ouro_tpraos_batch* b) {
   }
   if (p->timed && e == hipSuccess) e = hipEventRecord(p->ev0, p->st);
   const auto tl0 = std::chrono::steady_clock::now();
-  if (e == hipSuccess && !injected) e = hipGraphLaunch(p->exec, p->st);
+  if (e == hipSuccess && !injected) {
+    if (p->exec) e = hipGraphLaunch(p->exec, p->st);
+    else if (plan_enqueue(p) != OURO_OK) e = hipErrorLaunchFailure;
+  }
   if (p->timed)
     p->launch_us = std::chrono::duration<float, std::micro>(std::chrono::steady_clock::now() - tl0).count();
   if (p->timed && e == hipSuccess) e = hipEventRecord(p->ev1, p->st);
@@ -2142,7 +2194,7 @@ int ouro_leader_check_batch_host(size_t n, const uint8_t* beta, const uint64_t* 
 }
 
 // TIMING PROBE: the GPU time of the plan's last waited-for window (events
-// around its graph launch: H2D, the latency kernel, D2H), recorded when
+// around its launches: input copy, the latency kernel, output), recorded when
 // OURO_PLAN_TIMING was set at its submit; -1 otherwise.
 int ouro_debug_plan_timing(ouro_tpraos_plan* p, float* gpu_ms, float* copy_us, float* launch_us) {
   if (!p) return fail(OURO_EINVAL, "null plan");

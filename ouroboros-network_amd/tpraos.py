@@ -235,8 +235,9 @@ def verify_headers_lowlat(batch: HeaderBatch, nonce: bool = False):
 
 
 class HeaderPlan:
-    """A captured hipGraph plan for repeated batches of <= max_headers
-    (the ChainSync small-batch path, BASELINE.json configs[4])."""
+    """A plan (pinned staging, the latency kernel's launch fixed at create)
+    for repeated batches of <= max_headers (the ChainSync small-batch path,
+    BASELINE.json configs[4]); include/ouro_verify.h ouro_tpraos_plan_*."""
 
     def __init__(self, max_headers: int = 64, max_body_bytes: int = 64 * 1400):
         self._lib = _native.load()
