@@ -316,7 +316,8 @@ __global__ void k_tpraos_cores(ouro_tpraos_batch b, const uint32_t* __restrict__
                                int32_t* res_buf, int32_t* scratch,
                                const int32_t* __restrict__ btab, int mode, int wide_waves,
                                uint8_t* __restrict__ verdict, uint8_t* __restrict__ beta_eta,
-                               uint8_t* __restrict__ beta_leader);
+                               uint8_t* __restrict__ beta_leader, uint32_t* win_ctr,
+                               uint32_t* done);
 int lat_fused_items_host();  // kernels_lat.hip: waves per header of the fused launch
 int lat_stamps_read(unsigned long long* out);  // kernels_lat.hip: the latency probe's stamps
 __global__ void k_ed25519_wide(size_t n, const uint8_t* __restrict__ pk,
@@ -942,10 +943,12 @@ int lat_shape(size_t n_cap, LatShape* s) {
   return OURO_OK;
 }
 
+// (win_ctr / done: a plan's window counter and done word, or null)
 void lat_issue(hipStream_t st, const LatShape& s, const ouro_tpraos_batch& b, const uint32_t* d_n,
-               int32_t* res_buf, int32_t* scratch, uint8_t* verdict, uint8_t* be, uint8_t* bl) {
+               int32_t* res_buf, int32_t* scratch, uint8_t* verdict, uint8_t* be, uint8_t* bl,
+               uint32_t* win_ctr = nullptr, uint32_t* done = nullptr) {
   hipLaunchKernelGGL(k_tpraos_cores, dim3(s.g1), dim3(s.blk), 0, st, b, d_n, res_buf, scratch,
-                     s.btab, (int)s.flags, s.wide_lanes, verdict, be, bl);
+                     s.btab, (int)s.flags, s.wide_lanes, verdict, be, bl, win_ctr, done);
   if (s.fused) return;
   hipLaunchKernelGGL(k_tpraos_finish, dim3(s.g2), dim3(s.blk), 0, st, b, d_n, res_buf, verdict, be,
                      bl, scratch, s.quad);
@@ -1792,12 +1795,20 @@ struct ouro_tpraos_plan {
   void* hin = nullptr;  // device view of h_in (stage >= 1)
   uint8_t *dver = nullptr, *dbe = nullptr, *dbl = nullptr;  // the latency kernel's outputs
   LatShape shape;  // the latency launch at capacity (lat_shape, once)
+  // OURO_PLAN_FLAG (default 1; stage 2, fused kernel): the latency kernel's
+  // last header tail writes the generation into a done word in the pinned
+  // output block, and wait spins on it instead of the stream's completion
+  bool flag = false;
+  uint32_t* done_dev = nullptr;              // that word as the kernel sees it
+  const volatile uint32_t* done_host = nullptr;
 };
 
 namespace {
 void plan_free(ouro_tpraos_plan* p) {
   if (!p) return;
-  if (p->inflight && p->st) (void)hipStreamSynchronize(p->st);  // no DMA into freed staging
+  // no DMA into freed staging (and, with the done word, a waited-for launch
+  // may still be retiring its last waves)
+  if (p->st) (void)hipStreamSynchronize(p->st);
   if (p->ev0) (void)hipEventDestroy(p->ev0);
   if (p->ev1) (void)hipEventDestroy(p->ev1);
   if (p->exec) (void)hipGraphExecDestroy(p->exec);
@@ -1823,8 +1834,10 @@ int plan_enqueue(ouro_tpraos_plan* p) {
     OURO_HIP(hipMemcpyAsync(p->d_in, p->h_in, p->in_bytes, hipMemcpyHostToDevice, p->st));
   }
   const uint8_t* d = p->stage >= 3 ? static_cast<const uint8_t*>(p->hin) : p->d_in;
+  // the window counter: word 3 of the input block, zeroed by the copy
   lat_issue(p->st, p->shape, p->dev_batch, reinterpret_cast<const uint32_t*>(d), p->res,
-            p->scratch, p->dver, p->dbe, p->dbl);
+            p->scratch, p->dver, p->dbe, p->dbl,
+            p->flag ? reinterpret_cast<uint32_t*>(p->d_in) + 3 : nullptr, p->done_dev);
   OURO_HIP(hipGetLastError());
   if (p->stage < 2)
     OURO_HIP(hipMemcpyAsync(p->h_out, p->d_out, p->out_bytes, hipMemcpyDeviceToHost, p->st));
@@ -1848,7 +1861,7 @@ int plan_build(ouro_tpraos_plan* p) {
     o += align16(field_cap_bytes(p, f));
   }
   p->in_bytes = o;
-  p->out_bytes = align16(p->cap) + 160 * p->cap;
+  p->out_bytes = align16(p->cap) + 160 * p->cap + 64;  // + the done word (OURO_PLAN_FLAG)
   OURO_HIP(hipHostMalloc(&p->h_in, p->in_bytes, hipHostMallocNumaUser));
   OURO_HIP(hipHostMalloc(&p->h_out, p->out_bytes, hipHostMallocNumaUser));
   OURO_HIP(hipMalloc(&p->d_in, p->in_bytes));
@@ -1859,6 +1872,7 @@ int plan_build(ouro_tpraos_plan* p) {
   OURO_HIP(hipMemset(p->res, 0, sizeof(int32_t) * slot_region_words(p->cap, kLatResWords)));
   OURO_HIP(hipMalloc(&p->scratch, sizeof(int32_t) * lowlat_scratch_words(ds, p->cap)));
   memset(p->h_in, 0, p->in_bytes);
+  memset(p->h_out, 0, p->out_bytes);  // the done word starts at 0, never a generation
   // OURO_PLAN_STAGE (the window's copies, read here once): 0 = DMA copies in
   // and out; 1 = a copy kernel reads the pinned input block; 2 (default) =
   // that, and the latency kernel writes the results straight into the pinned
@@ -1909,6 +1923,17 @@ int plan_build(ouro_tpraos_plan* p) {
   p->dbe = dbe;
   p->dbl = dbl;
   if ((rc = lat_shape(p->cap, &p->shape))) return rc;
+  {
+    const char* e = getenv("OURO_PLAN_FLAG");
+    p->flag = p->stage == 2 && p->shape.fused && !(e && atoi(e) == 0);
+    if (p->flag) {
+      uint8_t* w = p->h_out + p->out_bytes - 64;
+      void* wd = nullptr;
+      OURO_HIP(hipHostGetDevicePointer(&wd, w, 0));
+      p->done_dev = static_cast<uint32_t*>(wd);
+      p->done_host = reinterpret_cast<const volatile uint32_t*>(w);
+    }
+  }
   if (!p->use_graph) return OURO_OK;
   OURO_HIP(hipStreamBeginCapture(p->st, hipStreamCaptureModeThreadLocal));
   if ((rc = plan_enqueue(p))) {
@@ -1963,6 +1988,7 @@ ouro_tpraos_batch plan_host_batch(const ouro_tpraos_plan* p) {
 // next launch ignores them.
 int plan_poison(ouro_tpraos_plan* p) {
   OURO_HIP(hipSetDevice(p->dev));
+  OURO_HIP(hipStreamSynchronize(p->st));  // the last launch retired (done word: maybe not yet)
   const size_t words = slot_region_words(p->cap, kLatResWords);
   std::vector<int32_t> h(words);
   OURO_HIP(hipMemcpy(h.data(), p->res, sizeof(int32_t) * words, hipMemcpyDeviceToHost));
@@ -2080,12 +2106,26 @@ int ouro_tpraos_plan_wait(ouro_tpraos_plan* p, uint8_t* verdict, uint8_t* beta_e
   int rc = OURO_OK;
   if (!p->failed) {
     hipError_t e = hipSetDevice(p->dev);
-    if (e == hipSuccess && p->spin) {
+    if (e == hipSuccess && p->flag) {
+      // the kernel's done word; the stream is asked now and then, so a launch
+      // that never writes it (a fault) still ends the wait with its error
+      for (uint32_t k = 1;; k++) {
+        if (*p->done_host == p->gen) break;
+        if ((k & 255u) == 0) {
+          e = hipStreamQuery(p->st);
+          if (e != hipErrorNotReady) break;
+          e = hipSuccess;
+        }
+        __builtin_ia32_pause();
+      }
+      std::atomic_thread_fence(std::memory_order_acquire);
+      if (e == hipSuccess && p->timed) e = hipEventSynchronize(p->ev1);
+    } else if (e == hipSuccess && p->spin) {
       // poll the stream instead of the runtime's wait, which may sleep on the
       // completion interrupt
       while ((e = hipStreamQuery(p->st)) == hipErrorNotReady) __builtin_ia32_pause();
     }
-    if (e == hipSuccess) e = hipStreamSynchronize(p->st);
+    if (e == hipSuccess && !p->flag) e = hipStreamSynchronize(p->st);
     if (e != hipSuccess) rc = fail(OURO_EDEVICE, std::string("plan wait: ") + hipGetErrorString(e));
   } else {
     rc = OURO_EDEVICE;

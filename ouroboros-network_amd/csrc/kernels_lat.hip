@@ -196,7 +196,8 @@ constexpr int kFusedItems = OURO_LAT_SPLIT ? kLatCores + 6 : kLatCores + 2;
 #ifndef OURO_LAT_STAMPS
 #define OURO_LAT_STAMPS 0
 #endif
-__device__ __noinline__ void hdr_item_fused(const ouro_tpraos_batch& b, size_t i, uint32_t opts,
+// true when this wave ran the header's tail (its outputs are written)
+__device__ __noinline__ bool hdr_item_fused(const ouro_tpraos_batch& b, size_t i, uint32_t opts,
                                             int item, Slot res, const uint16_t* bw, uint32_t skip,
                                             uint32_t gen,
                                             uint8_t* verdict, uint8_t* beta_eta,
@@ -267,7 +268,7 @@ __device__ __noinline__ void hdr_item_fused(const ouro_tpraos_batch& b, size_t i
     }
     if (!done) {
       stamp("half");
-      return;
+      return false;
     }
     const int32_t flag = (!skipped && eds_combine(ed)) ? kFlagOk : 0;
     if (lead) stg1(res.word(kResFlags + e), flag);
@@ -303,7 +304,7 @@ __device__ __noinline__ void hdr_item_fused(const ouro_tpraos_batch& b, size_t i
     }
     if (!arrive_last(ed.word(125), gen, 2)) {
       stamp("half");
-      return;
+      return false;
     }
     kstamp(3);
     const int32_t flag = (!skipped && ed_chain(ed, bw)) ? kFlagOk : 0;
@@ -323,7 +324,7 @@ __device__ __noinline__ void hdr_item_fused(const ouro_tpraos_batch& b, size_t i
     }
     if (!arrive_last(res.word(kLatCtr + 1 + which), gen, 3)) {
       stamp("half");
-      return;
+      return false;
     }
     if (!(((skip >> (kCoreVe + which)) | (skip >> (kCoreGe + which))) & 1u))
       vrf_split_combine_encode(res, which);
@@ -370,7 +371,7 @@ __device__ __noinline__ void hdr_item_fused(const ouro_tpraos_batch& b, size_t i
       if (OURO_LAT_SPLIT) {
         if (!last) {
           stamp("half");
-          return;
+          return false;
         }
         stamp("work");
         if (!skipped) vrf_split_combine_encode(res, which);
@@ -384,7 +385,11 @@ __device__ __noinline__ void hdr_item_fused(const ouro_tpraos_batch& b, size_t i
   if (arrive_last(res.word(kLatCtr), gen, kHdrParties)) {
     hdr_tail_wide(b, i, opts, res, verdict, beta_eta, beta_leader);
     stamp("tail");
+    return true;
   }
+  return false;
+#else
+  return false;
 #endif
 }
 
@@ -437,7 +442,8 @@ __global__ void __launch_bounds__(kBlock, OURO_LAT_WAVES) k_tpraos_cores(ouro_tp
                                                             int mode, int wide_waves,
                                                             uint8_t* __restrict__ verdict,
                                                             uint8_t* __restrict__ beta_eta,
-                                                            uint8_t* __restrict__ beta_leader) {
+                                                            uint8_t* __restrict__ beta_leader,
+                                                            uint32_t* win_ctr, uint32_t* done) {
   const size_t n = d_n[0];
   const uint32_t opts = d_n[1];
   const uint32_t gen = d_n[2];  // the launch's generation (arrive_last), never 0
@@ -450,10 +456,23 @@ __global__ void __launch_bounds__(kBlock, OURO_LAT_WAVES) k_tpraos_cores(ouro_tp
   const size_t wide_lanes = (size_t)wide_waves * 64;
   if (gtid < wide_lanes && fused) {  // wave-uniform
     const size_t wv = gtid >> 6, i = wv / kFusedItems;
-    if (i < n)
-      hdr_item_fused(b, i, opts, (int)(wv % kFusedItems), slot_of(res_buf, i, kLatResWords),
-                     reinterpret_cast<const uint16_t*>(btab + kBTabWords), skip, gen, verdict,
-                     beta_eta, beta_leader, ((uint32_t)mode >> 25) & 1u);
+    if (i < n &&
+        hdr_item_fused(b, i, opts, (int)(wv % kFusedItems), slot_of(res_buf, i, kLatResWords),
+                       reinterpret_cast<const uint16_t*>(btab + kBTabWords), skip, gen, verdict,
+                       beta_eta, beta_leader, ((uint32_t)mode >> 25) & 1u) &&
+        done) {
+      // the window's done word (a plan's pinned output block, OURO_PLAN_FLAG):
+      // each header's tail releases its outputs to the host and counts itself
+      // in win_ctr (zeroed by the window's input copy); the last one writes the
+      // launch's generation, which the plan's wait spins on instead of the
+      // stream's completion
+      if ((threadIdx.x & 63u) == 0) {
+        const uint32_t prev =
+            __hip_atomic_fetch_add(win_ctr, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (prev + 1u == (uint32_t)n)
+          __hip_atomic_store(done, gen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+    }
     return;
   }
   if (gtid < wide_lanes) {  // wave-uniform

@@ -6,8 +6,10 @@ the GPU (their measurements: DESIGN.md §4 "Measured design alternatives"):
 * OURO_PLAN_STAGE=0 / 1 / 2 / 3 -- a latency plan's window copies (2, the
   default: copy kernel in, results written by the latency kernel straight
   into the pinned block), with and without the eta nonce output;
-* OURO_PLAN_GRAPH=0 -- the plan's launches issued per submit instead of one
-  captured hipGraph.
+* OURO_PLAN_GRAPH=1 -- the plan's launches captured into one hipGraph
+  instead of issued per submit (the default since r04m);
+* OURO_PLAN_FLAG=0 -- the plan's wait on the stream's completion instead of
+  the kernel's done word in the pinned output block.
 
 Every form must give the oracle's verdicts and outputs; a switch that drifts
 from it fails here even while it is off by default.
@@ -82,13 +84,15 @@ def test_split_ed25519_and_kes_match_oracle(gpu_lib, monkeypatch):
     np.testing.assert_array_equal(got, want)
 
 
-@pytest.mark.parametrize("stage,graph", [("0", "1"), ("1", "1"), ("2", "1"), ("3", "1"),
-                                         ("0", "0"), ("2", "0")])
-def test_plan_stage_forms_match_oracle(gpu_lib, kats, monkeypatch, stage, graph):
+@pytest.mark.parametrize("stage,graph,flag", [("0", "1", "1"), ("1", "1", "1"), ("2", "1", "1"),
+                                              ("3", "1", "1"), ("0", "0", "1"), ("2", "0", "1"),
+                                              ("2", "0", "0")])
+def test_plan_stage_forms_match_oracle(gpu_lib, kats, monkeypatch, stage, graph, flag):
     from ouroboros_network_amd.tpraos import HeaderPlan
 
-    monkeypatch.setenv("OURO_PLAN_STAGE", stage)  # read when the plan's graph is captured
-    monkeypatch.setenv("OURO_PLAN_GRAPH", graph)  # 0: the same launches per submit, no graph
+    monkeypatch.setenv("OURO_PLAN_STAGE", stage)  # read when the plan is created
+    monkeypatch.setenv("OURO_PLAN_GRAPH", graph)  # 1: the launches captured into a hipGraph
+    monkeypatch.setenv("OURO_PLAN_FLAG", flag)  # 0: wait on the stream, not the done word
     batch = HC.golden_variants(kats, stride=9)
     wv, wbe, wbl = O.tpraos_verify_batch(batch)
     plan = HeaderPlan(max_headers=64, max_body_bytes=int(batch.body.size))
