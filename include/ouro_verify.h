@@ -310,12 +310,44 @@ int ouro_tpraos_pack_cbor_device(void *stream, const uint8_t *raw, size_t raw_by
  * ouro_tpraos_pack_cbor; verdict[i] = 1 iff header i slices (status
  * OURO_PACK_OK) and its Sum6KES signature verifies over the raw header body
  * under the opcert's hot key at t = kesPeriod(slot) - c0 (0 when the slot's
- * period is below c0; Integrity.hs:38-44).  The host slicer, then the Sum6KES
- * kernel (host buffers, synchronous; a device error recomputes on the host
- * path).  OURO_EINVAL for a span outside raw_bytes, NULLs or a zero period. */
+ * period is below c0; Integrity.hs:38-44).  Host buffers (pageable is fine),
+ * synchronous; runs on the raw-CBOR pipeline described at
+ * ouro_tpraos_verify_cbor (a device error recomputes on the host path).
+ * OURO_EINVAL for a span outside raw_bytes, NULLs or a zero period. */
 int ouro_integrity_verify_cbor(const uint8_t *raw, size_t raw_bytes, const uint64_t *off,
                                const uint32_t *len, size_t n, uint64_t slots_per_kes_period,
                                uint8_t *status, uint8_t *verdict);
+/* Raw TPraos headers in host memory -> the full header check in ONE call:
+ * the crypto of TPraos.updateChainDepState (ouroboros-consensus-shelley/src/
+ * Ouroboros/Consensus/Shelley/Protocol.hs:433-442) over every header of a
+ * batch the caller holds as the raw bytes it received or stored -- ChainSync
+ * windows (ouroboros-consensus/src/Ouroboros/Consensus/MiniProtocol/ChainSync/
+ * Client.hs:792) and ChainDB's re-validation of a stored chain suffix
+ * (.../Storage/ChainDB/Impl/LgrDB.hs:350-368).  Headers as for
+ * ouro_tpraos_pack_cbor (raw may be pageable, any offsets and order).
+ * VRF inputs: eta_alpha / leader_alpha (n x 32 each) when both are given,
+ * otherwise derived on the device from each header's slot as the OVERLAY rule
+ * does (mkSeed seedEta / seedL slot eta0, see ouro_tpraos_batch), with
+ * epoch_nonce = eta0 (32 B; NULL = NeutralNonce; one eta0 per call).  The
+ * headers' claimed certifiedOutputs are compared (OURO_HDR_*_CLAIM_OK).
+ * Outputs: status[i] = OURO_PACK_*; verdict[i] = OURO_HDR_* bits, 0 for a
+ * header that does not slice; beta_eta / beta_leader (n x 64) and eta_nonce
+ * (n x 32, Blake2b-256 of the claimed eta output) may be NULL.
+ * How it runs: the batch is cut into chunks of whole headers; the library's
+ * worker pool gathers each chunk's spans into pinned, NUMA-local staging,
+ * and per chunk one stream uploads the raw bytes, runs the device slicer
+ * and the header kernel and copies the results back, several chunks in
+ * flight so the host copies and PCIe hide behind the kernels
+ * (OURO_CBOR_CHUNK headers per chunk, default 32768; OURO_CBOR_SLOTS chunks
+ * in flight, default 6, at most 8; OURO_CBOR_COPY_THREADS gather threads,
+ * default 8).  Synchronous; a device error recomputes the batch on the host
+ * path.  OURO_EINVAL for a span outside raw_bytes, NULLs, a zero period or
+ * only one of the two alpha arrays. */
+int ouro_tpraos_verify_cbor(const uint8_t *raw, size_t raw_bytes, const uint64_t *off,
+                            const uint32_t *len, size_t n, uint64_t slots_per_kes_period,
+                            const uint8_t *epoch_nonce, const uint8_t *eta_alpha,
+                            const uint8_t *leader_alpha, uint8_t *status, uint8_t *verdict,
+                            uint8_t *beta_eta, uint8_t *beta_leader, uint8_t *eta_nonce);
 /* The same on raw headers already in device memory (device pointers; arena
  * of ouro_tpraos_pack_bytes(n) bytes): the device slicer and the Sum6KES
  * kernel enqueued on `stream`, not synchronised.  A rejected header's row is
@@ -417,15 +449,9 @@ int ouro_device_count(void);
  * ouro_tpraos_verify_batch_multi bind themselves to their device's node; all
  * pinned staging is allocated with hipHostMallocNumaUser (the allocating
  * thread's policy).  ouro_debug_multi_workers: per worker its device, node and
- * the CPUs it is bound to (0 = unbound); returns the worker count. */
+ * the CPUs it is bound to (0 = unbound; declared in ouro_verify_debug.h). */
 int ouro_device_numa_node(int device);
 int ouro_bind_thread_to_device(int device);
-int ouro_debug_multi_workers(int *devices, int *nodes, int *cpus, int max);
-/* (test/diagnostic, no device: bind the calling thread to a PCI bus id's node
- * as read from OURO_SYSFS_ROOT (default /sys); returns the node, *ncpus the
- * CPUs bound.  ouro_debug_thread_cpus: the CPUs the caller may run on.) */
-int ouro_debug_numa_bind_pci(const char *busid, int *ncpus);
-int ouro_debug_thread_cpus(int *cpus, int max);
 int ouro_tpraos_verify_batch_multi(const ouro_tpraos_batch *b, const int *devices, int ndev,
                                    uint8_t *verdict, uint8_t *beta_eta, uint8_t *beta_leader);
 
@@ -488,40 +514,6 @@ int ouro_tpraos_verify_batch_host(const ouro_tpraos_batch *b, uint8_t *verdict,
 int ouro_leader_check_batch_host(size_t n, const uint8_t *beta, const uint64_t *sigma_num,
                                  const uint64_t *sigma_den, int64_t act_log_hi,
                                  uint64_t act_log_lo, int f_is_one, uint8_t *verdict);
-
-/* Diagnostics: items the host path has verified since the process started --
- * single items routed there, and host-buffer batches recomputed there after a
- * device error.  Host-only. */
-int ouro_debug_host_path(unsigned long long *single_items,
-                         unsigned long long *recomputed_batches);
-
-/* TIMING PROBE (bench.py latency phases) of the plan's last waited-for
- * window, when OURO_PLAN_TIMING was set in the environment at its submit (-1
- * otherwise): gpu_ms = events recorded around its launches (input copy, the
- * latency kernel, output); copy_us / launch_us = host time of submit's copy
- * into the pinned block and of the launch calls.  Any pointer may be NULL. */
-int ouro_debug_plan_timing(ouro_tpraos_plan *plan, float *gpu_ms, float *copy_us,
-                           float *launch_us);
-
-/* Diagnostics: per-thread contexts (stream, scratch, staging) are pooled per
- * device; a thread borrows one on its first call and returns it when it
- * exits.  created = contexts made so far on `device`, idle = returned ones
- * waiting in the pool.  Host-only. */
-int ouro_debug_contexts(int device, size_t *created, size_t *idle);
-
-/* TIMING PROBE (tools/lat_stamps.py): header 0's per-item stamps of the last
- * fused latency launch, 16 items x 24 tags of s_memrealtime (100 MHz), for a
- * library built with -DOURO_LAT_STAMPS=1 and run with OURO_LAT_STAMPS set.
- * Returns the number of stamps written to out, or -1 (the product build). */
-int ouro_debug_lat_stamps(unsigned long long *out);
-
-/* CLOCK PROBE (bench.py roofline.frac_clock): the shader clock the header
- * kernel ran at, from per-workgroup s_memtime / s_memrealtime stamps at entry
- * and exit of the last k_tpraos_verify launch (4 values per workgroup, up to
- * max_slots rows), in a library built with -DOURO_CLOCK_STAMPS=1
- * (lib/libouro_verify_clock.so).  Returns the rows written, or -1 (the
- * product build, in which no stamp executes). */
-int ouro_debug_clock_stamps(unsigned long long *out, int max_slots);
 
 /* ---------------------------------------------- leader threshold ----- */
 /* ledger-specs checkLeaderValue (shelley-spec-ledger BlockChain.hs), called by

@@ -11,6 +11,7 @@ from ._native import DeviceError, NativeUnavailable
 from .byron import (ByronDSIGN, pack_byron_cbor, parse_byron_header, verify_byron_cbor,
                     verify_byron_headers)
 from .dsign import Ed25519DSIGN
+from .header import verify_headers_cbor, verify_integrity_cbor
 from .kes import Sum6KES, kes_period
 from .tpraos import HeaderBatch, first_invalid, verify_headers, verify_headers_multi
 from .vrf import PraosVRF
@@ -30,7 +31,9 @@ __all__ = [
     "verify_byron_cbor",
     "verify_byron_headers",
     "verify_headers",
+    "verify_headers_cbor",
     "verify_headers_multi",
+    "verify_integrity_cbor",
 ]
 
 

@@ -84,7 +84,8 @@ class ByronBatch(ctypes.Structure):
                                        "delegate_vk", "magic")]
 
 
-# every symbol include/ouro_verify.h declares, with its ctypes signature
+# every symbol include/ouro_verify.h (the boundary) and include/ouro_verify_debug.h
+# (diagnostics) declare, with its ctypes signature
 _P = ctypes.c_void_p
 _SZ = ctypes.c_size_t
 _I = ctypes.c_int
@@ -121,6 +122,10 @@ SIGNATURES = {
     "ouro_debug_numa_bind_pci": (_I, [ctypes.c_char_p, _P]),
     "ouro_debug_thread_cpus": (_I, [_P, _I]),
     "ouro_integrity_verify_cbor": (_I, [_P, _SZ, _P, _P, _SZ, ctypes.c_uint64, _P, _P]),
+    "ouro_tpraos_verify_cbor": (_I, [_P, _SZ, _P, _P, _SZ, ctypes.c_uint64, _P, _P, _P, _P, _P,
+                                     _P, _P, _P]),
+    "ouro_debug_cbor_stats": (_I, [_P]),
+    "ouro_debug_test_hooks": (_I, []),
     "ouro_integrity_verify_cbor_device": (_I, [_P, _P, _SZ, _P, _P, _SZ, ctypes.c_uint64, _P,
                                                _SZ, _P, _P]),
     "ouro_sum6kes_verify_batch": (_I, [_SZ, _P, _P, _P, _P, _P, _P, _P]),
@@ -216,6 +221,16 @@ def load_shim(path: str = SHIM_PATH) -> ctypes.CDLL:
                 fn.argtypes = args
             _shim = lib
         return _shim
+
+
+# the test-hook build of the same library (tests/test_gpu_hooks.py loads it in a
+# child process through OURO_VERIFY_LIB)
+TEST_LIB_PATH = os.path.join(_HERE, "lib", "libouro_verify_test.so")
+
+
+def test_hooks() -> bool:
+    """True when the loaded library is the test-hook build (OURO_TEST_HOOKS)."""
+    return bool(load().ouro_debug_test_hooks())
 
 
 def check(rc: int, what: str) -> int:

@@ -24,6 +24,7 @@
 #include "host_path.h"
 #include "launch.h"
 #include "leader.h"
+#include "task_pool.h"
 #include "tpraos.h"
 
 using namespace ouro;
@@ -566,6 +567,27 @@ struct Pipe {
   PipeSlot s[2];
 };
 
+// ---- raw header CBOR from host memory (state; the engine is raw_run) ----
+// A slot of the raw-CBOR pipeline: its stream, pinned NUMA-local staging for
+// one chunk's gathered header bytes and for its results, and the chunk's
+// device buffers (raw bytes, the slicer's arena, results).
+constexpr int kRawMaxSlots = 8;
+struct RawSlot {
+  hipStream_t st = nullptr;
+  hipEvent_t done = nullptr;
+  uint8_t* h_in = nullptr;   // rebased offsets | lengths | eta0 | alphas | raw bytes
+  size_t h_in_cap = 0;
+  uint8_t* h_out = nullptr;  // status | verdict | beta_eta | beta_leader | eta_nonce
+  size_t h_out_cap = 0;
+  Buf d_in, d_arena, d_out;
+  size_t lo = 0, m = 0;
+  bool busy = false;
+};
+struct RawPipe {
+  bool ready = false;
+  RawSlot s[kRawMaxSlots];
+};
+
 // Everything a calling thread needs on one device: its stream, the scratch
 // slots of each stream it launches on, staging buffers and the two-slot
 // pipeline.  Contexts are POOLED per device ("a per-thread
@@ -582,6 +604,7 @@ struct ThreadCtx {
   std::map<hipStream_t, Buf> scratch;  // per stream: concurrent launches never share slots
   Buf in[32];  // staging slots; a header batch uses up to 24
   Pipe pipe;
+  RawPipe raw;  // ouro_tpraos_verify_cbor / ouro_integrity_verify_cbor
 };
 struct CtxPool {
   std::mutex mu;
@@ -662,10 +685,20 @@ int plan(DeviceState* ds, int id, size_t n, hipStream_t stream, int* grid, int32
   return OURO_OK;
 }
 
-// TEST HOOK (tests/test_gpu_host_path.py): with OURO_TEST_DEVICE_ERROR set in
-// the environment every launch reports a device error, so the tests reach the
-// host recompute path on a healthy GPU.  No ABI surface.
+// TEST HOOKS, compiled only into the test build (lib/libouro_verify_test.so,
+// -DOURO_TEST_HOOKS=1; tests/test_gpu_hooks.py runs the hook tests in a child
+// process on it): with OURO_TEST_DEVICE_ERROR set in the environment every
+// launch reports a device error, so the tests reach the host recompute path
+// on a healthy GPU; OURO_TEST_PLAN_POISON (plan_poison below).  The product
+// library reads neither variable.
+#ifndef OURO_TEST_HOOKS
+#define OURO_TEST_HOOKS 0
+#endif
+#if OURO_TEST_HOOKS
 bool injected_device_error() { return getenv("OURO_TEST_DEVICE_ERROR") != nullptr; }
+#else
+constexpr bool injected_device_error() { return false; }
+#endif
 
 int launch_check() {
   OURO_HIP(hipGetLastError());
@@ -690,7 +723,8 @@ int or_host(int rc, F&& recompute) {
   g_host_recompute++;
   const std::string why = t_last_error;
   const int r = recompute();
-  t_last_error = "recomputed on the host path after: " + why;
+  t_last_error = r == OURO_OK ? "recomputed on the host path after: " + why
+                              : "host path failed (" + t_last_error + ") after: " + why;
   return r;
 }
 // Single items run on the host path (one GPU round trip is ~220-420 us, the
@@ -1676,6 +1710,338 @@ int ouro_tpraos_pack_cbor_device(void* stream, const uint8_t* raw, size_t raw_by
   return launch_check();
 }
 
+}  // extern "C"
+
+// ---- raw header CBOR in host memory -> verdicts in one call -----------------
+// The reference's bulk callers hold raw header bytes in host memory: ChainDB's
+// re-validation of a chain suffix (ouroboros-consensus/src/Ouroboros/Consensus/
+// Storage/ChainDB/Impl/LgrDB.hs:350-368), ChainSync windows
+// (.../MiniProtocol/ChainSync/Client.hs:792), and storage integrity on every
+// block (.../Storage/VolatileDB/Impl/Parser.hs:66-85,
+// .../Storage/ImmutableDB/Impl/Validation.hs:358-365).  raw_run takes such a
+// batch straight through the device:
+//   * the batch is cut into chunks of whole headers (OURO_CBOR_CHUNK headers,
+//     default 32,768, and at most kRawChunkBytes of raw bytes each);
+//   * chunk c runs on slot c % S (S = OURO_CBOR_SLOTS streams, default 6):
+//     the library's worker pool gathers its header spans from the caller's
+//     pageable buffer into the slot's pinned, NUMA-local staging (runs of
+//     adjacent spans as one memcpy; offsets rebased by a prefix sum), the
+//     slot's stream uploads that block -- the raw bytes, ~1 KB per header,
+//     not the 1.4 KB SoA --, runs the device slicer (k_tpraos_pack) into the
+//     slot's arena, then the header kernel with mkSeed from (slot, eta0) on
+//     the device (or the Sum6KES kernel, for integrity), and copies status,
+//     verdicts and outputs back into pinned memory;
+//   * before reusing a slot the host harvests its previous chunk into the
+//     caller's buffers, so up to S chunks are in flight: the host's gathers,
+//     the uploads and the other slots' kernels overlap, and the kernels of
+//     neighbouring chunks share the CUs as each one's waves retire.
+// A device error stops the pipeline (everything in flight is waited for) and
+// the whole batch is recomputed on the host path (raw_host).
+namespace {
+constexpr size_t a16(size_t x) { return (x + 15) & ~(size_t)15; }
+constexpr size_t kRawChunkBytes = (size_t)96 << 20;
+
+enum RawKind { kRawHdr = 0, kRawKes = 1 };
+struct RawCall {
+  RawKind kind;
+  const uint8_t* raw;
+  size_t raw_bytes;
+  const uint64_t* off;
+  const uint32_t* len;
+  size_t n;
+  uint64_t spkp;
+  const uint8_t* eta0;           // epoch nonce (32 B), or null = NeutralNonce
+  const uint8_t *ea, *la;        // explicit VRF inputs (n x 32 each), or null: mkSeed
+  uint8_t* status;
+  uint8_t* verdict;
+  uint8_t *be, *bl, *nonce;      // optional outputs (header kind)
+};
+struct RawChunk {
+  size_t lo, m, bytes;
+};
+
+// the pinned / device input block of a chunk of m headers and `bytes` raw bytes
+struct RawIn {
+  size_t off, len, eta0, alpha, raw, total;
+};
+RawIn raw_in(size_t m, size_t bytes, bool alphas) {
+  RawIn l;
+  l.off = 0;
+  l.len = a16(8 * m);
+  l.eta0 = l.len + a16(4 * m);
+  l.alpha = l.eta0 + 32;
+  l.raw = a16(l.alpha + (alphas ? 64 * m : 0));
+  l.total = l.raw + a16(std::max<size_t>(bytes, 16));
+  return l;
+}
+// its result block: status | verdict | beta_eta | beta_leader | eta_nonce | slot
+struct RawOut {
+  size_t status, verdict, be, bl, nonce, slot, total;
+};
+RawOut raw_out(size_t m) {
+  RawOut o;
+  o.status = 0;
+  o.verdict = a16(m);
+  o.be = o.verdict + a16(m);
+  o.bl = o.be + 64 * m;
+  o.nonce = o.bl + 64 * m;
+  o.slot = o.nonce + 32 * m;  // device only: the slicer's slots for mkSeed
+  o.total = o.slot + 8 * m;
+  return o;
+}
+// bytes of the result block copied back
+size_t raw_out_bytes(const RawCall& c, const RawOut& o, size_t m) {
+  if (c.kind == kRawKes) return o.verdict + m;
+  if (c.nonce) return o.slot;
+  if (c.bl) return o.nonce;
+  if (c.be) return o.bl;
+  return o.verdict + m;
+}
+
+// Every span inside raw (as ouro_tpraos_pack_cbor demands), and the chunks.
+int raw_chunks(const RawCall& c, size_t per, std::vector<RawChunk>* out) {
+  out->clear();
+  RawChunk k{0, 0, 0};
+  for (size_t i = 0; i < c.n; i++) {
+    if (c.off[i] > c.raw_bytes || c.raw_bytes - c.off[i] < c.len[i])
+      return fail(OURO_EINVAL, "header " + std::to_string(i) + ": span outside raw_bytes");
+    if (k.m && (k.m == per || k.bytes + c.len[i] > kRawChunkBytes)) {
+      out->push_back(k);
+      k = RawChunk{i, 0, 0};
+    }
+    k.m++;
+    k.bytes += c.len[i];
+  }
+  if (k.m) out->push_back(k);
+  return OURO_OK;
+}
+
+size_t env_size(const char* name, size_t dflt, size_t lo, size_t hi) {
+  if (const char* e = getenv(name)) {
+    const size_t v = (size_t)strtoull(e, nullptr, 10);
+    if (v >= lo && v <= hi) return v;
+  }
+  return dflt;
+}
+
+// last call's phases on this thread (ouro_debug_cbor_stats)
+thread_local double t_raw_stats[6] = {-1, -1, -1, -1, -1, -1};
+
+int pinned_at_least(uint8_t** p, size_t* cap, size_t bytes) {
+  if (*cap >= bytes) return OURO_OK;
+  if (*p) OURO_HIP(hipHostFree(*p));
+  *p = nullptr;
+  *cap = 0;
+  // (hipHostMallocNumaUser: the calling thread's NUMA policy -- a bench rank
+  // or multi-device worker is bound to its GPU's node, numa.cpp)
+  OURO_HIP(hipHostMalloc(reinterpret_cast<void**>(p), bytes, hipHostMallocNumaUser));
+  *cap = bytes;
+  return OURO_OK;
+}
+
+// the chunk's header spans from the caller's buffer into the slot's pinned block
+int raw_stage(RawSlot& s, const RawCall& c, const RawChunk& k, int width) {
+  const bool alphas = c.ea != nullptr;
+  const RawIn L = raw_in(k.m, k.bytes, alphas);
+  int rc = pinned_at_least(&s.h_in, &s.h_in_cap, L.total + L.total / 8);
+  if (rc) return rc;
+  uint64_t* noff = reinterpret_cast<uint64_t*>(s.h_in + L.off);
+  uint64_t at = 0;
+  for (size_t i = 0; i < k.m; i++) {
+    noff[i] = at;
+    at += c.len[k.lo + i];
+  }
+  memcpy(s.h_in + L.len, c.len + k.lo, 4 * k.m);
+  if (c.eta0) memcpy(s.h_in + L.eta0, c.eta0, 32);
+  if (alphas) {
+    memcpy(s.h_in + L.alpha, c.ea + 32 * k.lo, 32 * k.m);
+    memcpy(s.h_in + L.alpha + 32 * k.m, c.la + 32 * k.lo, 32 * k.m);
+  }
+  uint8_t* dst = s.h_in + L.raw;
+  // tasks of ~1 MB: enough to balance, few enough to keep each memcpy long
+  const size_t ntasks = std::max<size_t>(1, std::min<size_t>(k.m, k.bytes >> 20));
+  const int r = ouro_pool::parallel_for(ntasks, width, [&](size_t t) {
+    const size_t a = k.m * t / ntasks, b = k.m * (t + 1) / ntasks;
+    for (size_t i = a; i < b;) {
+      // a run of headers adjacent in the caller's buffer: one memcpy
+      const uint64_t src = c.off[k.lo + i];
+      uint64_t bytes = c.len[k.lo + i];
+      size_t j = i + 1;
+      while (j < b && c.off[k.lo + j] == src + bytes) bytes += c.len[k.lo + j++];
+      memcpy(dst + noff[i], c.raw + src, bytes);
+      i = j;
+    }
+  });
+  return r ? fail(OURO_EDEVICE, "raw CBOR gather failed") : OURO_OK;
+}
+
+// the slot's stream: upload, device slicer, kernel, results back
+int raw_launch(RawSlot& s, const RawCall& c, const RawChunk& k) {
+  const bool alphas = c.ea != nullptr;
+  const RawIn L = raw_in(k.m, k.bytes, alphas);
+  const RawOut O = raw_out(k.m);
+  const size_t back = raw_out_bytes(c, O, k.m);
+  int rc;
+  if ((rc = ensure(s.d_in, L.total)) || (rc = ensure(s.d_arena, ouro_tpraos_pack_bytes(k.m))) ||
+      (rc = ensure(s.d_out, O.total)) || (rc = pinned_at_least(&s.h_out, &s.h_out_cap, back)))
+    return rc;
+  uint8_t* din = static_cast<uint8_t*>(s.d_in.p);
+  uint8_t* dout = static_cast<uint8_t*>(s.d_out.p);
+  OURO_HIP(hipMemcpyAsync(din, s.h_in, L.total, hipMemcpyHostToDevice, s.st));
+  uint64_t* dslot = reinterpret_cast<uint64_t*>(dout + O.slot);
+  const bool seeds = c.kind == kRawHdr && !alphas;
+  const cbor::Out o = cbor::arena_out(cbor::arena_base(s.d_arena.p), k.m, seeds ? dslot : nullptr,
+                                      nullptr);
+  const uint8_t* draw = din + L.raw;
+  const size_t blocks = std::min<size_t>((k.m + kBlock - 1) / kBlock, 4096);
+  hipLaunchKernelGGL(k_tpraos_pack, dim3((unsigned)blocks), dim3(kBlock), 0, s.st, draw, k.bytes,
+                     reinterpret_cast<const uint64_t*>(din + L.off),
+                     reinterpret_cast<const uint32_t*>(din + L.len), k.m, c.spkp, o,
+                     dout + O.status);
+  if ((rc = launch_check())) return rc;
+  ouro_tpraos_batch b{};
+  cbor::batch_from(&b, o, draw, k.m);
+  if (c.kind == kRawKes) {
+    rc = launch_kes(s.st, k.m, b.hot_vk, b.kes_t, b.body, b.body_off, b.body_len, b.kes_sig,
+                    dout + O.verdict);
+  } else {
+    if (alphas) {
+      b.eta_alpha = din + L.alpha;
+      b.leader_alpha = din + L.alpha + 32 * k.m;
+    } else {
+      b.slot = dslot;
+      b.epoch_nonce = c.eta0 ? din + L.eta0 : nullptr;
+    }
+    if (c.nonce) b.eta_nonce = dout + O.nonce;
+    rc = launch_hdr(s.st, b, dout + O.verdict, dout + O.be, dout + O.bl);
+  }
+  if (rc) return rc;
+  OURO_HIP(hipMemcpyAsync(s.h_out, dout, back, hipMemcpyDeviceToHost, s.st));
+  OURO_HIP(hipEventRecord(s.done, s.st));
+  s.lo = k.lo;
+  s.m = k.m;
+  s.busy = true;
+  return OURO_OK;
+}
+
+// the slot's finished chunk into the caller's buffers
+int raw_drain(RawSlot& s, const RawCall& c) {
+  if (!s.busy) return OURO_OK;
+  s.busy = false;
+  OURO_HIP(hipEventSynchronize(s.done));
+  const RawOut O = raw_out(s.m);
+  const uint8_t* st = s.h_out + O.status;
+  const uint8_t* v = s.h_out + O.verdict;
+  memcpy(c.status + s.lo, st, s.m);
+  // a header the slicer rejected is invalid (its zeroed row cannot verify;
+  // masked so that no bit at all is set for it)
+  for (size_t i = 0; i < s.m; i++) c.verdict[s.lo + i] = st[i] == OURO_PACK_OK ? v[i] : 0;
+  if (c.kind == kRawHdr) {
+    if (c.be) memcpy(c.be + 64 * s.lo, s.h_out + O.be, 64 * s.m);
+    if (c.bl) memcpy(c.bl + 64 * s.lo, s.h_out + O.bl, 64 * s.m);
+    if (c.nonce) memcpy(c.nonce + 32 * s.lo, s.h_out + O.nonce, 32 * s.m);
+  }
+  return OURO_OK;
+}
+
+int raw_run(const RawCall& c, const std::vector<RawChunk>& chunks) {
+  using clk = std::chrono::steady_clock;
+  const auto t0 = clk::now();
+  double gather_ms = 0, wait_ms = 0;
+  DeviceState* ds;
+  int dev, rc = device_state(&ds);
+  if (rc || (rc = current_device(&dev))) return rc;
+  RawPipe& p = ctx_of(dev).raw;
+  const int S = (int)env_size("OURO_CBOR_SLOTS", 6, 1, kRawMaxSlots);
+  for (int k = 0; k < S; k++) {
+    RawSlot& s = p.s[k];
+    if (!s.st) OURO_HIP(hipStreamCreateWithFlags(&s.st, hipStreamNonBlocking));
+    if (!s.done) OURO_HIP(hipEventCreateWithFlags(&s.done, hipEventDisableTiming));
+  }
+  const int width = (int)env_size("OURO_CBOR_COPY_THREADS", 8, 1, 64);
+  size_t ci = 0;
+  for (; ci < chunks.size() && !rc; ci++) {
+    RawSlot& s = p.s[ci % S];
+    const auto a = clk::now();
+    rc = raw_drain(s, c);
+    const auto b = clk::now();
+    if (!rc) rc = raw_stage(s, c, chunks[ci], width);
+    const auto d = clk::now();
+    if (!rc) rc = raw_launch(s, c, chunks[ci]);
+    wait_ms += std::chrono::duration<double, std::milli>(b - a).count();
+    gather_ms += std::chrono::duration<double, std::milli>(d - b).count();
+  }
+  // the rest in chunk order; after an error, wait for everything in flight
+  for (int k = 0; k < S; k++) {
+    RawSlot& s = p.s[(ci + k) % S];
+    if (rc) {
+      (void)hipStreamSynchronize(s.st);
+      s.busy = false;
+    } else {
+      const auto a = clk::now();
+      rc = raw_drain(s, c);
+      wait_ms += std::chrono::duration<double, std::milli>(clk::now() - a).count();
+    }
+  }
+  const double total = std::chrono::duration<double, std::milli>(clk::now() - t0).count();
+  const double st[6] = {total, gather_ms, wait_ms, (double)chunks.size(), (double)S, (double)width};
+  memcpy(t_raw_stats, st, sizeof st);
+  return rc;
+}
+
+// the host path over the same batch: host slicer + host verification, in
+// chunks (no batch-sized arena), results straight into the caller's buffers
+int raw_host(const RawCall& c) {
+  const size_t C = 1 << 16;
+  const size_t cap = std::min(C, c.n);
+  const size_t nb = ouro_tpraos_pack_bytes(cap);
+  std::unique_ptr<uint8_t[]> arena(new (std::nothrow) uint8_t[nb]);
+  std::unique_ptr<uint64_t[]> slots(new (std::nothrow) uint64_t[cap]);
+  if (!arena || !slots) return fail(OURO_EDEVICE, "raw CBOR host path: out of host memory");
+  for (size_t lo = 0; lo < c.n; lo += C) {
+    const size_t m = std::min(C, c.n - lo);
+    ouro_tpraos_batch b{};  // (the slicer sets the required members only)
+    int rc = ouro_tpraos_pack_cbor(c.raw, c.raw_bytes, c.off + lo, c.len + lo, m, c.spkp,
+                                   arena.get(), nb, &b, slots.get(), nullptr, c.status + lo, 0);
+    if (rc) return fail(rc, "ouro_tpraos_pack_cbor: bad arguments");
+    if (c.kind == kRawKes) {
+      rc = ouro_host::kes_batch(m, b.hot_vk, b.kes_t, b.body, b.body_off, b.body_len, b.kes_sig,
+                                c.verdict + lo);
+    } else {
+      if (c.ea) {
+        b.eta_alpha = c.ea + 32 * lo;
+        b.leader_alpha = c.la + 32 * lo;
+      } else {
+        b.slot = slots.get();
+        b.epoch_nonce = c.eta0;
+      }
+      if (c.nonce) b.eta_nonce = c.nonce + 32 * lo;
+      rc = ouro_host::hdr_batch(&b, c.verdict + lo, c.be ? c.be + 64 * lo : nullptr,
+                                c.bl ? c.bl + 64 * lo : nullptr);
+    }
+    if (rc) return fail(rc, "raw CBOR host path failed");
+    for (size_t i = lo; i < lo + m; i++)
+      if (c.status[i] != OURO_PACK_OK) c.verdict[i] = 0;
+  }
+  return OURO_OK;
+}
+
+int raw_verify(const RawCall& c) {
+  if (c.n == 0) return OURO_OK;
+  if (!c.raw || !c.off || !c.len || !c.status || !c.verdict || c.spkp == 0)
+    return fail(OURO_EINVAL, "null argument / zero period");
+  if ((c.ea == nullptr) != (c.la == nullptr))
+    return fail(OURO_EINVAL, "give both VRF input arrays or neither");
+  std::vector<RawChunk> chunks;
+  const size_t per = env_size("OURO_CBOR_CHUNK", 32768, 256, (size_t)1 << 24);
+  int rc = raw_chunks(c, per, &chunks);
+  if (rc) return rc;
+  return or_host(raw_run(c, chunks), [&] { return raw_host(c); });
+}
+}  // namespace
+
+extern "C" {
+
 // ---- storage integrity (KES only) over raw headers ----
 // verifyHeaderIntegrity (ouroboros-consensus-shelley/src/Ouroboros/Consensus/
 // Shelley/Ledger/Integrity.hs:20-44): Sum6KES of the raw header body under the
@@ -1683,27 +2049,37 @@ int ouro_tpraos_pack_cbor_device(void* stream, const uint8_t* raw, size_t raw_by
 // VolatileDB parser runs on every block at open
 // (ouroboros-consensus/src/Ouroboros/Consensus/Storage/VolatileDB/Impl/Parser.hs:66-85)
 // and ImmutableDB chunk validation on every block of a chunk
-// (.../ImmutableDB/Impl/Validation.hs:358-365).  One call: the slicer (cbor.h,
-// kes_t_of = Integrity.hs:38-44), then the Sum6KES kernel on its rows; a header
-// the slicer rejects is 0 (its zeroed row cannot verify, and is masked too).
+// (.../ImmutableDB/Impl/Validation.hs:358-365).  The raw-CBOR pipeline above:
+// the device slicer (cbor.h, kes_t_of = Integrity.hs:38-44), then the Sum6KES
+// kernel on its rows; a header the slicer rejects is 0.
 int ouro_integrity_verify_cbor(const uint8_t* raw, size_t raw_bytes, const uint64_t* off,
                                const uint32_t* len, size_t n, uint64_t slots_per_kes_period,
                                uint8_t* status, uint8_t* verdict) {
-  if (n == 0) return OURO_OK;
-  if (!status || !verdict || !len || slots_per_kes_period == 0)
-    return fail(OURO_EINVAL, "null argument / zero period");
-  const size_t nb = ouro_tpraos_pack_bytes(n);
-  std::unique_ptr<uint8_t[]> arena(new (std::nothrow) uint8_t[nb]);
-  if (!arena) return fail(OURO_EDEVICE, "ouro_integrity_verify_cbor: out of host memory");
-  ouro_tpraos_batch b;
-  int rc = ouro_tpraos_pack_cbor(raw, raw_bytes, off, len, n, slots_per_kes_period, arena.get(),
-                                 nb, &b, nullptr, nullptr, status, 0);
-  if (rc) return fail(rc, "ouro_tpraos_pack_cbor: bad arguments");
-  // (host-buffer Sum6KES batch: a device error recomputes on the host path)
-  if ((rc = ouro_sum6kes_verify_batch(n, b.hot_vk, b.kes_t, b.body, b.body_off, b.body_len,
-                                      b.kes_sig, verdict)))
-    return rc;
-  for (size_t i = 0; i < n; i++) verdict[i] = status[i] == OURO_PACK_OK && verdict[i];
+  RawCall c{kRawKes, raw, raw_bytes, off, len, n, slots_per_kes_period, nullptr, nullptr,
+            nullptr, status, verdict, nullptr, nullptr, nullptr};
+  return raw_verify(c);
+}
+
+// Raw TPraos headers -> the full header check (ouroboros-consensus-shelley/
+// src/Ouroboros/Consensus/Shelley/Protocol.hs:433-442 over each decoded
+// header) in one call through the raw-CBOR pipeline above.
+int ouro_tpraos_verify_cbor(const uint8_t* raw, size_t raw_bytes, const uint64_t* off,
+                            const uint32_t* len, size_t n, uint64_t slots_per_kes_period,
+                            const uint8_t* epoch_nonce, const uint8_t* eta_alpha,
+                            const uint8_t* leader_alpha, uint8_t* status, uint8_t* verdict,
+                            uint8_t* beta_eta, uint8_t* beta_leader, uint8_t* eta_nonce) {
+  RawCall c{kRawHdr, raw, raw_bytes, off, len, n, slots_per_kes_period, epoch_nonce, eta_alpha,
+            leader_alpha, status, verdict, beta_eta, beta_leader, eta_nonce};
+  return raw_verify(c);
+}
+
+// DIAGNOSTIC: 1 in the test-hook build (lib/libouro_verify_test.so), 0 in the product
+int ouro_debug_test_hooks(void) { return OURO_TEST_HOOKS; }
+
+// DIAGNOSTIC: the calling thread's last raw-CBOR call (ms and counts)
+int ouro_debug_cbor_stats(double* out6) {
+  if (!out6) return fail(OURO_EINVAL, "null buffer");
+  memcpy(out6, t_raw_stats, sizeof t_raw_stats);
   return OURO_OK;
 }
 
@@ -1717,7 +2093,7 @@ int ouro_integrity_verify_cbor_device(void* stream, const uint8_t* raw, size_t r
                                       size_t arena_bytes, uint8_t* status, uint8_t* verdict) {
   if (n == 0) return OURO_OK;
   if (!verdict) return fail(OURO_EINVAL, "null verdict");
-  ouro_tpraos_batch b;
+  ouro_tpraos_batch b{};
   int rc = ouro_tpraos_pack_cbor_device(stream, raw, raw_bytes, off, len, n,
                                         slots_per_kes_period, arena, arena_bytes, &b, nullptr,
                                         nullptr, status);
@@ -1980,12 +2356,13 @@ ouro_tpraos_batch plan_host_batch(const ouro_tpraos_plan* p) {
   return b;
 }
 
-// TEST HOOK (tests/test_gpu_claims.py::test_plan_counters_from_cut_off_launch),
-// reached only through the environment (OURO_TEST_PLAN_POISON, read by
-// ouro_tpraos_plan_submit; no ABI surface): leaves every arrival counter of the
+// TEST HOOK (tests/test_gpu_claims.py::test_plan_counters_from_cut_off_launch;
+// the test build only, OURO_TEST_HOOKS): OURO_TEST_PLAN_POISON set at
+// ouro_tpraos_plan_submit leaves every arrival counter of the
 // plan's records as a launch of its last generation would have left them had
 // it been cut off one arrival short of each finish, so the test can show the
 // next launch ignores them.
+#if OURO_TEST_HOOKS
 int plan_poison(ouro_tpraos_plan* p) {
   OURO_HIP(hipSetDevice(p->dev));
   OURO_HIP(hipStreamSynchronize(p->st));  // the last launch retired (done word: maybe not yet)
@@ -2007,6 +2384,7 @@ int plan_poison(ouro_tpraos_plan* p) {
   OURO_HIP(hipMemcpy(p->res, h.data(), sizeof(int32_t) * words, hipMemcpyHostToDevice));
   return OURO_OK;
 }
+#endif
 }  // namespace
 
 extern "C" {
@@ -2060,7 +2438,9 @@ int ouro_tpraos_plan_submit(ouro_tpraos_plan* p, const ouro_tpraos_batch* b) {
   }
   if (p->timed)
     p->copy_us = std::chrono::duration<float, std::micro>(std::chrono::steady_clock::now() - tc0).count();
+#if OURO_TEST_HOOKS
   if (p->gen && getenv("OURO_TEST_PLAN_POISON") && (rc = plan_poison(p))) return rc;
+#endif
   // every launch a new generation, so no counter an earlier launch left
   // behind (one that never completed) is ever counted again
   p->gen = p->gen % 0x0fffffffu + 1u;

@@ -22,37 +22,35 @@
 // single-byte corruption and truncation of them.
 #include <algorithm>
 #include <cstring>
-#include <thread>
 #include <vector>
 
 #include "../../include/ouro_verify.h"
 #include "cbor.h"
 #include "cbor_byron.h"
+#include "task_pool.h"
 
 namespace {
 
 using namespace ouro::cbor;
 
-// work(lo, hi) over [0, n) on up to `nthreads` threads (<= 0: one per
-// hardware thread), at least 4096 headers each: below that a thread costs
-// more than it saves
+// work(lo, hi) over [0, n) on up to `nthreads` threads (<= 0: one per CPU
+// this process may run on) of the library's worker pool (task_pool.h), at
+// least 4096 headers each: below that a thread costs more than it saves.
+// The parse neither allocates nor throws, so the pool cannot fail it.
 template <class F>
 void parallel_rows(size_t n, int nthreads, F work) {
-  size_t threads = nthreads > 0 ? (size_t)nthreads
-                                : std::max<unsigned>(1, std::thread::hardware_concurrency());
+  size_t threads = nthreads > 0 ? (size_t)nthreads : (size_t)ouro_pool::usable_cpus();
   threads = std::max<size_t>(1, std::min(threads, (n + 4095) / 4096));
   threads = std::min<size_t>(threads, 64);
   if (threads <= 1) {
     work(0, n);
     return;
   }
-  std::vector<std::thread> pool;
   const size_t per = (n + threads - 1) / threads;
-  for (size_t t = 0; t < threads; t++) {
+  ouro_pool::parallel_for(threads, (int)threads, [&](size_t t) {
     const size_t lo = t * per, hi = std::min(n, lo + per);
-    if (lo < hi) pool.emplace_back(work, lo, hi);
-  }
-  for (auto& th : pool) th.join();
+    if (lo < hi) work(lo, hi);
+  });
 }
 
 size_t byron_msg_bytes(size_t n, const uint32_t* len) {

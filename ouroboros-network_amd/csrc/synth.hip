@@ -289,7 +289,7 @@ __global__ void __launch_bounds__(kBlock) k_synth_seeded(
     size_t n, uint64_t first, int npools, const uint32_t* pool, uint64_t slot0,
     const uint8_t* eta0, uint64_t* slot, uint8_t* eta_alpha, uint8_t* leader_alpha,
     uint8_t* eta_proof, uint8_t* leader_proof, uint8_t* eta_out, uint8_t* lead_out,
-    int32_t* scratch, const int32_t* btab) {
+    int32_t* scratch, const int32_t* btab, const uint64_t* slot_in) {
   const size_t tid = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   const size_t nth = (size_t)gridDim.x * blockDim.x;
   const Slot lane = slot_of(scratch, tid, kLaneWords);
@@ -307,7 +307,7 @@ __global__ void __launch_bounds__(kBlock) k_synth_seeded(
       vrf.prefix[w] = rec[16 + w];
       vrf.pk[w] = rec[24 + w];
     }
-    const uint64_t s = slot0 + i;
+    const uint64_t s = slot_in ? slot_in[i] : slot0 + i;
     slot[i] = s;
     uint32_t h[8], ae[8], al[8], pe[20], pl[20];
     mkseed_hash(h, s, eta0 ? e0 : nullptr);
@@ -539,7 +539,21 @@ int ouro_synth_seeded(size_t n, uint64_t first, int npools, const uint32_t* pool
   if (prepare(n)) return -2;
   hipLaunchKernelGGL(k_synth_seeded, dim3(grid_for(n)), dim3(kBlock), 0, 0, n, first, npools,
                      pool, slot0, eta0, slot, eta_alpha, leader_alpha, eta_proof, leader_proof,
-                     eta_out, lead_out, g_ctx.scratch, g_ctx.btab);
+                     eta_out, lead_out, g_ctx.scratch, g_ctx.btab, (const uint64_t*)nullptr);
+  return done();
+}
+
+// the same at given slots (slot_in, device, n entries): the raw-CBOR bench's
+// node configuration, whose raw headers carry k_synth_raw's slots
+int ouro_synth_seeded_at(size_t n, uint64_t first, int npools, const uint32_t* pool,
+                         const uint64_t* slot_in, const uint8_t* eta0, uint64_t* slot,
+                         uint8_t* eta_alpha, uint8_t* leader_alpha, uint8_t* eta_proof,
+                         uint8_t* leader_proof, uint8_t* eta_out, uint8_t* lead_out) {
+  if (npools <= 0 || !slot_in) return -3;
+  if (prepare(n)) return -2;
+  hipLaunchKernelGGL(k_synth_seeded, dim3(grid_for(n)), dim3(kBlock), 0, 0, n, first, npools,
+                     pool, (uint64_t)0, eta0, slot, eta_alpha, leader_alpha, eta_proof,
+                     leader_proof, eta_out, lead_out, g_ctx.scratch, g_ctx.btab, slot_in);
   return done();
 }
 

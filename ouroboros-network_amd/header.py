@@ -292,6 +292,23 @@ def _pack_lib():
     return _PACK_LIB
 
 
+def raw_triplet(raw_headers):
+    """(buf, off, len) as contiguous uint8 / uint64 / uint32 arrays from either
+    a sequence of bytes (one header each, concatenated) or a (buf, off, len)
+    triple with the headers at buf[off[i]:off[i]+len[i]]."""
+    if isinstance(raw_headers, tuple) and len(raw_headers) == 3:
+        buf, off, ln = raw_headers
+        buf = np.frombuffer(buf, np.uint8) if isinstance(buf, (bytes, bytearray)) else \
+            np.ascontiguousarray(buf, np.uint8).reshape(-1)
+        return buf, np.ascontiguousarray(off, np.uint64), np.ascontiguousarray(ln, np.uint32)
+    items = [bytes(r) for r in raw_headers]
+    ln = np.array([len(r) for r in items], np.uint32)
+    off = np.zeros(len(items), np.uint64)
+    if len(items) > 1:
+        off[1:] = np.cumsum(ln[:-1], dtype=np.uint64)
+    return np.frombuffer(b"".join(items) or b"\0", np.uint8), off, ln
+
+
 def pack_cbor(raw_headers, *, slots_per_kes_period: int = 129600,
               eta_alpha: Optional[np.ndarray] = None, leader_alpha: Optional[np.ndarray] = None,
               seeds: bool = False, epoch_nonce: Optional[bytes] = None, claimed: bool = True,
@@ -308,19 +325,7 @@ def pack_cbor(raw_headers, *, slots_per_kes_period: int = 129600,
 
     from . import _native
     lib = _pack_lib() or _native.load()
-    if isinstance(raw_headers, tuple) and len(raw_headers) == 3:
-        buf, off, ln = raw_headers
-        buf = np.frombuffer(buf, np.uint8) if isinstance(buf, (bytes, bytearray)) else \
-            np.ascontiguousarray(buf, np.uint8).reshape(-1)
-        off = np.ascontiguousarray(off, np.uint64)
-        ln = np.ascontiguousarray(ln, np.uint32)
-    else:
-        items = [bytes(r) for r in raw_headers]
-        ln = np.array([len(r) for r in items], np.uint32)
-        off = np.zeros(len(items), np.uint64)
-        if len(items) > 1:
-            off[1:] = np.cumsum(ln[:-1], dtype=np.uint64)
-        buf = np.frombuffer(b"".join(items) or b"\0", np.uint8)
+    buf, off, ln = raw_triplet(raw_headers)
     n = int(off.size)
     if ln.size != n:
         raise ValueError("off / len: one entry per header")
@@ -391,25 +396,14 @@ def verify_integrity_cbor(raw_headers, slots_per_kes_period: int, host: bool = F
     """verifyHeaderIntegrity over raw headers (KES only; the storage layer's
     check, ouroboros-consensus-shelley/src/Ouroboros/Consensus/Shelley/Ledger/
     Integrity.hs:20-44): returns (valid bool array, slicer status array).
-    Default: ouro_integrity_verify_cbor (host slicer + the Sum6KES kernel).
+    Default: ouro_integrity_verify_cbor (the raw-CBOR pipeline: header bytes
+    gathered into pinned staging, the device slicer, the Sum6KES kernel).
     host=True: the same slicer, then the library's host path
     (ouro_sum6kes_verify_batch_host) -- no device touched."""
     import ctypes
 
     from . import _native
-    if isinstance(raw_headers, tuple) and len(raw_headers) == 3:
-        buf, off, ln = raw_headers
-        buf = np.frombuffer(buf, np.uint8) if isinstance(buf, (bytes, bytearray)) else \
-            np.ascontiguousarray(buf, np.uint8).reshape(-1)
-        off = np.ascontiguousarray(off, np.uint64)
-        ln = np.ascontiguousarray(ln, np.uint32)
-    else:
-        items = [bytes(r) for r in raw_headers]
-        ln = np.array([len(r) for r in items], np.uint32)
-        off = np.zeros(len(items), np.uint64)
-        if len(items) > 1:
-            off[1:] = np.cumsum(ln[:-1], dtype=np.uint64)
-        buf = np.frombuffer(b"".join(items) or b"\0", np.uint8)
+    buf, off, ln = raw_triplet(raw_headers)
     n = int(off.size)
     status = np.zeros(max(n, 1), np.uint8)
     verdict = np.zeros(max(n, 1), np.uint8)
@@ -431,3 +425,48 @@ def verify_integrity_cbor(raw_headers, slots_per_kes_period: int, host: bool = F
     _native.check(rc, "ouro_sum6kes_verify_batch_host")
     ok = (verdict[:n] != 0) & (p.status == PACK_OK)
     return ok, p.status.copy()
+
+
+def verify_headers_cbor(raw_headers, slots_per_kes_period: int, *,
+                        epoch_nonce: Optional[bytes] = None,
+                        eta_alpha: Optional[np.ndarray] = None,
+                        leader_alpha: Optional[np.ndarray] = None, nonce: bool = False):
+    """The full TPraos header check straight from raw header CBOR in host
+    memory, one call (include/ouro_verify.h ouro_tpraos_verify_cbor): the
+    crypto of TPraos.updateChainDepState (ouroboros-consensus-shelley/src/
+    Ouroboros/Consensus/Shelley/Protocol.hs:433-442) over every header.
+    VRF inputs: eta_alpha / leader_alpha (n x 32 each) when given, else mkSeed
+    from each header's slot and epoch_nonce (None = NeutralNonce) on the
+    device.  Returns (verdict, beta_eta, beta_leader, status[, eta_nonce]):
+    verdict = OURO_HDR_* bits (0 where the header does not slice)."""
+    import ctypes
+
+    from . import _native
+    buf, off, ln = raw_triplet(raw_headers)
+    n = int(off.size)
+    if ln.size != n:
+        raise ValueError("off / len: one entry per header")
+    if epoch_nonce is not None and len(epoch_nonce) != 32:
+        raise ValueError("epoch_nonce: 32 bytes")
+    if (eta_alpha is None) != (leader_alpha is None):
+        raise ValueError("give both alpha arrays or neither")
+    m = max(n, 1)
+    status = np.zeros(m, np.uint8)
+    verdict = np.zeros(m, np.uint8)
+    be = np.zeros((m, 64), np.uint8)
+    bl = np.zeros((m, 64), np.uint8)
+    en = np.zeros((m, 32), np.uint8) if nonce else None
+    ptr = lambda a: None if a is None else a.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
+    ea = la = None
+    if eta_alpha is not None:
+        ea = np.ascontiguousarray(eta_alpha, np.uint8).reshape(n, 32)
+        la = np.ascontiguousarray(leader_alpha, np.uint8).reshape(n, 32)
+    eta0 = None if epoch_nonce is None else np.frombuffer(bytes(epoch_nonce), np.uint8)
+    if n:
+        lib = _native.load()
+        rc = lib.ouro_tpraos_verify_cbor(ptr(buf), buf.size, ptr(off), ptr(ln), n,
+                                         slots_per_kes_period, ptr(eta0), ptr(ea), ptr(la),
+                                         ptr(status), ptr(verdict), ptr(be), ptr(bl), ptr(en))
+        _native.check(rc, "ouro_tpraos_verify_cbor")
+    out = (verdict[:n], be[:n], bl[:n], status[:n])
+    return out + (en[:n],) if nonce else out

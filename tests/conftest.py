@@ -13,7 +13,23 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (gfx950) and the built HIP library")
     config.addinivalue_line("markers", "slow: larger CPU-side cases")
     config.addinivalue_line("markers", "device_error: forces device errors (the host recompute "
-                            "path is expected to run)")
+                            "path is expected to run); needs the test-hook build")
+    config.addinivalue_line("markers", "hooks: needs the test-hook build of the library "
+                            "(lib/libouro_verify_test.so; tests/test_gpu_hooks.py runs these)")
+
+
+@pytest.fixture(autouse=True)
+def _hook_tests_need_the_test_build(request):
+    """The product library compiles no test hooks (OURO_TEST_HOOKS): tests that
+    inject device errors or poison plan records run only where the test build
+    is loaded -- in the child process tests/test_gpu_hooks.py starts."""
+    if request.node.get_closest_marker("device_error") is None and \
+            request.node.get_closest_marker("hooks") is None:
+        return
+    from ouroboros_network_amd import _native
+
+    if not _native.test_hooks():
+        pytest.skip("needs the test-hook build (run by tests/test_gpu_hooks.py)")
 
 
 def _recomputed(lib):

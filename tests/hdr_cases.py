@@ -157,3 +157,70 @@ def kes_body_lengths(kats, lengths=KES_BODY_LENGTHS, seed=b"\x07" * 32):
     ea = [bytes.fromhex(kats["headers"][0]["eta_alpha"])] * len(rows)
     la = [bytes.fromhex(kats["headers"][0]["leader_alpha"])] * len(rows)
     return H.pack(rows, ea, la, slots_per_kes_period=100)
+
+
+# ---- raw wire headers (for the raw-CBOR entries) ------------------------------
+def _cbor_head(mt: int, v: int) -> bytes:
+    if v < 24:
+        return bytes([mt << 5 | v])
+    for ai, w in ((24, 1), (25, 2), (26, 4), (27, 8)):
+        if v < 1 << (8 * w):
+            return bytes([mt << 5 | ai]) + v.to_bytes(w, "big")
+    raise ValueError(v)
+
+
+def cbor_uint(v: int) -> bytes:
+    return _cbor_head(0, v)
+
+
+def cbor_bytes(b: bytes) -> bytes:
+    return _cbor_head(2, len(b)) + b
+
+
+def wire_header(fields, kes_sig: bytes, era=None) -> bytes:
+    """[header_body, kes_sig] CBOR-in-CBOR wrapped as N2N v1 (#6.24 bytes), or
+    as the Cardano HFC form [era, #6.24 bytes] when era is given
+    (ouroboros-network/test/messages.cddl:27-34).  `fields` are the 15 encoded
+    header_body items."""
+    body = _cbor_head(4, 15) + b"".join(fields)
+    inner = b"\x82" + body + cbor_bytes(kes_sig)
+    wrapped = b"\xd8\x18" + cbor_bytes(inner)
+    return wrapped if era is None else b"\x82" + cbor_uint(era) + wrapped
+
+
+def seeded_raw(kats, epoch_nonce, n, spkp=100, rng=None, era_every=3):
+    """n raw wire headers that verify completely under mkSeed inputs: the first
+    golden header's fields re-encoded with a slot per header, both VRF certs
+    proved by the golden VRF key (seed 32 x 0x01) over
+    mkSeed seedEta / seedL slot eta0 (epoch_nonce None = NeutralNonce), a fresh
+    Sum6KES key whose OCERT the golden cold key signs, and the KES signature at
+    t = slot // spkp - kesPeriod over the re-encoded body.  Every era_every-th
+    header is HFC-wrapped.  Returns (list of raw headers, slots)."""
+    rng = rng or np.random.default_rng(11)
+    h0 = H.parse_header(bytes.fromhex(kats["headers"][0]["raw"]))
+    f0 = H.array_items(h0.body, 0)
+    keep = lambda k: h0.body[f0[k][0]:f0[k][1]]  # noqa: E731
+    cold_pk, cold_sk = O.ed25519_keypair(GOLDEN_VRF_SEED)
+    _, vrf_sk = O.vrf_keypair(GOLDEN_VRF_SEED)
+    kes_seed = b"\x05" * 32
+    hot = O.kes_keygen(kes_seed)
+    out, slots = [], []
+    for i in range(n):
+        slot = int(rng.integers(0, 2**40)) if i % 5 else int(rng.integers(0, 2**20))
+        t = int(rng.integers(0, 64))
+        c0 = max(0, slot // spkp - t)
+        t = slot // spkp - c0
+        counter = int(rng.integers(0, 2**16))
+        sigma = O.ed25519_sign(cold_sk, hot + counter.to_bytes(8, "big") + c0.to_bytes(8, "big"))
+        certs = []
+        for uc in (H.SEED_ETA, H.SEED_L):
+            pi = O.vrf_prove(vrf_sk, O.mk_seed(uc, slot, epoch_nonce))
+            certs.append(b"\x82" + cbor_bytes(O.vrf_proof_to_hash(pi)) + cbor_bytes(pi))
+        fields = [keep(0), cbor_uint(slot), keep(2), cbor_bytes(cold_pk), keep(4), certs[0],
+                  certs[1], keep(7), keep(8), cbor_bytes(hot), cbor_uint(counter), cbor_uint(c0),
+                  cbor_bytes(sigma), keep(13), keep(14)]
+        body = _cbor_head(4, 15) + b"".join(fields)
+        sig = O.kes_sign(kes_seed, min(t, 63) if t < 64 else 63, body)
+        out.append(wire_header(fields, sig, era=(2 if i % era_every == 0 else None)))
+        slots.append(slot)
+    return out, np.array(slots, np.uint64)

@@ -134,8 +134,9 @@ def test_nonce_fold_from_device_outputs(gpu_lib, kats):
 
 @contextlib.contextmanager
 def _poisoned_submit():
-    """The plan test hook (kernels.hip plan_poison), reached only through the
-    environment: every submit while it is set first poisons the counters."""
+    """The plan test hook (kernels.hip plan_poison; the test build only),
+    reached through the environment: every submit while it is set first
+    poisons the counters."""
     os.environ["OURO_TEST_PLAN_POISON"] = "1"
     try:
         yield
@@ -143,6 +144,7 @@ def _poisoned_submit():
         del os.environ["OURO_TEST_PLAN_POISON"]
 
 
+@pytest.mark.hooks
 def test_plan_counters_from_cut_off_launch(gpu_lib, kats):
     """A plan whose arrival counters were left mid-count by an earlier launch
     that never completed (simulated: with OURO_TEST_PLAN_POISON set,

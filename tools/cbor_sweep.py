@@ -1,0 +1,81 @@
+"""Tuning sweep of the raw-CBOR pipeline (ouro_tpraos_verify_cbor /
+ouro_integrity_verify_cbor) on one GPU: chunk size, chunks in flight and
+gather threads (OURO_CBOR_CHUNK / _SLOTS / _COPY_THREADS, read per call),
+over n synthetic node-configuration raw headers in pageable host memory.
+Prints one JSON object per configuration (best of `reps` calls).
+    python tools/cbor_sweep.py [n] [reps]"""
+import ctypes
+import itertools
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    import torch
+
+    import bench
+    from ouroboros_network_amd import _native
+
+    n = int(sys.argv[1]) if len(sys.argv) > 1 else 1 << 20
+    reps = int(sys.argv[2]) if len(sys.argv) > 2 else 3
+    dev = torch.device("cuda", 0)
+    lib = _native.load()
+    lib.ouro_bind_thread_to_device(0)
+    eta0 = bytes(range(101, 133))
+    raw, rl = bench.synth_raw_node_headers(n, 1024, dev, eta0)
+    buf = raw.cpu().numpy()
+    del raw
+    torch.cuda.empty_cache()
+    P = lambda a: a.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
+    off = np.arange(n, dtype=np.uint64) * rl
+    ln = np.full(n, rl, np.uint32)
+    e0 = np.frombuffer(eta0, np.uint8).copy()
+    st = np.zeros(n, np.uint8)
+    v = np.zeros(n, np.uint8)
+    be = np.zeros((n, 64), np.uint8)
+    bl = np.zeros((n, 64), np.uint8)
+    stats = np.zeros(6)
+
+    def hdr():
+        return lib.ouro_tpraos_verify_cbor(P(buf), buf.size, P(off), P(ln), n, 129600, P(e0),
+                                           None, None, P(st), P(v), P(be), P(bl), None)
+
+    def kes():
+        return lib.ouro_integrity_verify_cbor(P(buf), buf.size, P(off), P(ln), n, 129600, P(st),
+                                              P(v))
+
+    grid = {
+        "hdr": list(itertools.product([16384, 32768, 65536], [4, 6, 8], [8])) +
+        [(32768, 6, 4), (32768, 6, 16)],
+        "kes": list(itertools.product([32768, 65536, 131072], [3, 6], [8, 16])),
+    }
+    for kind, fn in (("hdr", hdr), ("kes", kes)):
+        for chunk, slots, threads in grid[kind]:
+            os.environ["OURO_CBOR_CHUNK"] = str(chunk)
+            os.environ["OURO_CBOR_SLOTS"] = str(slots)
+            os.environ["OURO_CBOR_COPY_THREADS"] = str(threads)
+            assert fn() == 0, lib.ouro_last_error()
+            ts, ss = [], []
+            for _ in range(reps):
+                t0 = time.perf_counter()
+                assert fn() == 0, lib.ouro_last_error()
+                ts.append(time.perf_counter() - t0)
+                lib.ouro_debug_cbor_stats(stats.ctypes.data)
+                ss.append(stats.copy())
+            k = int(np.argmin(ts))
+            ok = bool((st == 0).all() and (((v & 0x3F) == 0x3F) if kind == "hdr" else v == 1).all())
+            print(json.dumps({"kind": kind, "chunk": chunk, "slots": slots, "threads": threads,
+                              "ms": round(ts[k] * 1e3, 2), "M_per_s": round(n / ts[k] / 1e6, 3),
+                              "gather_ms": round(ss[k][1], 2), "wait_ms": round(ss[k][2], 2),
+                              "all_valid": ok}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
