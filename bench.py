@@ -813,6 +813,65 @@ def e2e_leg(hdr, n: int, reps: int = 3):
     return res
 
 
+def inproc_leg(hdr, n: int, devices, reps: int = 3):
+    """One process, several GPUs: the
+    one-process Haskell node's path, ouro_tpraos_verify_batch_multi over the
+    listed devices -- contiguous shards on persistent per-device workers, each
+    NUMA-bound with its own pinned staging, results straight into the host
+    buffers -- against ouro_tpraos_verify_batch on one device, both from
+    pageable host memory (PCIe-inclusive; never `value`).  A device listed
+    twice runs two pipelines on it (the one-GPU rehearsal)."""
+    from ouroboros_network_amd import _native
+    from ouroboros_network_amd.tpraos import verify_headers, verify_headers_multi
+
+    hb = hdr.host_sample(n)
+    dv = hdr.verdict.cpu().numpy()
+    res = {"workload": f"configs[3] batch of {n} headers in pageable host memory",
+           "devices": list(devices)}
+    for name, fn in (("single_device", lambda: verify_headers(hb)),
+                     ("multi", lambda: verify_headers_multi(hb, devices=list(devices)))):
+        v, _, _ = fn()  # warm: workers, streams, pinned staging
+        ts = []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            v, _, _ = fn()
+            ts.append(time.perf_counter() - t0)
+        res[name] = {"headers_per_s": round(n / min(ts), 1), "ms": round(min(ts) * 1e3, 2),
+                     "equals_device_path": bool((v == dv).all())}
+    workers = np.zeros(64, np.int32), np.zeros(64, np.int32), np.zeros(64, np.int32)
+    k = _native.load().ouro_debug_multi_workers(*[w.ctypes.data for w in workers], 64)
+    res["workers"] = [{"device": int(workers[0][i]), "numa_node": int(workers[1][i]),
+                       "bound_cpus": int(workers[2][i])} for i in range(min(k, 64))]
+    return res
+
+
+def h2d_gbps(device, mib: int = 256, reps: int = 5) -> float:
+    """This rank's pinned host -> HBM copy rate (GB/s, best of reps)."""
+    import torch
+
+    h = torch.empty(mib << 20, dtype=torch.uint8).pin_memory()
+    d = torch.empty(mib << 20, dtype=torch.uint8, device=device)
+    best = 1e9
+    for _ in range(reps):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        d.copy_(h, non_blocking=True)
+        e1.record()
+        torch.cuda.synchronize()
+        best = min(best, e0.elapsed_time(e1))
+    return round((mib << 20) / (best * 1e-3) / 1e9, 2)
+
+
+def pci_bus_id(device) -> str:
+    import torch
+
+    p = torch.cuda.get_device_properties(device)
+    dom, bus, dev = (getattr(p, k, None) for k in ("pci_domain_id", "pci_bus_id", "pci_device_id"))
+    if bus is None:
+        return f"device{device.index}"
+    return f"{dom or 0:04x}:{bus:02x}:{dev or 0:02x}.0"
+
+
 def raw_leg(n: int, npools: int, device, threads: int, chunk: int = 0, reps: int = 3):
     """Raw wire CBOR -> verdicts: n synthetic headers as
     the bytes ChainSync hands over (#6.24-wrapped [header_body, kes_sig],
@@ -1318,6 +1377,10 @@ def main():
     ap.add_argument("--components-only", action="store_true",
                     help="time only the standalone Ed25519 / VRF / Sum6KES kernels over --headers "
                          "items (the profiling run of tools/profile_components.sh)")
+    ap.add_argument("--inproc", default=None,
+                    help="comma-separated device list (e.g. 0,1,2,3 or 0,0): also time "
+                         "ouro_tpraos_verify_batch_multi over those devices in this one process "
+                         "(the one-process node's multi-GPU path; key `inproc`)")
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (RCCL over xGMI, the real path) or gloo (rehearsal of the "
                          "multi-rank path on fewer GPUs: ranks share devices, gather via host)")
@@ -1347,6 +1410,13 @@ def main():
             dist.init_process_group("nccl", device_id=device)
         else:
             dist.init_process_group(args.dist_backend)
+        # a multi-GPU line only from a real N-GPU world: N ranks, each on its
+        # own GPU (the gloo rehearsal may share one); fails loudly otherwise
+        from ouroboros_network_amd.shard import check_rank_devices
+
+        topo = [None] * world
+        dist.all_gather_object(topo, {"rank": rank, "device": gpu, "bus_id": pci_bus_id(device)})
+        check_rank_devices(topo, args.gpus, allow_shared=args.dist_backend != "nccl")
 
     from ouroboros_network_amd.shard import all_gather_results, pack_results
 
@@ -1446,9 +1516,14 @@ def main():
     if world > 1:
         # what the process group itself reports, and every rank's kernel time
         per_rank = [None] * world
+        try:
+            bw = h2d_gbps(device)
+        except Exception:  # noqa: BLE001
+            bw = None
         dist.all_gather_object(per_rank, {"rank": rank, "device": gpu, "headers": n,
+                                          "bus_id": pci_bus_id(device),
                                           "kernel_ms": round(kern_ms, 3),
-                                          "numa_node": numa_node})
+                                          "numa_node": numa_node, "h2d_gb_per_s": bw})
         dist_info = {"world_size_seen": dist.get_world_size(), "backend": dist.get_backend(),
                      "per_rank": per_rank}
         if strong:
@@ -1598,6 +1673,11 @@ def main():
                 out["raw_cbor"] = raw_leg(n, args.pools, device, cpu["usable"])
             except Exception as e:  # noqa: BLE001
                 out["raw_cbor"] = {"error": str(e)}
+        if args.inproc and world == 1:
+            try:
+                out["inproc"] = inproc_leg(hdr, n, [int(x) for x in args.inproc.split(",")])
+            except Exception as e:  # noqa: BLE001
+                out["inproc"] = {"error": str(e)}
         if not args.no_e2e and world == 1:
             try:
                 out["cbor_abi"] = cbor_abi_leg(n, args.pools, device)

@@ -2450,6 +2450,13 @@ int ouro_tpraos_plan_submit(ouro_tpraos_plan* p, const ouro_tpraos_batch* b) {
   p->pending = n;
   p->nonce_dst = b->eta_nonce;
   p->failed = false;
+#if OURO_TEST_HOOKS
+  // TEST HOOK (tests/test_gpu_hooks_plan.py): every result byte of the pinned
+  // output block (not the done word) set to a sentinel before the launch, so
+  // a wait that returned before the kernel's stores were visible would hand
+  // back the sentinel instead of the oracle's verdicts and outputs
+  if (getenv("OURO_TEST_PLAN_SENTINEL")) memset(p->h_out, 0xEE, p->out_bytes - 64);
+#endif
   const bool injected = injected_device_error();
   hipError_t e = hipSetDevice(p->dev);
   if (p->timed && !p->ev0 && e == hipSuccess) {
@@ -2564,12 +2571,33 @@ int ouro_debug_clock_stamps(unsigned long long* out, int max_slots) {
 #endif
 }
 
+}  // extern "C"
+
+namespace {
+// The (offset, length) spans of a host-path batch: the same argument checks
+// as the device calls' window_of: an offset + length that wraps,
+// or a null buffer with any nonzero length, is OURO_EINVAL -- never a read of
+// invalid memory.
+int check_spans(size_t n, const uint64_t* off, const uint32_t* len, const void* buf,
+                const char* what) {
+  for (size_t i = 0; i < n; i++) {
+    if (!len[i]) continue;
+    if (off[i] + len[i] < off[i]) return fail(OURO_EINVAL, "offset + length overflows");
+    if (!buf) return fail(OURO_EINVAL, std::string("null ") + what + " buffer");
+  }
+  return OURO_OK;
+}
+}  // namespace
+
+extern "C" {
+
 // ---- the host path, called explicitly (host_path.h) ----
 int ouro_ed25519_verify_batch_host(size_t n, const uint8_t* pk, const uint8_t* sig,
                                    const uint8_t* msg, const uint64_t* msg_off,
                                    const uint32_t* msg_len, uint8_t* verdict) {
   if (n == 0) return OURO_OK;
   if (!pk || !sig || !msg_off || !msg_len || !verdict) return fail(OURO_EINVAL, "null argument");
+  if (int rc = check_spans(n, msg_off, msg_len, msg, "message")) return rc;
   return ouro_host::ed_batch(n, pk, sig, msg, msg_off, msg_len, verdict, 0);
 }
 int ouro_byron_ed25519_verify_batch_host(size_t n, const uint8_t* pk, const uint8_t* sig,
@@ -2577,6 +2605,7 @@ int ouro_byron_ed25519_verify_batch_host(size_t n, const uint8_t* pk, const uint
                                          const uint32_t* msg_len, uint8_t* verdict) {
   if (n == 0) return OURO_OK;
   if (!pk || !sig || !msg_off || !msg_len || !verdict) return fail(OURO_EINVAL, "null argument");
+  if (int rc = check_spans(n, msg_off, msg_len, msg, "message")) return rc;
   return ouro_host::ed_batch(n, pk, sig, msg, msg_off, msg_len, verdict, 1);
 }
 int ouro_vrf03_verify_batch_host(size_t n, const uint8_t* pk, const uint8_t* proof,
@@ -2586,6 +2615,7 @@ int ouro_vrf03_verify_batch_host(size_t n, const uint8_t* pk, const uint8_t* pro
   if (n == 0) return OURO_OK;
   if (flags & ~OURO_VRF_STRICT_S) return fail(OURO_EINVAL, "unknown VRF flags");
   if (!pk || !proof || !alpha_off || !alpha_len || !verdict) return fail(OURO_EINVAL, "null argument");
+  if (int rc = check_spans(n, alpha_off, alpha_len, alpha, "alpha")) return rc;
   return ouro_host::vrf_batch(n, pk, proof, alpha, alpha_off, alpha_len, beta, verdict, flags);
 }
 int ouro_sum6kes_verify_batch_host(size_t n, const uint8_t* vk, const uint32_t* t,
@@ -2593,6 +2623,7 @@ int ouro_sum6kes_verify_batch_host(size_t n, const uint8_t* vk, const uint32_t* 
                                    const uint32_t* msg_len, const uint8_t* sig, uint8_t* verdict) {
   if (n == 0) return OURO_OK;
   if (!vk || !t || !msg_off || !msg_len || !sig || !verdict) return fail(OURO_EINVAL, "null argument");
+  if (int rc = check_spans(n, msg_off, msg_len, msg, "message")) return rc;
   return ouro_host::kes_batch(n, vk, t, msg, msg_off, msg_len, sig, verdict);
 }
 int ouro_tpraos_verify_batch_host(const ouro_tpraos_batch* b, uint8_t* verdict,
@@ -2602,6 +2633,7 @@ int ouro_tpraos_verify_batch_host(const ouro_tpraos_batch* b, uint8_t* verdict,
   if (!verdict) return fail(OURO_EINVAL, "null verdict");
   int rc = check_hdr_batch(b);
   if (rc) return rc;
+  if ((rc = check_spans(b->n, b->body_off, b->body_len, b->body, "body"))) return rc;
   return ouro_host::hdr_batch(b, verdict, beta_eta, beta_leader);
 }
 int ouro_leader_check_batch_host(size_t n, const uint8_t* beta, const uint64_t* sigma_num,

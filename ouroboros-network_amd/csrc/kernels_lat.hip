@@ -465,7 +465,11 @@ __global__ void __launch_bounds__(kBlock, OURO_LAT_WAVES) k_tpraos_cores(ouro_tp
       // each header's tail releases its outputs to the host and counts itself
       // in win_ctr (zeroed by the window's input copy); the last one writes the
       // launch's generation, which the plan's wait spins on instead of the
-      // stream's completion
+      // stream's completion.  Every lane of the wave first releases its own
+      // stores at system scope (the tail's lanes write the verdict and both
+      // outputs -- lane 32 beta_leader -- not only lane 0), so the done word
+      // can never become visible before any of them.
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
       if ((threadIdx.x & 63u) == 0) {
         const uint32_t prev =
             __hip_atomic_fetch_add(win_ctr, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_SYSTEM);

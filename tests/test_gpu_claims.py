@@ -173,3 +173,29 @@ def test_plan_counters_from_cut_off_launch(gpu_lib, kats):
             _check(plan.run(second.slice(5, 17), nonce=True), tuple(a[5:17] for a in w2))
     finally:
         plan.close()
+
+
+@pytest.mark.hooks
+def test_plan_results_never_stale(gpu_lib, kats):
+    """ADVICE r04 (the done word): with OURO_TEST_PLAN_SENTINEL (test build)
+    every result byte of the plan's pinned output block is overwritten with a
+    sentinel before each launch, so a wait that returned before all of the
+    tail's stores were visible -- the verdict and both outputs, written by
+    several lanes of the tail wave -- would return the sentinel.  Windows
+    alternate between two different batches; every one must equal the oracle."""
+    from ouroboros_network_amd import tpraos as T
+
+    a = HC.golden_variants(kats, stride=13).slice(0, 64)
+    b = HC.seeded(kats, bytes(range(32)), copies=4).slice(0, 40)
+    wa, wb = O.tpraos_verify_batch_nonce(a), O.tpraos_verify_batch_nonce(b)
+    plan = T.HeaderPlan(64, 64 * 1400)
+    os.environ["OURO_TEST_PLAN_SENTINEL"] = "1"
+    try:
+        for k in range(200):
+            batch, want = (a, wa) if k % 2 == 0 else (b, wb)
+            got = plan.run(batch, nonce=True)
+            for g, w in zip(got, want):
+                np.testing.assert_array_equal(g, w)
+    finally:
+        del os.environ["OURO_TEST_PLAN_SENTINEL"]
+        plan.close()

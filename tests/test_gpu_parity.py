@@ -6,6 +6,8 @@ Inputs: seeded synthetic batches (oracle signer, SURVEY.md §8(d) seeds), with
 offset; ouroboros-consensus-test/src/Test/Util/Corruption.hs), plus the fixed
 edge-case sets in edge_cases.py.
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -230,7 +232,21 @@ def test_golden_tx_witnesses(gpu_lib, kats):
     assert got.all()
 
 
-def test_single_item_abi(gpu_lib, kats):
+@pytest.fixture(params=["gpu", "host"])
+def single_route(request):
+    """Single items on both routes (VERDICT r04 hygiene): the host path (the
+    default since round 4) and the GPU (OURO_SINGLE_ITEM=gpu), so the -m gpu
+    set exercises the device's single-item route too."""
+    old = os.environ.get("OURO_SINGLE_ITEM")
+    os.environ["OURO_SINGLE_ITEM"] = request.param
+    yield request.param
+    if old is None:
+        os.environ.pop("OURO_SINGLE_ITEM", None)
+    else:
+        os.environ["OURO_SINGLE_ITEM"] = old
+
+
+def test_single_item_abi(gpu_lib, kats, single_route):
     from ouroboros_network_amd import Ed25519DSIGN, PraosVRF, Sum6KES
     from ouroboros_network_amd import header as H
 
@@ -522,7 +538,7 @@ def test_byron_raw_headers_to_verdicts(small_path, gpu_lib, kats):
     assert not bad.any() and (st == B.PACK_OK).all()
 
 
-def test_kes_periods_beyond_the_tree(gpu_lib):
+def test_kes_periods_beyond_the_tree(gpu_lib, single_route):
     """Periods >= 64 (the reference's Period is a 64-bit Word): every t >= 63
     walks right at all six levels to leaf 63 (SumKES.verifyKES; SingleKES's
     assert is compiled out), so a leaf-63 signature verifies and others do

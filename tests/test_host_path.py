@@ -3,9 +3,12 @@ oracle, on the CPU -- no GPU needed.
 
 Since round 4 the single-item entry points (ouro_ed25519_verify,
 ouro_byron_ed25519_verify, ouro_vrf03_verify, ouro_vrf03_proof_to_hash,
-ouro_sum6kes_verify) run the kernels' own lane routines compiled for the CPU,
-and every host-buffer batch whose device run fails is recomputed on that path
-(include/ouro_verify.h).  The explicit *_batch_host entry points expose it for
+ouro_sum6kes_verify) run on the CPU, and every host-buffer batch whose device
+run fails is recomputed on that path (include/ouro_verify.h).  Since round 5
+the path's field and group arithmetic is its own 64-bit implementation
+(csrc/host_fast.h: 5 x 51-bit limbs); OURO_HOST_IMPL=lanes selects the
+kernels' lane routines compiled for the CPU instead, and every test here runs
+both.  The explicit *_batch_host entry points expose it for
 batches.  These tests load the product library itself (lib/libouro_verify.so)
 and compare with the oracle (oracle/, test infrastructure only) on the same
 edge-case sets the GPU parity tests use; nothing under oracle/ is linked into
@@ -28,11 +31,67 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB = os.path.join(ROOT, "ouroboros-network_amd", "lib", "libouro_verify.so")
 
 
-@pytest.fixture(scope="module")
-def lib():
+@pytest.fixture(scope="module", params=["fast", "lanes"])
+def lib(request):
     from ouroboros_network_amd import _native
 
-    return _native.load()
+    old = os.environ.get("OURO_HOST_IMPL")
+    os.environ["OURO_HOST_IMPL"] = request.param
+    yield _native.load()
+    if old is None:
+        os.environ.pop("OURO_HOST_IMPL", None)
+    else:
+        os.environ["OURO_HOST_IMPL"] = old
+
+
+@pytest.fixture(params=["fast", "lanes"])
+def impl(request):
+    """the host path's implementation for tests that call through Python"""
+    old = os.environ.get("OURO_HOST_IMPL")
+    os.environ["OURO_HOST_IMPL"] = request.param
+    yield request.param
+    if old is None:
+        os.environ.pop("OURO_HOST_IMPL", None)
+    else:
+        os.environ["OURO_HOST_IMPL"] = old
+
+
+def test_host_entries_check_their_spans(lib):
+    """the *_batch_host entries run the device calls' span checks --
+    a NULL message with a nonzero length and an offset that wraps are
+    OURO_EINVAL, never a read of invalid memory."""
+    P = ctypes.c_void_p
+    n = 2
+    pk = np.zeros((n, 32), np.uint8)
+    sig = np.zeros((n, 64), np.uint8)
+    v = np.zeros(n, np.uint8)
+    ln = np.array([0, 5], np.uint32)
+    off = np.array([0, 0], np.uint64)
+    wrap = np.array([0, 2**64 - 2], np.uint64)
+    msg = np.zeros(16, np.uint8)
+    for fn in (lib.ouro_ed25519_verify_batch_host, lib.ouro_byron_ed25519_verify_batch_host):
+        assert fn(n, O.p(pk), O.p(sig), None, O.p(off), O.p(ln), O.p(v)) == -3
+        assert fn(n, O.p(pk), O.p(sig), O.p(msg), O.p(wrap), O.p(ln), O.p(v)) == -3
+    pi = np.zeros((n, 80), np.uint8)
+    assert lib.ouro_vrf03_verify_batch_host(n, O.p(pk), O.p(pi), None, O.p(off), O.p(ln), None,
+                                            O.p(v), 0) == -3
+    t = np.zeros(n, np.uint32)
+    ks = np.zeros((n, 448), np.uint8)
+    assert lib.ouro_sum6kes_verify_batch_host(n, O.p(pk), O.p(t), O.p(msg), O.p(wrap), O.p(ln),
+                                              O.p(ks), O.p(v)) == -3
+    # a header batch whose body span wraps
+    batch = HC.golden_variants(__import__("json").load(open(os.path.join(
+        ROOT, "tests", "golden", "reference_kats.json"))), stride=400, s_rows=False)
+    bo = batch.body_off.copy()
+    bo[-1] = 2**64 - 3
+    s = batch.c_struct()
+    s.body_off = bo.ctypes.data  # (HeaderBatch itself rejects such offsets)
+    vv = np.zeros(len(batch), np.uint8)
+    assert lib.ouro_tpraos_verify_batch_host(ctypes.byref(s), O.p(vv), None, None) == -3
+    # zero-length spans need no buffer at all
+    z = np.zeros(n, np.uint32)
+    assert lib.ouro_ed25519_verify_batch_host(n, O.p(pk), O.p(sig), None, O.p(off), O.p(z),
+                                              O.p(v)) == 0
 
 
 def _counts(lib):
@@ -62,7 +121,7 @@ def test_ed25519_single_edge_cases(lib):
         assert (got == 0) == O.ed25519_verify(sig, m, pk)
 
 
-def test_ed25519_batch_host_corrupted_and_ragged():
+def test_ed25519_batch_host_corrupted_and_ragged(impl):
     """Batches over host threads: synthetic signatures with 1/3 corrupted,
     messages of ragged lengths (0..300 B, unaligned offsets)."""
     from ouroboros_network_amd import dsign
@@ -136,7 +195,7 @@ def test_vrf_single_vectors_and_edges(lib, kats):
             assert h.raw == want_h
 
 
-def test_vrf_batch_host_both_s_modes():
+def test_vrf_batch_host_both_s_modes(impl):
     from ouroboros_network_amd import vrf
 
     pk, proof, alpha = O.synth_vrf(40, first=11)
@@ -188,7 +247,7 @@ def _oracle_hdr(batch, nonce=False):
     return O.tpraos_verify_batch_nonce(batch) if nonce else O.tpraos_verify_batch(batch)
 
 
-def test_headers_host_golden_variants(kats):
+def test_headers_host_golden_variants(kats, impl):
     """k_tpraos_verify's body on the host: golden headers and every kind of
     single-field corruption hdr_cases makes, equal to the oracle's verdict
     bits and outputs."""
@@ -202,7 +261,7 @@ def test_headers_host_golden_variants(kats):
     assert (got[0] & 0x0F != 15).sum() > 10
 
 
-def test_headers_host_claims_seeds_nonces(kats):
+def test_headers_host_claims_seeds_nonces(kats, impl):
     from ouroboros_network_amd.tpraos import verify_headers_host
 
     rng = np.random.default_rng(21)

@@ -162,3 +162,54 @@ def test_result_gather_over_rccl(tmp_path):
     collective bench.py uses at N > 1, exercised on the one-GPU box."""
     mp.spawn(_nccl_worker, args=(1, _free_port(), str(tmp_path)), nprocs=1, join=True)
     assert (tmp_path / "ok").read_text() == "1"
+
+
+def _topology_worker(rank, world, port, out_dir, shared):
+    import json
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    import torch.distributed as dist
+
+    from ouroboros_network_amd.shard import check_rank_devices
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    info = {"rank": rank, "device": 0 if shared else rank,
+            "bus_id": "0000:05:00.0" if shared else f"0000:{5 + rank:02x}:00.0"}
+    infos = [None] * world
+    dist.all_gather_object(infos, info)
+    res = {}
+    for name, kw in (("exact", dict(expected_world=world)),
+                     ("wrong_n", dict(expected_world=world + 1)),
+                     ("shared_ok", dict(expected_world=world, allow_shared=True))):
+        try:
+            check_rank_devices(infos, **kw)
+            res[name] = "ok"
+        except RuntimeError as e:
+            res[name] = str(e)
+    dist.destroy_process_group()
+    with open(os.path.join(out_dir, f"r{rank}.json"), "w") as f:
+        json.dump(res, f)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("shared", [False, True])
+def test_bench_rank_device_checks_gloo(tmp_path, world, shared):
+    """bench.py --gpus N refuses a line unless the process group has N ranks
+    and (outside the gloo rehearsal) every rank drives its own GPU: the check
+    run over a real gloo world of 2 and 3 ranks with distinct and with shared
+    devices."""
+    import json
+
+    mp.spawn(_topology_worker, args=(world, _free_port(), str(tmp_path), shared), nprocs=world,
+             join=True)
+    for r in range(world):
+        res = json.load(open(tmp_path / f"r{r}.json"))
+        assert res["wrong_n"].startswith("world size")
+        assert res["shared_ok"] == "ok"
+        if shared:
+            assert "share GPUs" in res["exact"]
+        else:
+            assert res["exact"] == "ok"
