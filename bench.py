@@ -1268,7 +1268,9 @@ def single_item_leg(ed, hdr, iters: int = 300):
     number a per-item Haskell FFI caller sees -- on both routes: the library's
     host path (the default since round 4: the kernels' lane routines compiled
     for the CPU) and the GPU (OURO_SINGLE_ITEM=gpu: a one-item batch, H2D,
-    one wave, D2H), next to the reference's own libsodium call on the host."""
+    one wave, D2H), next to the reference's own libsodium call on the host;
+    host_path_lanes = the round-4 host path (the kernels' lane routines
+    compiled for the CPU, OURO_HOST_IMPL=lanes) for comparison."""
     from ouroboros_network_amd import _native
 
     lib = _native.load()
@@ -1315,10 +1317,22 @@ def single_item_leg(ed, hdr, iters: int = 300):
             else:
                 os.environ["OURO_SINGLE_ITEM"] = old
 
+    def lanes_route():
+        old = os.environ.get("OURO_HOST_IMPL")
+        os.environ["OURO_HOST_IMPL"] = "lanes"
+        try:
+            return route("host")
+        finally:
+            if old is None:
+                os.environ.pop("OURO_HOST_IMPL", None)
+            else:
+                os.environ["OURO_HOST_IMPL"] = old
+
     res = {"workload": f"{iters} single-item calls, valid synthetic items, one thread",
            "routing": "single items run on the library's host path by default "
-                      "(include/ouro_verify.h); OURO_SINGLE_ITEM=gpu sends them to the device",
-           "host_path": route("host"), "gpu": route("gpu")}
+                      "(include/ouro_verify.h; since round 5 its own 5 x 51-bit CPU arithmetic, "
+                      "csrc/host_fast.h); OURO_SINGLE_ITEM=gpu sends them to the device",
+           "host_path": route("host"), "host_path_lanes": lanes_route(), "gpu": route("gpu")}
     # the default route's figures at the top level (the names the ABI exports)
     res.update(res["host_path"])
     if os.path.exists(SODIUM_SO):

@@ -338,9 +338,9 @@ int ouro_integrity_verify_cbor(const uint8_t *raw, size_t raw_bytes, const uint6
  * and per chunk one stream uploads the raw bytes, runs the device slicer
  * and the header kernel and copies the results back, several chunks in
  * flight so the host copies and PCIe hide behind the kernels
- * (OURO_CBOR_CHUNK headers per chunk, default 32768; OURO_CBOR_SLOTS chunks
- * in flight, default 6, at most 8; OURO_CBOR_COPY_THREADS gather threads,
- * default 8).  Synchronous; a device error recomputes the batch on the host
+ * (OURO_CBOR_CHUNK headers per chunk, default 65536; OURO_CBOR_SLOTS chunks
+ * in flight, default 6 -- 4 for ouro_integrity_verify_cbor --, at most 8;
+ * OURO_CBOR_COPY_THREADS gather threads, default 8).  Synchronous; a device error recomputes the batch on the host
  * path.  OURO_EINVAL for a span outside raw_bytes, NULLs, a zero period or
  * only one of the two alpha arrays. */
 int ouro_tpraos_verify_cbor(const uint8_t *raw, size_t raw_bytes, const uint64_t *off,

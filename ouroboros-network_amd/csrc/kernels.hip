@@ -78,6 +78,13 @@ __global__ void __launch_bounds__(kBlock, OURO_WAVES) k_vrf03_verify(
   }
 }
 
+// OURO_KES_STAGE=1: the leaf message's tail (the header body) staged by the
+// wave into LDS with coalesced loads (sha512.h ShaStagedTail); the loop then
+// runs whole waves (a lane past the batch end repeats the last item, its
+// verdict not stored) because staging needs every lane.
+#ifndef OURO_KES_STAGE
+#define OURO_KES_STAGE 0
+#endif
 __global__ void __launch_bounds__(kBlock, OURO_WAVES) k_sum6kes_verify(
     size_t n, const uint8_t* __restrict__ vk, const uint32_t* __restrict__ t,
     const uint8_t* __restrict__ msg, const uint64_t* __restrict__ msg_off,
@@ -86,6 +93,22 @@ __global__ void __launch_bounds__(kBlock, OURO_WAVES) k_sum6kes_verify(
   const size_t tid = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   const size_t nth = (size_t)gridDim.x * blockDim.x;
   const Slot lane = slot_of(scratch, tid, kSlotWords);
+#if OURO_KES_STAGE
+  __shared__ uint32_t s_stage[kBlock / 64 * kStageWaveDw];
+  uint32_t* rows = s_stage + (threadIdx.x >> 6) * kStageWaveDw;
+  const size_t lid = threadIdx.x & 63u;
+  for (size_t base = tid - lid; base < n; base += nth) {  // wave-uniform
+    const size_t i0 = base + lid;
+    const size_t i = i0 < n ? i0 : n - 1;
+    uint32_t v[8];
+    load_words(v, vk + 32 * i, 2);
+    const uint32_t* sw = reinterpret_cast<const uint32_t*>(sig + 448 * i);
+    const bool ok = sum6kes_verify_lane(v, t[i], sw, ShaStagedTail{msg + msg_off[i], rows},
+                                        msg_len[i], lane, btab);
+    if (i0 < n) verdict[i0] = ok ? 1 : 0;
+  }
+  return;
+#endif
   for (size_t i = tid; i < n; i += nth) {
     uint32_t v[8];
     load_words(v, vk + 32 * i, 2);
@@ -1721,8 +1744,9 @@ int ouro_tpraos_pack_cbor_device(void* stream, const uint8_t* raw, size_t raw_by
 // .../Storage/ImmutableDB/Impl/Validation.hs:358-365).  raw_run takes such a
 // batch straight through the device:
 //   * the batch is cut into chunks of whole headers (OURO_CBOR_CHUNK headers,
-//     default 32,768, and at most kRawChunkBytes of raw bytes each);
-//   * chunk c runs on slot c % S (S = OURO_CBOR_SLOTS streams, default 6):
+//     default 65,536, and at most kRawChunkBytes of raw bytes each);
+//   * chunk c runs on slot c % S (S = OURO_CBOR_SLOTS streams, default 6 for
+//     headers, 4 for integrity):
 //     the library's worker pool gathers its header spans from the caller's
 //     pageable buffer into the slot's pinned, NUMA-local staging (runs of
 //     adjacent spans as one memcpy; offsets rebased by a prefix sum), the
@@ -1952,7 +1976,10 @@ int raw_run(const RawCall& c, const std::vector<RawChunk>& chunks) {
   int dev, rc = device_state(&ds);
   if (rc || (rc = current_device(&dev))) return rc;
   RawPipe& p = ctx_of(dev).raw;
-  const int S = (int)env_size("OURO_CBOR_SLOTS", 6, 1, kRawMaxSlots);
+  // chunks in flight: the header kernel wants ~3 grids of work queued (6 x
+  // 64 K headers); the Sum6KES kernel is PCIe-bound, 4 suffice
+  // (profiles/r05a/cbor_sweep.jsonl)
+  const int S = (int)env_size("OURO_CBOR_SLOTS", c.kind == kRawKes ? 4 : 6, 1, kRawMaxSlots);
   for (int k = 0; k < S; k++) {
     RawSlot& s = p.s[k];
     if (!s.st) OURO_HIP(hipStreamCreateWithFlags(&s.st, hipStreamNonBlocking));
@@ -2033,7 +2060,7 @@ int raw_verify(const RawCall& c) {
   if ((c.ea == nullptr) != (c.la == nullptr))
     return fail(OURO_EINVAL, "give both VRF input arrays or neither");
   std::vector<RawChunk> chunks;
-  const size_t per = env_size("OURO_CBOR_CHUNK", 32768, 256, (size_t)1 << 24);
+  const size_t per = env_size("OURO_CBOR_CHUNK", 65536, 256, (size_t)1 << 24);
   int rc = raw_chunks(c, per, &chunks);
   if (rc) return rc;
   return or_host(raw_run(c, chunks), [&] { return raw_host(c); });
@@ -2122,6 +2149,29 @@ __global__ void __launch_bounds__(256) k_plan_stage(const uint4* __restrict__ sr
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n16) dst[i] = src[i];
 }
+// The same over the byte ranges a window actually uses (the block header, and
+// per member given its n rows or the body span -- not the capacity), in 16-B
+// units: thread t copies unit t of the concatenated ranges (round 5: the
+// copy reads pinned memory over PCIe, so its bytes are its time).
+constexpr int kPlanMaxRanges = 24;
+struct PlanRanges {
+  uint32_t count;
+  uint32_t start16[kPlanMaxRanges];
+  uint32_t len16[kPlanMaxRanges];
+};
+__global__ void __launch_bounds__(256) k_plan_stage_ranges(const uint4* __restrict__ src,
+                                                           uint4* __restrict__ dst,
+                                                           PlanRanges r) {
+  uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  for (uint32_t k = 0; k < r.count; k++) {
+    if (t < r.len16[k]) {
+      const uint32_t i = r.start16[k] + t;
+      dst[i] = src[i];
+      return;
+    }
+    t -= r.len16[k];
+  }
+}
 
 // ---- plans: pinned staging, the window's copy kernel + latency kernel -------
 // issued straight on the plan's stream per window (default), or replayed from
@@ -2177,6 +2227,11 @@ struct ouro_tpraos_plan {
   bool flag = false;
   uint32_t* done_dev = nullptr;              // that word as the kernel sees it
   const volatile uint32_t* done_host = nullptr;
+  // the window's used byte ranges of the input block (recorded at submit):
+  // the copy kernel moves those instead of the whole capacity block
+  // (OURO_PLAN_TRIM=0 at create: the whole block, the round-4 form)
+  bool trim = true;
+  PlanRanges ranges{};
 };
 
 namespace {
@@ -2202,7 +2257,13 @@ void plan_free(ouro_tpraos_plan* p) {
 // the window's launches on the plan's stream: issued per submit (the
 // default), or captured once into the graph (OURO_PLAN_GRAPH=1, A/B)
 int plan_enqueue(ouro_tpraos_plan* p) {
-  if (p->stage == 1 || p->stage == 2) {
+  if ((p->stage == 1 || p->stage == 2) && p->ranges.count && !p->use_graph) {
+    uint32_t units = 0;
+    for (uint32_t k = 0; k < p->ranges.count; k++) units += p->ranges.len16[k];
+    hipLaunchKernelGGL(k_plan_stage_ranges, dim3((units + 255) / 256), dim3(256), 0, p->st,
+                       static_cast<const uint4*>(p->hin), reinterpret_cast<uint4*>(p->d_in),
+                       p->ranges);
+  } else if (p->stage == 1 || p->stage == 2) {
     const size_t n16 = p->in_bytes / 16;  // in_bytes is a multiple of 16
     hipLaunchKernelGGL(k_plan_stage, dim3((unsigned)((n16 + 255) / 256)), dim3(256), 0, p->st,
                        static_cast<const uint4*>(p->hin), reinterpret_cast<uint4*>(p->d_in), n16);
@@ -2260,6 +2321,7 @@ int plan_build(ouro_tpraos_plan* p) {
   if (const char* e = getenv("OURO_PLAN_STAGE")) p->stage = atoi(e);
   if (const char* e = getenv("OURO_PLAN_SPIN")) p->spin = atoi(e);
   if (const char* e = getenv("OURO_PLAN_GRAPH")) p->use_graph = atoi(e) != 0;
+  if (const char* e = getenv("OURO_PLAN_TRIM")) p->trim = atoi(e) != 0;
   if (p->stage >= 1) OURO_HIP(hipHostGetDevicePointer(&p->hin, p->h_in, 0));
   uint8_t* d = p->stage >= 3 ? static_cast<uint8_t*>(p->hin) : p->d_in;
   ouro_tpraos_batch& b = p->dev_batch;
@@ -2431,10 +2493,31 @@ int ouro_tpraos_plan_submit(ouro_tpraos_plan* p, const ouro_tpraos_batch* b) {
   const auto tc0 = std::chrono::steady_clock::now();
   if (b->slot) src[kFEtaAlpha] = src[kFLeaderAlpha] = nullptr;  // derived on the device
   else src[kFEpochNonce] = nullptr;
+  bool trim = p->trim;
+  p->ranges.count = 0;
+  if (trim) {  // the block header: n, option bits, generation, window counter
+    p->ranges.start16[0] = 0;
+    p->ranges.len16[0] = 1;
+    p->ranges.count = 1;
+  }
   for (int f = 0; f < kPlanFields; f++) {
     const size_t bytes = kFieldBytes[f] > 0 ? (size_t)kFieldBytes[f] * n
                                             : (kFieldBytes[f] == 0 ? w.span() : 32);
-    if (bytes && src[f]) memcpy(p->h_in + p->off[f], src[f], bytes);
+    if (bytes && src[f]) {
+      memcpy(p->h_in + p->off[f], src[f], bytes);
+      if (trim) {
+        PlanRanges& r = p->ranges;
+        const uint32_t s16 = (uint32_t)(p->off[f] / 16), l16 = (uint32_t)((bytes + 15) / 16);
+        if (r.start16[r.count - 1] + r.len16[r.count - 1] == s16) r.len16[r.count - 1] += l16;
+        else if (r.count < (uint32_t)kPlanMaxRanges) {
+          r.start16[r.count] = s16;
+          r.len16[r.count++] = l16;
+        } else {
+          r.count = 0;  // (cannot happen: 19 members) copy the whole block
+          trim = false;
+        }
+      }
+    }
   }
   if (p->timed)
     p->copy_us = std::chrono::duration<float, std::micro>(std::chrono::steady_clock::now() - tc0).count();

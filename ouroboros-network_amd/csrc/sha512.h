@@ -158,6 +158,29 @@ struct ShaGlobalTail {
 #endif
 };
 
+// A tail in global memory that the WAVE stages into LDS with coalesced loads
+// (round 5, OURO_KES_STAGE; the throughput Sum6KES kernel's leaf message).
+// Each lane's message sits at its own address, so the per-lane loads of
+// ShaGlobalTail touch 64 cache lines per wave instruction; here the wave loads
+// lane k's next 256 bytes with all 64 lanes at once (one dword each: four
+// lines per instruction), k = 0..63, into row k of the wave's LDS block, and
+// each lane then builds its message words from its own row.  Stage s covers
+// tail bytes [t0, t0 + 256), t0 = 0 (blocks 0, 1 of an R || A || M hash:
+// prefix 64 bytes) or 256 s - 64 (blocks 2s, 2s + 1).  Loads stop at the
+// message end exactly as ShaGlobalTail's do (only dwords that start before
+// it).  Needs every lane of the wave active (the kernel keeps EXEC full).
+constexpr int kStageRowDw = 65;                       // odd: conflict-free row reads
+constexpr int kStageWaveDw = 64 * kStageRowDw;        // 16,640 B per wave
+struct ShaStagedTail {
+  const uint8_t* msg;
+  uint32_t* rows;  // this wave's kStageWaveDw dwords of LDS
+  OURO_FI uint32_t tail(uint32_t q) const { return ldg_u8(msg + q); }
+};
+template <class T>
+struct is_staged_tail : std::false_type {};
+template <>
+struct is_staged_tail<ShaStagedTail> : std::true_type {};
+
 template <class T, class = void>
 struct has_word_be : std::false_type {};
 template <class T>
@@ -186,12 +209,116 @@ OURO_FI uint64_t sha_pad_word(uint64_t raw, uint32_t p, uint32_t total) {
   return (raw & keep) | (0x80ull << (56 - 8 * v));
 }
 
+#if defined(__HIP_DEVICE_COMPILE__)
+// largest lane value over the wave (every lane active)
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t x) {
+  uint32_t m = 0;
+#pragma unroll 1
+  for (int b = 31; b >= 0; b--) {
+    const uint32_t t = m | (1u << b);
+    if (__ballot(x >= t) != 0) m = t;
+  }
+  return m;
+}
+// tail bytes [t0, t0 + 256) of every lane's message into its LDS row: iteration
+// k loads 64 consecutive dwords of lane k's message, one per lane; then each
+// lane its own 65th dword
+__device__ __forceinline__ void sha_stage(const ShaStagedTail& t, uint32_t t0, uint32_t tl) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint64_t base = (uint64_t)(uintptr_t)t.msg;
+  const uint64_t w0 = (base + t0) & ~3ull, end = base + tl;
+  const int wlo = (int)(uint32_t)w0, whi = (int)(uint32_t)(w0 >> 32);
+  const int elo = (int)(uint32_t)end, ehi = (int)(uint32_t)(end >> 32);
+#pragma unroll 8
+  for (int k = 0; k < 64; k++) {
+    const uint64_t bk = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(whi, k) << 32) |
+                        (uint32_t)__builtin_amdgcn_readlane(wlo, k);
+    const uint64_t ek = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(ehi, k) << 32) |
+                        (uint32_t)__builtin_amdgcn_readlane(elo, k);
+    const uint64_t ad = bk + 4ull * lane;
+    t.rows[k * kStageRowDw + lane] =
+        ad < ek ? (uint32_t)ldg1(reinterpret_cast<const void*>((uintptr_t)ad)) : 0u;
+  }
+  const uint64_t ad = w0 + 256;
+  t.rows[lane * kStageRowDw + 64] =
+      ad < end ? (uint32_t)ldg1(reinterpret_cast<const void*>((uintptr_t)ad)) : 0u;
+}
+// sha512_prefixed over a 64-byte register prefix and a staged tail: the block
+// loop runs to the wave's largest block count (staging needs the whole wave),
+// each lane compressing only its own blocks
+template <int PL>
+__device__ __forceinline__ void sha512_prefixed_staged(uint64_t out[8], const uint32_t* prefix,
+                                                       const ShaStagedTail& tail, uint32_t tl) {
+  static_assert(PL == 64, "staged tails follow a 64-byte prefix (R || A)");
+  const uint32_t total = PL + tl;
+  const uint32_t nb = (total + 17 + 127) >> 7;
+  const uint32_t nbmax = wave_max_u32(nb);
+  const uint32_t r8 = (uint32_t)((uintptr_t)tail.msg & 3u) * 8u;
+  const uint32_t* row = tail.rows + (threadIdx.x & 63u) * kStageRowDw;
+  uint32_t t0 = 0;
+  auto word = [&](uint32_t q) -> uint64_t {  // tail bytes q..q+7, big-endian
+    const uint32_t di = (q - t0) >> 2;
+    const uint32_t d0 = row[di], d1 = row[di + 1], d2 = row[di + 2];
+    const uint32_t lo = __builtin_amdgcn_alignbit(d1, d0, r8);
+    const uint32_t hi = __builtin_amdgcn_alignbit(d2, d1, r8);
+    return ((uint64_t)__builtin_bswap32(lo) << 32) | __builtin_bswap32(hi);
+  };
+  auto len_words = [&](uint32_t widx, uint64_t r) -> uint64_t {
+    if (widx == nb * 16 - 1) return (uint64_t)total << 3;
+    if (widx == nb * 16 - 2) return 0;
+    return r;
+  };
+  uint64_t H[8];
+  sha512_init(H);
+  sha_stage(tail, 0, tl);
+  {
+    uint64_t W[16];
+#pragma unroll
+    for (int w = 0; w < 16; w++) {
+      const uint32_t p0 = (uint32_t)(w * 8);
+      uint64_t r;
+      if (w < 8) {
+        r = ((uint64_t)__builtin_bswap32(prefix[2 * w]) << 32) | __builtin_bswap32(prefix[2 * w + 1]);
+      } else {
+        r = sha_pad_word(word(p0 - PL), p0, total);
+      }
+      W[w] = len_words((uint32_t)w, r);
+    }
+    sha512_compress(H, W);
+  }
+#pragma unroll 1
+  for (uint32_t b = 1; b < nbmax; b++) {
+    if (b >= 2 && (b & 1u) == 0) {
+      t0 = 256u * (b >> 1) - 64u;
+      sha_stage(tail, t0, tl);
+    }
+    if (b < nb) {
+      uint64_t W[16];
+#pragma unroll
+      for (int w = 0; w < 16; w++) {
+        const uint32_t p0 = b * 128 + (uint32_t)w * 8;
+        W[w] = len_words(b * 16 + (uint32_t)w, sha_pad_word(word(p0 - PL), p0, total));
+      }
+      sha512_compress(H, W);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 8; i++) out[i] = H[i];
+}
+#endif
+
 // SHA-512 over prefix (PL bytes, as little-endian packed words) || tail (tl
 // bytes).  PL <= 128 - 17 is not required: the prefix may spill into block 1
 // only for all-register inputs (tail length 0), which stay fully unrolled.
 template <int PL, class Tail>
 OURO_FI void sha512_prefixed(uint64_t out[8], const uint32_t* prefix, const Tail& tail,
                              uint32_t tl) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  if constexpr (is_staged_tail<Tail>::value) {
+    sha512_prefixed_staged<PL>(out, prefix, tail, tl);
+    return;
+  }
+#endif
   const uint32_t total = PL + tl;
   const uint32_t nb = (total + 17 + 127) >> 7;
   uint64_t H[8];

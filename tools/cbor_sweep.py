@@ -52,9 +52,9 @@ def main():
                                               P(v))
 
     grid = {
-        "hdr": list(itertools.product([16384, 32768, 65536], [4, 6, 8], [8])) +
-        [(32768, 6, 4), (32768, 6, 16)],
-        "kes": list(itertools.product([32768, 65536, 131072], [3, 6], [8, 16])),
+        "hdr": [(65536, 5, 8), (65536, 6, 8), (65536, 7, 8), (98304, 4, 8), (98304, 5, 8),
+                (131072, 3, 8), (131072, 4, 8), (49152, 8, 8)],
+        "kes": [(65536, 2, 8), (65536, 3, 8), (65536, 4, 8), (49152, 4, 8), (98304, 3, 8)],
     }
     for kind, fn in (("hdr", hdr), ("kes", kes)):
         for chunk, slots, threads in grid[kind]:
