@@ -888,11 +888,38 @@ __device__ __forceinline__ bool eds_combine(Slot e) {
   return ldg1(e.word(kEsOk)) != 0 && pw_is_identity(Q);
 }
 
-// V = [s]H - [c]Gamma over THREE waves: [s windows 0..31]H (the V item),
-// [s windows 32..63](2^128 H) (the V2 item: H again, then 128 doublings) and
-// -[c]Gamma (the Gamma item); the last of the three adds them and encodes H
-// and V.  Record per VRF (kLatVsplit + 4 kPwWords which): H, the low and
-// high parts, -[c]Gamma, as wave-wide points.
+// The window at which the split form cuts s between the V and V2 items.  V2
+// pays 4 K doublings to 2^(4K) H and then a (64 - K)-window chain, so its
+// time is ~253 doublings plus the additions of windows K..63 whatever K; V's
+// chain grows with K.  32 (bit 128) leaves V2 with 32 additions V does not
+// wait for: a larger K moves additions off the critical item until the two
+// chains end together.
+#ifndef OURO_LAT_VWIN
+#define OURO_LAT_VWIN 32
+#endif
+static_assert(OURO_LAT_VWIN >= 8 && OURO_LAT_VWIN <= 60, "V / V2 split window");
+
+// (s >> 4K) plus the carry s's signed windows 0..K-1 hand to window K
+template <int K>
+OURO_FI void sc_high_from_window(uint32_t hh[8], const uint32_t s[8]) {
+  const uint32_t cin = (uint32_t)(sc_recode_carries<4, 64>(s) >> K) & 1u;
+  constexpr int kW = (4 * K) >> 5, kB = (4 * K) & 31;
+  uint64_t c = cin;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    uint32_t w = i + kW < 8 ? s[i + kW] >> kB : 0u;
+    if (kB != 0 && i + kW + 1 < 8) w |= s[i + kW + 1] << ((32 - kB) & 31);
+    c += w;
+    hh[i] = (uint32_t)c;
+    c >>= 32;
+  }
+}
+
+// V = [s]H - [c]Gamma over THREE waves: [s windows 0..K-1]H (the V item),
+// [s windows K..63](2^(4K) H) (the V2 item: H again, then 4K doublings;
+// K = OURO_LAT_VWIN) and -[c]Gamma (the Gamma item); the last of the three
+// adds them and encodes H and V.  Record per VRF (kLatVsplit + 4 kPwWords
+// which): H, the low and high parts, -[c]Gamma, as wave-wide points.
 template <class Tail>
 __device__ __forceinline__ void vrf_sh_split(Slot v, const uint32_t pk[8], const uint32_t pi[20],
                                              const Tail& alpha, bool high) {
@@ -926,13 +953,14 @@ __device__ __forceinline__ void vrf_sh_split(Slot v, const uint32_t pk[8], const
     Hw = pw_dbl(pw_dbl(pw_dbl(pw_from_p3(P, L), L), L), L);
   }
   lstamp(15);
+  constexpr int K = OURO_LAT_VWIN;
   if (!high) {
     st_pw(v, Hw);
   } else {
 #pragma unroll 1
-    for (int k = 0; k < 128; k++) Hw = pw_dbl(Hw, L);
+    for (int k = 0; k < 4 * K; k++) Hw = pw_dbl(Hw, L);
     uint32_t hh[8];
-    sc_high_half_with_carry(hh, s);
+    sc_high_from_window<K>(hh, s);
 #pragma unroll
     for (int k = 0; k < 8; k++) s[k] = hh[k];
   }
@@ -940,7 +968,8 @@ __device__ __forceinline__ void vrf_sh_split(Slot v, const uint32_t pk[8], const
   TabW tab;
   tab_build(tab, Hw, d2_wide(L), L);
   lstamp(17);
-  st_pw(v + (high ? 2 : 1) * kPwWords, pw_dsm<false, false>(tab, s, 32, tab, s, 0, s, nullptr, L));
+  st_pw(v + (high ? 2 : 1) * kPwWords,
+        pw_dsm<false, false>(tab, s, high ? 64 - K : K, tab, s, 0, s, nullptr, L));
   lstamp(18);
 }
 

@@ -23,6 +23,7 @@
 
 #include "oracle.h"
 #include "ouro_verify.h"
+#include "ouro_verify_debug.h"
 
 int crypto_vrf_ietfdraft03_verify(unsigned char *, const unsigned char *, const unsigned char *,
                                   const unsigned char *, unsigned long long);

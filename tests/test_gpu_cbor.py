@@ -234,3 +234,29 @@ def test_device_error_recomputes_on_the_host_path(gpu_lib, kats, small_chunks):
         assert "recomputed on the host path" in msg, msg
     finally:
         os.environ.pop("OURO_TEST_DEVICE_ERROR", None)
+
+
+@pytest.mark.gpu
+def test_c_callers(gpu_lib, kats, tmp_path):
+    """tests/c/cbor_callers.c: 8 pthreads call ouro_tpraos_verify_cbor and
+    ouro_integrity_verify_cbor through the C ABI on the golden cases (every
+    single-byte corruption and truncations), each result checked against the
+    pinned host slicer + oracle."""
+    import subprocess
+
+    from ouroboros_network_amd import header as H
+
+    exe = os.path.join(os.path.dirname(os.path.abspath(__file__)), "c", "build", "cbor_callers")
+    assert os.path.exists(exe), "build tests/c (make -C tests/c)"
+    raws, ea, la = _golden_cases(kats, stride=3)
+    v, be, bl, _en, st = _expect(raws, SPKP, ea, la)
+    ok, _ = H.verify_integrity_cbor(raws, SPKP, host=True)
+    buf, off, ln = H.raw_triplet(raws)
+    n = len(raws)
+    path = tmp_path / "cbor_input.bin"
+    with open(path, "wb") as f:
+        f.write(np.array([n, buf.size, SPKP], np.uint64).tobytes())
+        for a in (buf, off, ln, ea, la, st, v, be, bl, ok.astype(np.uint8)):
+            f.write(np.ascontiguousarray(a).tobytes())
+    r = subprocess.run([exe, str(path), "8", "3"], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and r.stdout.startswith("ok"), (r.stdout, r.stderr[-2000:])
