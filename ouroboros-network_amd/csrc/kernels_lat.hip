@@ -126,7 +126,7 @@ __device__ __noinline__ void hdr_core_wide(const ouro_tpraos_batch& b, size_t i,
         break;
       }
       if (fused && OURO_LAT_SPLIT) {  // [s windows 0..31]H; V2 and Gamma do the rest
-        vrf_sh_split(res + kLatVsplit + 4 * kPwWords * (int)leader, p, pi, alpha, false);
+        vrf_sh_split(res + kLatVsplit + 4 * kPwWords * (int)leader, res, p, pi, alpha, 0);
         flag = kFlagOk;
         break;
       }
@@ -187,7 +187,7 @@ __device__ __noinline__ void hdr_core_wide(const ouro_tpraos_batch& b, size_t i,
 // combinations, two Gamma betas) complete a header.  skip: the timing probe's mask (cores
 // 0..7; the doubling and V2 items follow their cores).
 static_assert(!(OURO_V_WHOLE && OURO_LAT_SPLIT), "OURO_V_WHOLE needs the two-wave form");
-constexpr int kFusedItems = OURO_LAT_SPLIT ? kLatCores + 6 : kLatCores + 2;
+constexpr int kFusedItems = OURO_LAT_SPLIT ? kLatCores + 6 + (OURO_LAT_V3 ? 2 : 0) : kLatCores + 2;
 [[maybe_unused]] constexpr uint32_t kHdrParties = OURO_LAT_SPLIT ? 8u : (uint32_t)kLatCores;
 // stamps (a timing probe, tools/lat_stamps.py: a build with
 // -DOURO_LAT_STAMPS=1, run with OURO_LAT_STAMPS set): header 0's items print
@@ -311,8 +311,10 @@ __device__ __noinline__ bool hdr_item_fused(const ouro_tpraos_batch& b, size_t i
     kstamp(4);
     if (lead) stg1(res.word(kResFlags + e), flag);
   } else if (OURO_LAT_SPLIT && item >= kLatCores + 4) {
-    // V2: [s windows 32..63](2^128 H), then the VRF's three-party arrival
-    const int which = item - (kLatCores + 4);
+    // V2 (items 12 / 13): [s windows K..](2^(4K) H); V3 (14 / 15, OURO_LAT_V3):
+    // the top windows; then the VRF's combination arrival
+    const int which = (item - (kLatCores + 4)) & 1;
+    const int part = item >= kLatCores + 6 ? 2 : 1;
     const bool skipped = (skip >> (kCoreVe + which)) & 1u;
     if (!skipped) {
       uint32_t p[8], pi[20];
@@ -320,9 +322,10 @@ __device__ __noinline__ bool hdr_item_fused(const ouro_tpraos_batch& b, size_t i
       ld_words(pi, (which ? b.leader_proof : b.eta_proof) + 80 * i, 5);
       SeedMsg alpha;
       lat_seed(alpha, b, i, which != 0, opts);
-      vrf_sh_split(res + kLatVsplit + 4 * kPwWords * which, p, pi, alpha, true);
+      vrf_sh_split(res + kLatVsplit + 4 * kPwWords * which, res + kLatV3 + kPwWords * which, p,
+                   pi, alpha, part);
     }
-    if (!arrive_last(res.word(kLatCtr + 1 + which), gen, 3)) {
+    if (!arrive_last(res.word(kLatCtr + 1 + which), gen, kVParts)) {
       stamp("half");
       return false;
     }
@@ -343,7 +346,7 @@ __device__ __noinline__ bool hdr_item_fused(const ouro_tpraos_batch& b, size_t i
       flag = vrf_gamma_part_wide(res + kLatVsplit + 4 * kPwWords * which + 3 * kPwWords, Gw, pi);
     }
     stamp("work");
-    if (arrive_last(res.word(kLatCtr + 1 + which), gen, 3)) {
+    if (arrive_last(res.word(kLatCtr + 1 + which), gen, kVParts)) {
       if (!(((skip >> (kCoreVe + which)) | skipped) & 1u)) vrf_split_combine_encode(res, which);
       stamp("comb");
       // the combination's own arrival (this item arrives again for beta below)
@@ -366,7 +369,7 @@ __device__ __noinline__ bool hdr_item_fused(const ouro_tpraos_batch& b, size_t i
     const bool vg = item == kCoreVe || item == kCoreVl || item == kCoreGe || item == kCoreGl;
     if (!OURO_V_WHOLE && vg) {
       const int which = (item == kCoreVl || item == kCoreGl) ? 1 : 0;
-      const bool last = arrive_last(res.word(kLatCtr + 1 + which), gen, OURO_LAT_SPLIT ? 3 : 2);
+      const bool last = arrive_last(res.word(kLatCtr + 1 + which), gen, OURO_LAT_SPLIT ? kVParts : 2u);
       const bool skipped = ((skip >> (kCoreVe + which)) | (skip >> (kCoreGe + which))) & 1u;
       if (OURO_LAT_SPLIT) {
         if (!last) {

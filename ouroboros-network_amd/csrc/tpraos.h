@@ -51,7 +51,14 @@ constexpr int kLatNonce = kLatEd + 2 * kEdWords;
 // -[c]Gamma (64 words each), combined by the last of three cores
 constexpr int kPwWords = 64;
 constexpr int kLatVsplit = kLatNonce + 16;            // VRF which at kLatVsplit + 4 kPwWords which
-constexpr int kLatResWords = kLatVsplit + 8 * kPwWords;  // 1,684 words (16-B multiple)
+// the four-wave V (wide_cores.h vrf_sh_split; A/B): the V3 item's part per VRF
+#ifndef OURO_LAT_V3
+#define OURO_LAT_V3 0
+#endif
+// parties of a VRF's combination in the fused split form: V, V2, Gamma (and V3)
+constexpr uint32_t kVParts = OURO_LAT_V3 ? 4u : 3u;
+constexpr int kLatV3 = kLatVsplit + 8 * kPwWords;     // VRF which at kLatV3 + kPwWords which
+constexpr int kLatResWords = kLatV3 + 2 * kPwWords;   // 1,812 words (16-B multiple)
 enum HdrCore { kCoreOcert = 0, kCoreKes, kCoreUe, kCoreUl, kCoreVe, kCoreVl, kHdrCores,
                // latency mode splits each V = [s]H - [c]Gamma over two lanes: the V
                // cores do [s]H (252-bit chain), these do -[c]Gamma (128-bit chain)

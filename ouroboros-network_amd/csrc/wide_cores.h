@@ -888,18 +888,27 @@ __device__ __forceinline__ bool eds_combine(Slot e) {
   return ldg1(e.word(kEsOk)) != 0 && pw_is_identity(Q);
 }
 
-// The window at which the split form cuts s between the V and V2 items.  V2
-// pays 4 K doublings to 2^(4K) H and then a (64 - K)-window chain, so its
-// time is ~253 doublings plus the additions of windows K..63 whatever K; V's
-// chain grows with K.  32 (bit 128) leaves V2 with 32 additions V does not
-// wait for: a larger K moves additions off the critical item until the two
-// chains end together.
+// The windows at which the split form cuts s between its V items.  V2 pays
+// 4 K doublings to 2^(4K) H before its chain over windows K..63, so its time
+// is ~253 doublings plus the additions of its windows whatever K, while V's
+// chain grows with K: K = 32 (bit 128, rounds 3--4) left V2 32 additions
+// that V did not wait for; 48 ends the two chains together (profiles/r05d).
+// OURO_LAT_V3 = 1 cuts once more, at K2: V2 then takes windows K..K2-1 and a
+// V3 item (H again, 4 K2 doublings) windows K2..63, which takes all but a few
+// additions off the item that does the ~253 doublings.
 #ifndef OURO_LAT_VWIN
-#define OURO_LAT_VWIN 32
+#define OURO_LAT_VWIN (OURO_LAT_V3 ? 49 : 48)
+#endif
+#ifndef OURO_LAT_VWIN2
+#define OURO_LAT_VWIN2 61
 #endif
 static_assert(OURO_LAT_VWIN >= 8 && OURO_LAT_VWIN <= 60, "V / V2 split window");
+static_assert(!OURO_LAT_V3 || (OURO_LAT_VWIN2 > OURO_LAT_VWIN && OURO_LAT_VWIN2 <= 63),
+              "V2 / V3 split window");
 
-// (s >> 4K) plus the carry s's signed windows 0..K-1 hand to window K
+// (s >> 4K) plus the carry s's signed windows 0..K-1 hand to window K: the
+// windows below K recoded from the whole s plus [that]·16^K are s exactly
+// (pw_dsm recodes its scalar whole and adds only the windows it is given)
 template <int K>
 OURO_FI void sc_high_from_window(uint32_t hh[8], const uint32_t s[8]) {
   const uint32_t cin = (uint32_t)(sc_recode_carries<4, 64>(s) >> K) & 1u;
@@ -915,14 +924,16 @@ OURO_FI void sc_high_from_window(uint32_t hh[8], const uint32_t s[8]) {
   }
 }
 
-// V = [s]H - [c]Gamma over THREE waves: [s windows 0..K-1]H (the V item),
-// [s windows K..63](2^(4K) H) (the V2 item: H again, then 4K doublings;
-// K = OURO_LAT_VWIN) and -[c]Gamma (the Gamma item); the last of the three
-// adds them and encodes H and V.  Record per VRF (kLatVsplit + 4 kPwWords
-// which): H, the low and high parts, -[c]Gamma, as wave-wide points.
+// V = [s]H - [c]Gamma over THREE waves: [s windows 0..K-1]H (the V item,
+// part 0), [s windows K..63](2^(4K) H) (the V2 item, part 1: H again, then 4K
+// doublings; K = OURO_LAT_VWIN) and -[c]Gamma (the Gamma item); the last of
+// the three adds them and encodes H and V.  With OURO_LAT_V3 part 1 stops at
+// window K2 and part 2 (the V3 item) does [(s >> 4K) windows K2-K..](2^(4 K2) H).
+// Record per VRF (kLatVsplit + 4 kPwWords which): H, the parts 0 and 1,
+// -[c]Gamma, as wave-wide points; part 2 at kLatV3 + kPwWords which.
 template <class Tail>
-__device__ __forceinline__ void vrf_sh_split(Slot v, const uint32_t pk[8], const uint32_t pi[20],
-                                             const Tail& alpha, bool high) {
+__device__ __forceinline__ void vrf_sh_split(Slot v, Slot v3, const uint32_t pk[8],
+                                             const uint32_t pi[20], const Tail& alpha, int part) {
   const Lanes L = lanes();
   uint32_t s_raw[8], s[8];
 #pragma unroll
@@ -953,35 +964,44 @@ __device__ __forceinline__ void vrf_sh_split(Slot v, const uint32_t pk[8], const
     Hw = pw_dbl(pw_dbl(pw_dbl(pw_from_p3(P, L), L), L), L);
   }
   lstamp(15);
-  constexpr int K = OURO_LAT_VWIN;
-  if (!high) {
+  constexpr int K = OURO_LAT_VWIN, K2 = OURO_LAT_V3 ? OURO_LAT_VWIN2 : 64;
+  int nw = K;
+  if (part == 0) {
     st_pw(v, Hw);
   } else {
+    const int dbl = 4 * (part == 1 ? K : K2);
 #pragma unroll 1
-    for (int k = 0; k < 4 * K; k++) Hw = pw_dbl(Hw, L);
+    for (int k = 0; k < dbl; k++) Hw = pw_dbl(Hw, L);
     uint32_t hh[8];
     sc_high_from_window<K>(hh, s);
+    if (OURO_LAT_V3 && part == 2) {
+      sc_high_from_window<(K2 - K) & 63>(s, hh);
+      nw = 64 - K2;
+    } else {
 #pragma unroll
-    for (int k = 0; k < 8; k++) s[k] = hh[k];
+      for (int k = 0; k < 8; k++) s[k] = hh[k];
+      nw = K2 - K;
+    }
   }
   lstamp(16);
   TabW tab;
   tab_build(tab, Hw, d2_wide(L), L);
   lstamp(17);
-  st_pw(v + (high ? 2 : 1) * kPwWords,
-        pw_dsm<false, false>(tab, s, high ? 64 - K : K, tab, s, 0, s, nullptr, L));
+  st_pw(part == 2 ? v3 : v + (part + 1) * kPwWords,
+        pw_dsm<false, false>(tab, s, nw, tab, s, 0, s, nullptr, L));
   lstamp(18);
 }
 
-// the last of a VRF's V, V2 and Gamma items: V = the three parts, H and V
+// the last of a VRF's V, V2 (V3) and Gamma items: V = the parts, H and V
 // encoded with one inversion
 __device__ __forceinline__ void vrf_split_combine_encode(Slot res, int which) {
   const Lanes L = lanes();
   const Slot v = res + kLatVsplit + 4 * kPwWords * which;
   const int32_t d2 = d2_wide(L);
   lstamp(4);
-  const pw Vw = pw_add_p3(pw_add_p3(ld_pw(v + kPwWords), ld_pw(v + 2 * kPwWords), d2, L),
-                          ld_pw(v + 3 * kPwWords), d2, L);
+  pw Vw = pw_add_p3(pw_add_p3(ld_pw(v + kPwWords), ld_pw(v + 2 * kPwWords), d2, L),
+                    ld_pw(v + 3 * kPwWords), d2, L);
+  if (OURO_LAT_V3) Vw = pw_add_p3(Vw, ld_pw(res + kLatV3 + kPwWords * which), d2, L);
   lstamp(5);
   uint32_t Henc[8], Venc[8];
   encode2_wide(Henc, Venc, ld_pw(v), Vw);

@@ -19,10 +19,17 @@
 // time bound for 255-bit operands is 724, and once g = 0 a batch leaves f, d,
 // e as they are.  The result is the unique inverse (0 -> 0), so it equals
 // z^(p-2) bit for bit; the latency parity tests compare the encodings with the
-// oracle.
+// oracle.  Since round 5 the loop ends at the first batch after which g is
+// zero (OURO_INV_EARLY): the inputs are public points, so a data-dependent
+// batch count leaks nothing.
 #pragma once
 #include "modinv.h"
 #include "wide.h"
+
+// leave the batch loop once g is zero (1) or always run all 25 batches (0, A/B)
+#ifndef OURO_INV_EARLY
+#define OURO_INV_EARLY 1
+#endif
 
 namespace ouro {
 
@@ -48,7 +55,9 @@ __device__ __forceinline__ int32_t sgcd_div30_rows(int64_t c, bool top) {
   return r1lo + row_from_prev(r1hi);
 }
 
-// z^-1 mod p (0 for z = 0); z the same in every lane
+// z^-1 mod p (0 for z = 0); z the same in every lane.  kEarly: leave the
+// batch loop once g is zero (OURO_INV_EARLY; both forms for the timing probe)
+template <bool kEarly = (OURO_INV_EARLY != 0)>
 __device__ __noinline__ fe fe_invert_wave(fe z) {
   const int k = (int)(threadIdx.x & 15u);  // limb index: the four rows alike
   uint32_t zw[8];
@@ -86,6 +95,23 @@ __device__ __noinline__ fe fe_invert_wave(fe z) {
     g = sgcd_div30_rows(cg, top);
     d = sgcd_div30_rows(cd, top);
     e = sgcd_div30_rows(ce, top);
+    // g = 0: done (17--19 batches for random operands, against the 25 of the
+    // bound).  Its limbs need not all be 0 (the carry rounds leave e.g.
+    // (0, 2^30, -1, ...)), but its low limb is 0 mod 2^30, which a nonzero g
+    // shows with probability 2^-30: only then is the value checked exactly,
+    // wave-uniformly from the row's limbs.
+    if (kEarly && ((uint32_t)__builtin_amdgcn_readfirstlane(g) & (uint32_t)kM30) == 0) {
+      int64_t c = 0;
+      bool zero = true;
+#pragma unroll
+      for (int i = 0; i < kTopLimb; i++) {
+        c += (int64_t)__builtin_amdgcn_readlane(g, i);
+        zero = zero && (c & kM30) == 0;
+        c >>= 30;
+      }
+      c += (int64_t)__builtin_amdgcn_readlane(g, kTopLimb);
+      if (zero && c == 0) break;
+    }
   }
   // f = +-1 (p for z = 0, where d = 0): its low limb says which
   const bool fneg = (uint32_t)__builtin_amdgcn_readfirstlane(f) == (uint32_t)kM30;

@@ -4,6 +4,8 @@
 // library does not contain this file.
 #include <hip/hip_runtime.h>
 
+#include <vector>
+
 #include "verify.h"
 #include "wide_cores.h"
 
@@ -206,9 +208,56 @@ __global__ void __launch_bounds__(WT_BOUNDS) k_wide_selftest(uint64_t seed, int3
 #endif
 }
 
+// timing probe of the wave inversion (wide_inv.h): each wave inverts a
+// chain of `iters` elements (z <- 1 / z + 1) with or without the early exit;
+// out[2 wave] = s_memrealtime ticks (100 MHz) for the chain, out[2 wave + 1]
+// = the last result's low word (keeps the chain live)
+template <bool kEarly>
+__global__ void __launch_bounds__(64) k_inv_timing(uint64_t seed, int iters,
+                                                  unsigned long long* out) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  uint32_t w[8];
+  rand_words(w, seed ^ ((uint64_t)blockIdx.x << 20), 7);
+  w[7] &= 0x7fffffffu;
+  fe z = fe_from_words(w);
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+#pragma unroll 1
+  for (int k = 0; k < iters; k++) z = fe_carry(fe_add(fe_invert_wave<kEarly>(z), fe_one()));
+  const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
+  uint32_t e[8];
+  fe_to_words(e, z);
+  if (threadIdx.x == 0) {
+    out[2 * blockIdx.x] = t1 - t0;
+    out[2 * blockIdx.x + 1] = e[0];
+  }
+#endif
+}
+
 }  // namespace
 
 extern "C" {
+// us per inversion averaged over `waves` waves x `iters` inversions, with
+// (early = 1) or without the early exit; -1 on a HIP error
+double ouro_wide_invert_us(int waves, int iters, int early, uint64_t seed) {
+  unsigned long long* d = nullptr;
+  if (hipMalloc(&d, sizeof(unsigned long long) * 2 * waves) != hipSuccess) return -1;
+  if (early)
+    hipLaunchKernelGGL(k_inv_timing<true>, dim3(waves), dim3(64), 0, 0, seed, iters, d);
+  else
+    hipLaunchKernelGGL(k_inv_timing<false>, dim3(waves), dim3(64), 0, 0, seed, iters, d);
+  std::vector<unsigned long long> h(2 * (size_t)waves);
+  double r = -1;
+  if (hipDeviceSynchronize() == hipSuccess &&
+      hipMemcpy(h.data(), d, sizeof(unsigned long long) * 2 * waves, hipMemcpyDeviceToHost) ==
+          hipSuccess) {
+    double t = 0;
+    for (int i = 0; i < waves; i++) t += (double)h[2 * i];
+    r = t / waves / iters / 100.0;
+  }
+  (void)hipFree(d);
+  return r;
+}
+
 // waves cases from seed; out: waves * 10 int32 (1 = pass), dbg: 24 int32.
 // Returns 0, or -2 on a HIP error.
 int ouro_wide_selftest(int waves, uint64_t seed, int32_t* out, int32_t* dbg) {

@@ -145,6 +145,41 @@ def test_ed25519_batch_host_corrupted_and_ragged(impl):
     assert 0 < got.sum() < n
 
 
+_POOL_CHILD = r"""
+import sys
+sys.path[:0] = [%r, %r]
+import numpy as np
+import oracle_ffi as O
+from ouroboros_network_amd import dsign
+rng = np.random.default_rng(11)
+vks, sigs, msgs, want = [], [], [], []
+for i in range(150):
+    pk, sk = O.ed25519_keypair(rng.bytes(32))
+    m = rng.bytes(int(rng.integers(0, 200)))
+    s = bytearray(O.ed25519_sign(sk, m))
+    if i %% 4 == 2:
+        s[int(rng.integers(0, 64))] ^= 1
+    vks.append(pk); sigs.append(bytes(s)); msgs.append(m)
+    want.append(O.ed25519_verify(bytes(s), m, pk))
+got = dsign.verify_batch(vks, msgs, sigs, host=True)
+assert (got == np.array(want)).all() and 0 < got.sum() < len(want)
+print("ok", int(got.sum()))
+"""
+
+
+@pytest.mark.parametrize("threads", ["1", "3"])
+def test_host_pool_serial_and_narrow(threads):
+    """the host path's task pool (csrc/task_pool.cpp)
+    with no worker threads at all (OURO_HOST_THREADS=1: the calling thread
+    runs every task, as when no worker can be spawned) and with two workers
+    gives the oracle's verdicts."""
+    env = dict(os.environ, OURO_HOST_THREADS=threads)
+    r = subprocess.run(["python3", "-c", _POOL_CHILD % (ROOT, os.path.join(ROOT, "tests"))],
+                       env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert r.stdout.startswith("ok")
+
+
 def test_byron_single_and_batch(lib, kats):
     from ouroboros_network_amd import dsign  # noqa: F401  (loads the library)
 

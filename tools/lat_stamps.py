@@ -8,7 +8,7 @@ runs a 64-header plan R times on that library (OURO_VERIFY_LIB), reads the
 stamps after each launch (ouro_debug_lat_stamps) and prints, per item and
 tag, the median time in us after the earliest start of the launch.
 Items: 0/8/10 OCERT points/scalars/doubling, 1/9/11 KES, 2/3 U eta/leader,
-4/5 V, 6/7 Gamma, 12/13 V2.  Tags: 0 start, 1 own part done, 2/3 chain X/Y
+4/5 V, 6/7 Gamma, 12/13 V2, 14/15 V3 (OURO_LAT_V3 builds).  Tags: 0 start, 1 own part done, 2/3 chain X/Y
 done, 4..7 VRF combination (start, adds, inverted, encoded), 8 end, 9/10/11
 tail (start, challenges, end), 12..18 V/V2 phases (hash, exp start, exp end,
 H, H128, table, chain).
@@ -24,7 +24,7 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 ITEMS = {0: "OCERT P", 8: "OCERT S", 10: "OCERT D", 1: "KES P", 9: "KES S", 11: "KES D",
          2: "U eta", 3: "U leader", 4: "V eta", 5: "V leader", 6: "Gamma eta",
-         7: "Gamma leader", 12: "V2 eta", 13: "V2 leader"}
+         7: "Gamma leader", 12: "V2 eta", 13: "V2 leader", 14: "V3 eta", 15: "V3 leader"}
 TAGS = {0: "start", 1: "part", 2: "chainX", 3: "chainY", 4: "comb0", 5: "combAdd",
         6: "combInv", 7: "combEnc", 8: "end", 9: "tail0", 10: "tailChal", 11: "tailEnd",
         12: "hash", 13: "exp0", 14: "exp1", 15: "H", 16: "H128", 17: "table", 18: "chain"}
