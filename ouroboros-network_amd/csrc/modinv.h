@@ -47,11 +47,24 @@ OURO_FI uint32_t sgcd_inv32(uint32_t f) {
 
 struct SgcdMat { int32_t u, v, q, r; };
 
+// -1 / f mod 2^kBits for an odd f: 5 correct bits, Newton steps to kBits
+template <int kBits>
+OURO_FI uint32_t sgcd_neg_inv(uint32_t f) {
+  if (kBits > 10) return 0u - sgcd_inv32(f);
+  uint32_t x = (3u * f) ^ 2u;
+  x *= 2u - f * x;  // 10 bits
+  return 0u - x;
+}
+
 // 30 divsteps on the low words of f (odd) and g; eta = -delta.  t maps
-// (f, g) to (u f + v g, q f + r g) / 2^30.
+// (f, g) to (u f + v g, q f + r g) / 2^30.  kCap: at most that many low bits
+// of g cancelled per step (<= 10: a one-Newton-step inverse of f, which is
+// recomputed at nearly every step -- ~133 swaps in ~137 steps per inversion
+// -- instead of three; the step count stays ~137 for random operands)
+template <int kCap = 30>
 OURO_FI int32_t sgcd_divsteps30(int32_t eta, uint32_t f, uint32_t g, SgcdMat& t) {
   uint32_t u = 1, v = 0, q = 0, r = 1;
-  uint32_t nfi = 0u - sgcd_inv32(f);  // -1 / f mod 2^32, recomputed when f changes
+  uint32_t nfi = sgcd_neg_inv<kCap>(f);  // -1 / f mod 2^kCap, recomputed when f changes
   int i = 30;
 #pragma unroll 1
   for (;;) {
@@ -70,10 +83,11 @@ OURO_FI int32_t sgcd_divsteps30(int32_t eta, uint32_t f, uint32_t g, SgcdMat& t)
       tmp = f; f = g; g = 0u - tmp;
       tmp = u; u = q; q = 0u - tmp;
       tmp = v; v = r; r = 0u - tmp;
-      nfi = 0u - sgcd_inv32(f);
+      nfi = sgcd_neg_inv<kCap>(f);
     }
     // then g <- (g + w f) / 2^k steps: cancel limit low bits of g at once
-    const int limit = (eta + 1) > i ? i : (eta + 1);
+    int limit = (eta + 1) > i ? i : (eta + 1);
+    if (kCap < 30) limit = limit > kCap ? kCap : limit;
     const uint32_t m = 0xffffffffu >> (32 - limit);
     const uint32_t w = (g * nfi) & m;
     g += f * w;
@@ -149,7 +163,8 @@ OURO_FI void sgcd_add_p(int32_t d[9], int32_t sign) {  // d += p if sign (0 / -1
   sgcd_propagate(d);
 }
 
-// z^-1 mod p (0 for z = 0), variable time
+// z^-1 mod p (0 for z = 0), variable time (kCap: sgcd_divsteps30)
+template <int kCap = 30>
 OURO_HD inline fe fe_invert_vartime(const fe& z) {
   uint32_t zw[8];
   fe_to_words(zw, z);
@@ -170,7 +185,7 @@ OURO_HD inline fe fe_invert_vartime(const fe& z) {
 #pragma unroll 1
   for (int it = 0; it < 32; it++) {
     SgcdMat t;
-    eta = sgcd_divsteps30(eta, (uint32_t)f[0], (uint32_t)g[0], t);
+    eta = sgcd_divsteps30<kCap>(eta, (uint32_t)f[0], (uint32_t)g[0], t);
     sgcd_update_de(d, e, t);
     sgcd_update_fg(f, g, t);
     int32_t nz = 0;

@@ -30,6 +30,11 @@
 #ifndef OURO_INV_EARLY
 #define OURO_INV_EARLY 1
 #endif
+// bits of g cancelled per divstep step at most (modinv.h sgcd_divsteps30): 10
+// needs a one-Newton-step inverse of f at each swap; 30 = three steps (A/B)
+#ifndef OURO_INV_CAP
+#define OURO_INV_CAP 10
+#endif
 
 namespace ouro {
 
@@ -81,7 +86,7 @@ __device__ __noinline__ fe fe_invert_wave(fe z) {
     const uint32_t d0 = (uint32_t)__builtin_amdgcn_readfirstlane(d);
     const uint32_t e0 = (uint32_t)__builtin_amdgcn_readfirstlane(e);
     SgcdMat t;
-    eta = sgcd_divsteps30(eta, f0, g0, t);
+    eta = sgcd_divsteps30<OURO_INV_CAP>(eta, f0, g0, t);
     // the multiples of p clearing the low 30 bits of t (d, e), in [0, 2^30)
     const uint32_t md = (0u - ((uint32_t)t.u * d0 + (uint32_t)t.v * e0) * sgcd_p_inv30()) &
                         (uint32_t)kM30;

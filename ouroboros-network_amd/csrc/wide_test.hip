@@ -233,9 +233,62 @@ __global__ void __launch_bounds__(64) k_inv_timing(uint64_t seed, int iters,
 #endif
 }
 
+// the same chain with only the batches' 30-divstep matrices (modinv.h
+// sgcd_divsteps30 on the low words, f / g advanced by the matrix mod 2^32):
+// what the wave inversion's scalar part costs without the limb updates
+template <int kCap>
+__global__ void __launch_bounds__(64) k_divsteps_timing(uint64_t seed, int iters,
+                                                       unsigned long long* out) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  uint32_t w[8];
+  rand_words(w, seed ^ ((uint64_t)blockIdx.x << 20), 9);
+  uint32_t f = 0x3fffffedu, g = (uint32_t)__builtin_amdgcn_readfirstlane(w[0]);
+  uint32_t acc = 0;
+  int32_t eta = -1;
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+#pragma unroll 1
+  for (int k = 0; k < iters * 18; k++) {
+    SgcdMat t;
+    eta = sgcd_divsteps30<kCap>(eta, f, g, t);
+    const uint32_t nf = (uint32_t)t.u * f + (uint32_t)t.v * g;
+    const uint32_t ng = (uint32_t)t.q * f + (uint32_t)t.r * g;
+    f = (nf >> 30 | 1u) ^ (uint32_t)k;  // keep f odd, vary the words
+    f |= 1u;
+    g = ng ^ (uint32_t)(k * 0x9e3779b9u);
+    acc += (uint32_t)t.u ^ (uint32_t)t.r;
+    if (eta > 100 || eta < -100) eta = -1;
+  }
+  const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
+  if (threadIdx.x == 0) {
+    out[2 * blockIdx.x] = t1 - t0;
+    out[2 * blockIdx.x + 1] = acc;
+  }
+#endif
+}
+
 }  // namespace
 
 extern "C" {
+// us per 18 batches of divsteps matrices (one inversion's worth), kCap 30 or 10
+double ouro_wide_divsteps_us(int waves, int iters, int cap10, uint64_t seed) {
+  unsigned long long* d = nullptr;
+  if (hipMalloc(&d, sizeof(unsigned long long) * 2 * waves) != hipSuccess) return -1;
+  if (cap10)
+    hipLaunchKernelGGL(k_divsteps_timing<10>, dim3(waves), dim3(64), 0, 0, seed, iters, d);
+  else
+    hipLaunchKernelGGL(k_divsteps_timing<30>, dim3(waves), dim3(64), 0, 0, seed, iters, d);
+  std::vector<unsigned long long> h(2 * (size_t)waves);
+  double r = -1;
+  if (hipDeviceSynchronize() == hipSuccess &&
+      hipMemcpy(h.data(), d, sizeof(unsigned long long) * 2 * waves, hipMemcpyDeviceToHost) ==
+          hipSuccess) {
+    double t = 0;
+    for (int i = 0; i < waves; i++) t += (double)h[2 * i];
+    r = t / waves / iters / 100.0;
+  }
+  (void)hipFree(d);
+  return r;
+}
 // us per inversion averaged over `waves` waves x `iters` inversions, with
 // (early = 1) or without the early exit; -1 on a HIP error
 double ouro_wide_invert_us(int waves, int iters, int early, uint64_t seed) {

@@ -1,6 +1,7 @@
 """Timing probe of the wave inversion (csrc/wide_inv.h) on the GPU: us per
-inversion with and without the early exit, one wave per SIMD
-(lib/libouro_wide_test.so ouro_wide_invert_us).
+inversion with and without the early exit, one wave per SIMD, and the cost of
+one inversion's 18 batches of divstep matrices alone (lib/libouro_wide_test.so
+ouro_wide_invert_us, ouro_wide_divsteps_us).
     python tools/inv_timing.py [waves] [iters]"""
 import ctypes
 import json
@@ -21,7 +22,16 @@ def main():
         for early in (1, 0):
             us = lib.ouro_wide_invert_us(waves, iters, early, 1234 + rep)
             res.setdefault("early" if early else "all_25_batches", []).append(round(us, 3))
-    print(json.dumps({"waves": waves, "iters": iters, "us_per_inversion": res}))
+    lib.ouro_wide_divsteps_us.restype = ctypes.c_double
+    lib.ouro_wide_divsteps_us.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                          ctypes.c_uint64]
+    ds = {}
+    for rep in range(3):
+        for cap10 in (1, 0):
+            us = lib.ouro_wide_divsteps_us(waves, iters, cap10, 99 + rep)
+            ds.setdefault("cap10" if cap10 else "cap30", []).append(round(us, 3))
+    print(json.dumps({"waves": waves, "iters": iters, "us_per_inversion": res,
+                      "us_per_18_divstep_matrices": ds}))
 
 
 if __name__ == "__main__":
