@@ -316,22 +316,42 @@ __device__ __noinline__ bool hdr_item_fused(const ouro_tpraos_batch& b, size_t i
     const int which = (item - (kLatCores + 4)) & 1;
     const int part = item >= kLatCores + 6 ? 2 : 1;
     const bool skipped = (skip >> (kCoreVe + which)) & 1u;
+    const bool none = ((skip >> (kCoreVe + which)) | (skip >> (kCoreGe + which))) & 1u;
+    int32_t* vctr = res.word(kLatCtr + 1 + which);
+    pw mine{0, 0, 0, 0};
     if (!skipped) {
       uint32_t p[8], pi[20];
       ld_words(p, b.vrf_vk + 32 * i, 2);
       ld_words(pi, (which ? b.leader_proof : b.eta_proof) + 80 * i, 5);
       SeedMsg alpha;
       lat_seed(alpha, b, i, which != 0, opts);
-      vrf_sh_split(res + kLatVsplit + 4 * kPwWords * which, res + kLatV3 + kPwWords * which, p,
-                   pi, alpha, part);
+      mine = vrf_sh_split(res + kLatVsplit + 4 * kPwWords * which, res + kLatV3 + kPwWords * which,
+                          p, pi, alpha, part, /*store=*/false);
     }
-    if (!arrive_last(res.word(kLatCtr + 1 + which), gen, kVParts)) {
-      stamp("half");
-      return false;
+    // the usual last party: V and Gamma already arrived -> combine with the
+    // part still in registers (OURO_LAST_PEEK); else publish it and arrive
+    const bool v2_last = part == 1 && !OURO_LAT_V3 && others_arrived(vctr, gen, kVParts);
+    if (!v2_last) {
+      if (!skipped)
+        st_pw(part == 2 ? res + kLatV3 + kPwWords * which
+                        : res + kLatVsplit + 4 * kPwWords * which + 2 * kPwWords,
+              mine);
+      if (!arrive_last(vctr, gen, kVParts)) {
+        stamp("half");
+        return false;
+      }
     }
-    if (!(((skip >> (kCoreVe + which)) | (skip >> (kCoreGe + which))) & 1u))
-      vrf_split_combine_encode(res, which);
+    if (!none) vrf_split_combine_encode(res, which, v2_last ? &mine : nullptr);
     stamp("comb");
+    // the header's last party likewise runs the tail without arriving
+    if (others_arrived(res.word(kLatCtr), gen, kHdrParties)) {
+      // lane 0's encodings (vrf_split_combine_encode) to the wave's other lanes
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+      hdr_tail_wide(b, i, opts, res, verdict, beta_eta, beta_leader);
+      stamp("tail");
+      return true;
+    }
   } else if (OURO_LAT_SPLIT && (item == kCoreGe || item == kCoreGl)) {
     // Gamma: -[c]Gamma first (the VRF's three-party combination waits for
     // it), then [8]Gamma, beta and the nonce candidates (only the tail reads

@@ -61,11 +61,49 @@ OURO_FI uint32_t sgcd_neg_inv(uint32_t f) {
 // of g cancelled per step (<= 10: a one-Newton-step inverse of f, which is
 // recomputed at nearly every step -- ~133 swaps in ~137 steps per inversion
 // -- instead of three; the step count stays ~137 for random operands)
-template <int kCap = 30>
+// kSel: the swap as selects and the inverse recomputed at every step, so a
+// step has no branch but the loop's own (the wave inversion runs this on the
+// scalar unit, where each taken branch costs an instruction refetch)
+template <int kCap = 30, bool kSel = false>
 OURO_FI int32_t sgcd_divsteps30(int32_t eta, uint32_t f, uint32_t g, SgcdMat& t) {
   uint32_t u = 1, v = 0, q = 0, r = 1;
   uint32_t nfi = sgcd_neg_inv<kCap>(f);  // -1 / f mod 2^kCap, recomputed when f changes
   int i = 30;
+  if (kSel) {
+#pragma unroll 1
+    for (;;) {
+      const int zeros = __builtin_ctz(g | (0xffffffffu << i));
+      g >>= zeros;
+      u <<= zeros;
+      v <<= zeros;
+      eta -= zeros;
+      i -= zeros;
+      if (i == 0) break;
+      const bool sw = eta < 0;
+      const uint32_t f1 = sw ? g : f, g1 = sw ? 0u - f : g;
+      const uint32_t u1 = sw ? q : u, q1 = sw ? 0u - u : q;
+      const uint32_t v1 = sw ? r : v, r1 = sw ? 0u - v : r;
+      eta = sw ? -eta : eta;
+      f = f1;
+      g = g1;
+      u = u1;
+      q = q1;
+      v = v1;
+      r = r1;
+      const uint32_t ni = sgcd_neg_inv<kCap>(f);
+      int limit = (eta + 1) > i ? i : (eta + 1);
+      if (kCap < 30) limit = limit > kCap ? kCap : limit;
+      const uint32_t w = (g * ni) & (0xffffffffu >> (32 - limit));
+      g += f * w;
+      q += u * w;
+      r += v * w;
+    }
+    t.u = (int32_t)u;
+    t.v = (int32_t)v;
+    t.q = (int32_t)q;
+    t.r = (int32_t)r;
+    return eta;
+  }
 #pragma unroll 1
   for (;;) {
     // halvings of an even g, at most up to the batch end (sentinel bits)
@@ -164,7 +202,7 @@ OURO_FI void sgcd_add_p(int32_t d[9], int32_t sign) {  // d += p if sign (0 / -1
 }
 
 // z^-1 mod p (0 for z = 0), variable time (kCap: sgcd_divsteps30)
-template <int kCap = 30>
+template <int kCap = 30, bool kSel = false>
 OURO_HD inline fe fe_invert_vartime(const fe& z) {
   uint32_t zw[8];
   fe_to_words(zw, z);
@@ -185,7 +223,7 @@ OURO_HD inline fe fe_invert_vartime(const fe& z) {
 #pragma unroll 1
   for (int it = 0; it < 32; it++) {
     SgcdMat t;
-    eta = sgcd_divsteps30<kCap>(eta, (uint32_t)f[0], (uint32_t)g[0], t);
+    eta = sgcd_divsteps30<kCap, kSel>(eta, (uint32_t)f[0], (uint32_t)g[0], t);
     sgcd_update_de(d, e, t);
     sgcd_update_fg(f, g, t);
     int32_t nz = 0;

@@ -626,6 +626,27 @@ __device__ __forceinline__ bool arrive_last(int32_t* ctr, uint32_t gen,
   return true;
 }
 
+// Whether every other party of a `parties` counter has arrived in this
+// launch (then acquired): the caller is the last without arriving, so it
+// need not publish what it holds in registers -- no release of its own
+// stores, no count (the counter is tagged, so the next launch starts it
+// afresh).  A false answer changes nothing: the caller publishes and arrives.
+// (A/B switch OURO_LAST_PEEK: 0 = always publish and arrive)
+#ifndef OURO_LAST_PEEK
+#define OURO_LAST_PEEK 1
+#endif
+__device__ __forceinline__ bool others_arrived(int32_t* ctr, uint32_t gen, uint32_t parties) {
+  if (!OURO_LAST_PEEK) return false;
+  uint32_t seen = 0;
+  if ((threadIdx.x & 63u) == 0)
+    seen = __hip_atomic_load(reinterpret_cast<unsigned int*>(ctr), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+  seen = (uint32_t)__builtin_amdgcn_readlane((int)seen, 0);
+  if (seen != (((gen & 0x0fffffffu) << 4) | (parties - 1u))) return false;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  return true;
+}
+
 // ---- fused mode: an Ed25519 check over two waves ------------------------------
 // The points item (encoding checks, both decodes: one exponentiation time) and
 // the scalars item (SHA-512 of R || A || M -- five blocks for a KES body --,
@@ -932,8 +953,9 @@ OURO_FI void sc_high_from_window(uint32_t hh[8], const uint32_t s[8]) {
 // Record per VRF (kLatVsplit + 4 kPwWords which): H, the parts 0 and 1,
 // -[c]Gamma, as wave-wide points; part 2 at kLatV3 + kPwWords which.
 template <class Tail>
-__device__ __forceinline__ void vrf_sh_split(Slot v, Slot v3, const uint32_t pk[8],
-                                             const uint32_t pi[20], const Tail& alpha, int part) {
+__device__ __forceinline__ pw vrf_sh_split(Slot v, Slot v3, const uint32_t pk[8],
+                                           const uint32_t pi[20], const Tail& alpha, int part,
+                                           bool store = true) {
   const Lanes L = lanes();
   uint32_t s_raw[8], s[8];
 #pragma unroll
@@ -987,19 +1009,23 @@ __device__ __forceinline__ void vrf_sh_split(Slot v, Slot v3, const uint32_t pk[
   TabW tab;
   tab_build(tab, Hw, d2_wide(L), L);
   lstamp(17);
-  st_pw(part == 2 ? v3 : v + (part + 1) * kPwWords,
-        pw_dsm<false, false>(tab, s, nw, tab, s, 0, s, nullptr, L));
+  const pw R = pw_dsm<false, false>(tab, s, nw, tab, s, 0, s, nullptr, L);
+  if (store) st_pw(part == 2 ? v3 : v + (part + 1) * kPwWords, R);
   lstamp(18);
+  return R;
 }
 
 // the last of a VRF's V, V2 (V3) and Gamma items: V = the parts, H and V
 // encoded with one inversion
-__device__ __forceinline__ void vrf_split_combine_encode(Slot res, int which) {
+// (hi: the V2 part in registers when the V2 item combines without having
+// stored it, else read from the record)
+__device__ __forceinline__ void vrf_split_combine_encode(Slot res, int which,
+                                                         const pw* hi = nullptr) {
   const Lanes L = lanes();
   const Slot v = res + kLatVsplit + 4 * kPwWords * which;
   const int32_t d2 = d2_wide(L);
   lstamp(4);
-  pw Vw = pw_add_p3(pw_add_p3(ld_pw(v + kPwWords), ld_pw(v + 2 * kPwWords), d2, L),
+  pw Vw = pw_add_p3(pw_add_p3(ld_pw(v + kPwWords), hi ? *hi : ld_pw(v + 2 * kPwWords), d2, L),
                     ld_pw(v + 3 * kPwWords), d2, L);
   if (OURO_LAT_V3) Vw = pw_add_p3(Vw, ld_pw(res + kLatV3 + kPwWords * which), d2, L);
   lstamp(5);

@@ -30,13 +30,69 @@
 #ifndef OURO_INV_EARLY
 #define OURO_INV_EARLY 1
 #endif
-// bits of g cancelled per divstep step at most (modinv.h sgcd_divsteps30): 10
-// needs a one-Newton-step inverse of f at each swap; 30 = three steps (A/B)
+// bits of g cancelled per divstep step at most (modinv.h sgcd_divsteps30): 30
+// (three Newton steps per inverse of f) or 10 (one step; A/B: no faster,
+// profiles/r05j/inv_timing.json)
 #ifndef OURO_INV_CAP
-#define OURO_INV_CAP 10
+#define OURO_INV_CAP 30
+#endif
+// the divstep steps branch-free (modinv.h sgcd_divsteps30 kSel; A/B: the
+// same time, profiles/r05j/inv_timing.json)
+#ifndef OURO_INV_SEL
+#define OURO_INV_SEL 0
 #endif
 
 namespace ouro {
+
+// modinv.h sgcd_divsteps30 with its state in vector registers: the same
+// steps (the swap as selects), issued by the VALU instead of the scalar unit,
+// whose dependent instructions are the slower of the two (the 18 batches of an
+// inversion's scalar loop take ~15 of its ~19 us, whatever the loop's
+// instruction count: profiles/r05j/inv_timing.json).  Every lane computes the
+// same; the loop's exit test reads lane 0.  A/B switch OURO_INV_VEC.
+template <int kCap>
+__device__ __forceinline__ int32_t sgcd_divsteps30_vec(int32_t eta, uint32_t f, uint32_t g,
+                                                       SgcdMat& t) {
+  uint32_t u = 1, v = 0, q = 0, r = 1;
+  int32_t i = 30;
+  asm volatile("" : "+v"(f), "+v"(g), "+v"(eta), "+v"(i), "+v"(u), "+v"(r));
+#pragma unroll 1
+  for (;;) {
+    const uint32_t zeros = (uint32_t)__builtin_ctz(g | (0xffffffffu << i));
+    g >>= zeros;
+    u <<= zeros;
+    v <<= zeros;
+    eta -= (int32_t)zeros;
+    i -= (int32_t)zeros;
+    if (__builtin_amdgcn_readfirstlane(i) == 0) break;
+    const bool sw = eta < 0;
+    const uint32_t f1 = sw ? g : f, g1 = sw ? 0u - f : g;
+    const uint32_t u1 = sw ? q : u, q1 = sw ? 0u - u : q;
+    const uint32_t v1 = sw ? r : v, r1 = sw ? 0u - v : r;
+    eta = sw ? -eta : eta;
+    f = f1;
+    g = g1;
+    u = u1;
+    q = q1;
+    v = v1;
+    r = r1;
+    const uint32_t ni = sgcd_neg_inv<kCap>(f);
+    int32_t limit = (eta + 1) > i ? i : (eta + 1);
+    if (kCap < 30) limit = limit > kCap ? kCap : limit;
+    const uint32_t w = (g * ni) & (0xffffffffu >> (32 - limit));
+    g += f * w;
+    q += u * w;
+    r += v * w;
+  }
+  t.u = __builtin_amdgcn_readfirstlane((int32_t)u);
+  t.v = __builtin_amdgcn_readfirstlane((int32_t)v);
+  t.q = __builtin_amdgcn_readfirstlane((int32_t)q);
+  t.r = __builtin_amdgcn_readfirstlane((int32_t)r);
+  return __builtin_amdgcn_readfirstlane(eta);
+}
+#ifndef OURO_INV_VEC
+#define OURO_INV_VEC 0
+#endif
 
 // lane j <- lane j + 1 / lane j - 1 of the same row (0 past the row's end)
 __device__ __forceinline__ int32_t row_from_next(int32_t x) {
@@ -62,7 +118,8 @@ __device__ __forceinline__ int32_t sgcd_div30_rows(int64_t c, bool top) {
 
 // z^-1 mod p (0 for z = 0); z the same in every lane.  kEarly: leave the
 // batch loop once g is zero (OURO_INV_EARLY; both forms for the timing probe)
-template <bool kEarly = (OURO_INV_EARLY != 0)>
+template <bool kEarly = (OURO_INV_EARLY != 0), int kCap = OURO_INV_CAP,
+          bool kSel = (OURO_INV_SEL != 0), bool kVec = (OURO_INV_VEC != 0)>
 __device__ __noinline__ fe fe_invert_wave(fe z) {
   const int k = (int)(threadIdx.x & 15u);  // limb index: the four rows alike
   uint32_t zw[8];
@@ -86,7 +143,8 @@ __device__ __noinline__ fe fe_invert_wave(fe z) {
     const uint32_t d0 = (uint32_t)__builtin_amdgcn_readfirstlane(d);
     const uint32_t e0 = (uint32_t)__builtin_amdgcn_readfirstlane(e);
     SgcdMat t;
-    eta = sgcd_divsteps30<OURO_INV_CAP>(eta, f0, g0, t);
+    if (kVec) eta = sgcd_divsteps30_vec<kCap>(eta, f0, g0, t);
+    else eta = sgcd_divsteps30<kCap, kSel>(eta, f0, g0, t);
     // the multiples of p clearing the low 30 bits of t (d, e), in [0, 2^30)
     const uint32_t md = (0u - ((uint32_t)t.u * d0 + (uint32_t)t.v * e0) * sgcd_p_inv30()) &
                         (uint32_t)kM30;

@@ -212,7 +212,7 @@ __global__ void __launch_bounds__(WT_BOUNDS) k_wide_selftest(uint64_t seed, int3
 // chain of `iters` elements (z <- 1 / z + 1) with or without the early exit;
 // out[2 wave] = s_memrealtime ticks (100 MHz) for the chain, out[2 wave + 1]
 // = the last result's low word (keeps the chain live)
-template <bool kEarly>
+template <bool kEarly, int kCap, bool kSel, bool kVec = false>
 __global__ void __launch_bounds__(64) k_inv_timing(uint64_t seed, int iters,
                                                   unsigned long long* out) {
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -222,7 +222,8 @@ __global__ void __launch_bounds__(64) k_inv_timing(uint64_t seed, int iters,
   fe z = fe_from_words(w);
   const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
 #pragma unroll 1
-  for (int k = 0; k < iters; k++) z = fe_carry(fe_add(fe_invert_wave<kEarly>(z), fe_one()));
+  for (int k = 0; k < iters; k++)
+    z = fe_carry(fe_add(fe_invert_wave<kEarly, kCap, kSel, kVec>(z), fe_one()));
   const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
   uint32_t e[8];
   fe_to_words(e, z);
@@ -236,7 +237,7 @@ __global__ void __launch_bounds__(64) k_inv_timing(uint64_t seed, int iters,
 // the same chain with only the batches' 30-divstep matrices (modinv.h
 // sgcd_divsteps30 on the low words, f / g advanced by the matrix mod 2^32):
 // what the wave inversion's scalar part costs without the limb updates
-template <int kCap>
+template <int kCap, bool kSel, bool kVec = false>
 __global__ void __launch_bounds__(64) k_divsteps_timing(uint64_t seed, int iters,
                                                        unsigned long long* out) {
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -249,7 +250,8 @@ __global__ void __launch_bounds__(64) k_divsteps_timing(uint64_t seed, int iters
 #pragma unroll 1
   for (int k = 0; k < iters * 18; k++) {
     SgcdMat t;
-    eta = sgcd_divsteps30<kCap>(eta, f, g, t);
+    if (kVec) eta = sgcd_divsteps30_vec<kCap>(eta, f, g, t);
+    else eta = sgcd_divsteps30<kCap, kSel>(eta, f, g, t);
     const uint32_t nf = (uint32_t)t.u * f + (uint32_t)t.v * g;
     const uint32_t ng = (uint32_t)t.q * f + (uint32_t)t.r * g;
     f = (nf >> 30 | 1u) ^ (uint32_t)k;  // keep f odd, vary the words
@@ -269,14 +271,21 @@ __global__ void __launch_bounds__(64) k_divsteps_timing(uint64_t seed, int iters
 }  // namespace
 
 extern "C" {
-// us per 18 batches of divsteps matrices (one inversion's worth), kCap 30 or 10
-double ouro_wide_divsteps_us(int waves, int iters, int cap10, uint64_t seed) {
+// us per 18 batches of divsteps matrices (one inversion's worth); mode 0 cap
+// 30, 1 cap 10, 2 cap 10 branch-free, 3 cap 30 branch-free, 4 cap 30 on the
+// VALU, 5 cap 10 on the VALU
+double ouro_wide_divsteps_us(int waves, int iters, int mode, uint64_t seed) {
   unsigned long long* d = nullptr;
   if (hipMalloc(&d, sizeof(unsigned long long) * 2 * waves) != hipSuccess) return -1;
-  if (cap10)
-    hipLaunchKernelGGL(k_divsteps_timing<10>, dim3(waves), dim3(64), 0, 0, seed, iters, d);
-  else
-    hipLaunchKernelGGL(k_divsteps_timing<30>, dim3(waves), dim3(64), 0, 0, seed, iters, d);
+  const dim3 gr(waves), bl(64);
+  switch (mode) {
+    case 0: hipLaunchKernelGGL((k_divsteps_timing<30, false>), gr, bl, 0, 0, seed, iters, d); break;
+    case 1: hipLaunchKernelGGL((k_divsteps_timing<10, false>), gr, bl, 0, 0, seed, iters, d); break;
+    case 2: hipLaunchKernelGGL((k_divsteps_timing<10, true>), gr, bl, 0, 0, seed, iters, d); break;
+    case 3: hipLaunchKernelGGL((k_divsteps_timing<30, true>), gr, bl, 0, 0, seed, iters, d); break;
+    case 4: hipLaunchKernelGGL((k_divsteps_timing<30, false, true>), gr, bl, 0, 0, seed, iters, d); break;
+    default: hipLaunchKernelGGL((k_divsteps_timing<10, false, true>), gr, bl, 0, 0, seed, iters, d); break;
+  }
   std::vector<unsigned long long> h(2 * (size_t)waves);
   double r = -1;
   if (hipDeviceSynchronize() == hipSuccess &&
@@ -289,15 +298,23 @@ double ouro_wide_divsteps_us(int waves, int iters, int cap10, uint64_t seed) {
   (void)hipFree(d);
   return r;
 }
-// us per inversion averaged over `waves` waves x `iters` inversions, with
-// (early = 1) or without the early exit; -1 on a HIP error
-double ouro_wide_invert_us(int waves, int iters, int early, uint64_t seed) {
+// us per inversion averaged over `waves` waves x `iters` inversions; mode:
+// 0 all 25 batches, cap 30, branching steps (round 4); 1 early exit; 2 early,
+// cap 10; 3 early, cap 10, branch-free steps; 4 early, cap 30, branch-free;
+// 5 early, cap 30, steps on the VALU; 6 the same with cap 10; -1 on a HIP error
+double ouro_wide_invert_us(int waves, int iters, int mode, uint64_t seed) {
   unsigned long long* d = nullptr;
   if (hipMalloc(&d, sizeof(unsigned long long) * 2 * waves) != hipSuccess) return -1;
-  if (early)
-    hipLaunchKernelGGL(k_inv_timing<true>, dim3(waves), dim3(64), 0, 0, seed, iters, d);
-  else
-    hipLaunchKernelGGL(k_inv_timing<false>, dim3(waves), dim3(64), 0, 0, seed, iters, d);
+  const dim3 gr(waves), bl(64);
+  switch (mode) {
+    case 0: hipLaunchKernelGGL((k_inv_timing<false, 30, false>), gr, bl, 0, 0, seed, iters, d); break;
+    case 1: hipLaunchKernelGGL((k_inv_timing<true, 30, false>), gr, bl, 0, 0, seed, iters, d); break;
+    case 2: hipLaunchKernelGGL((k_inv_timing<true, 10, false>), gr, bl, 0, 0, seed, iters, d); break;
+    case 3: hipLaunchKernelGGL((k_inv_timing<true, 10, true>), gr, bl, 0, 0, seed, iters, d); break;
+    case 4: hipLaunchKernelGGL((k_inv_timing<true, 30, true>), gr, bl, 0, 0, seed, iters, d); break;
+    case 5: hipLaunchKernelGGL((k_inv_timing<true, 30, false, true>), gr, bl, 0, 0, seed, iters, d); break;
+    default: hipLaunchKernelGGL((k_inv_timing<true, 10, false, true>), gr, bl, 0, 0, seed, iters, d); break;
+  }
   std::vector<unsigned long long> h(2 * (size_t)waves);
   double r = -1;
   if (hipDeviceSynchronize() == hipSuccess &&

@@ -17,19 +17,22 @@ def main():
     lib = ctypes.CDLL(os.path.join(ROOT, "ouroboros-network_amd", "lib", "libouro_wide_test.so"))
     lib.ouro_wide_invert_us.restype = ctypes.c_double
     lib.ouro_wide_invert_us.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_uint64]
-    res = {}
-    for rep in range(3):
-        for early in (1, 0):
-            us = lib.ouro_wide_invert_us(waves, iters, early, 1234 + rep)
-            res.setdefault("early" if early else "all_25_batches", []).append(round(us, 3))
+    inv_modes = {0: "all_25_batches_cap30", 1: "early_cap30", 2: "early_cap10",
+                 3: "early_cap10_branchfree", 4: "early_cap30_branchfree",
+                 5: "early_cap30_valu", 6: "early_cap10_valu"}
+    ds_modes = {0: "cap30", 1: "cap10", 2: "cap10_branchfree", 3: "cap30_branchfree",
+                4: "cap30_valu", 5: "cap10_valu"}
+    res, ds = {}, {}
     lib.ouro_wide_divsteps_us.restype = ctypes.c_double
     lib.ouro_wide_divsteps_us.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                           ctypes.c_uint64]
-    ds = {}
     for rep in range(3):
-        for cap10 in (1, 0):
-            us = lib.ouro_wide_divsteps_us(waves, iters, cap10, 99 + rep)
-            ds.setdefault("cap10" if cap10 else "cap30", []).append(round(us, 3))
+        for m, name in inv_modes.items():
+            res.setdefault(name, []).append(round(lib.ouro_wide_invert_us(waves, iters, m,
+                                                                          1234 + rep), 3))
+        for m, name in ds_modes.items():
+            ds.setdefault(name, []).append(round(lib.ouro_wide_divsteps_us(waves, iters, m,
+                                                                           99 + rep), 3))
     print(json.dumps({"waves": waves, "iters": iters, "us_per_inversion": res,
                       "us_per_18_divstep_matrices": ds}))
 
