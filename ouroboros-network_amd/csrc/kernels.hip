@@ -1823,15 +1823,38 @@ size_t raw_out_bytes(const RawCall& c, const RawOut& o, size_t m) {
 }
 
 // Every span inside raw (as ouro_tpraos_pack_cbor demands), and the chunks.
+size_t env_size(const char* name, size_t dflt, size_t lo, size_t hi) {
+  if (const char* e = getenv(name)) {
+    const size_t v = (size_t)strtoull(e, nullptr, 10);
+    if (v >= lo && v <= hi) return v;
+  }
+  return dflt;
+}
+
+// Headers in chunk j when `left` headers (this chunk's included) remain.
+// ramp: the first chunks a quarter and a half of `per`, so the first kernel
+// starts after a short gather and upload, and the last ones halving down to a
+// quarter, so the chip is not left running one full chunk's kernel alone at
+// the end (OURO_CBOR_RAMP=0: all `per`).
+size_t raw_chunk_target(size_t j, size_t left, size_t per, bool ramp) {
+  if (!ramp) return per;
+  size_t t = j == 0 ? per / 4 : (j == 1 ? per / 2 : per);
+  if (left <= per + per / 2) t = std::min(t, std::max(per / 4, left / 2));
+  return std::max<size_t>(t, 256);
+}
+
 int raw_chunks(const RawCall& c, size_t per, std::vector<RawChunk>* out) {
   out->clear();
+  const bool ramp = env_size("OURO_CBOR_RAMP", 1, 0, 1) != 0;
   RawChunk k{0, 0, 0};
+  size_t target = raw_chunk_target(0, c.n, per, ramp);
   for (size_t i = 0; i < c.n; i++) {
     if (c.off[i] > c.raw_bytes || c.raw_bytes - c.off[i] < c.len[i])
       return fail(OURO_EINVAL, "header " + std::to_string(i) + ": span outside raw_bytes");
-    if (k.m && (k.m == per || k.bytes + c.len[i] > kRawChunkBytes)) {
+    if (k.m && (k.m >= target || k.bytes + c.len[i] > kRawChunkBytes)) {
       out->push_back(k);
       k = RawChunk{i, 0, 0};
+      target = raw_chunk_target(out->size(), c.n - i, per, ramp);
     }
     k.m++;
     k.bytes += c.len[i];
@@ -1840,13 +1863,6 @@ int raw_chunks(const RawCall& c, size_t per, std::vector<RawChunk>* out) {
   return OURO_OK;
 }
 
-size_t env_size(const char* name, size_t dflt, size_t lo, size_t hi) {
-  if (const char* e = getenv(name)) {
-    const size_t v = (size_t)strtoull(e, nullptr, 10);
-    if (v >= lo && v <= hi) return v;
-  }
-  return dflt;
-}
 
 // last call's phases on this thread (ouro_debug_cbor_stats)
 thread_local double t_raw_stats[6] = {-1, -1, -1, -1, -1, -1};

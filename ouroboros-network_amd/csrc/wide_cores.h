@@ -1064,6 +1064,9 @@ __device__ __forceinline__ void eta_nonce_candidates(const ouro_tpraos_batch& b,
 // record's encodings, beta, claimed-output bits, the eta nonce -- and the
 // verdict.  Same bits and outputs
 // as k_tpraos_finish (tpraos.h vrf_finish_split).
+#ifndef OURO_TAIL_PRELOAD
+#define OURO_TAIL_PRELOAD 1
+#endif
 __device__ __forceinline__ void hdr_tail_wide(const ouro_tpraos_batch& b, size_t i, uint32_t opts,
                                               Slot res, uint8_t* verdict, uint8_t* beta_eta,
                                               uint8_t* beta_leader) {
@@ -1082,16 +1085,46 @@ __device__ __forceinline__ void hdr_tail_wide(const ouro_tpraos_batch& b, size_t
   if (fg & kFlagGammaX0) Genc[7] &= 0x7fffffffu;
 #pragma unroll
   for (int k = 0; k < 4; k++) c[k] = pi[8 + k];
+  // everything the verdict needs besides the challenge, loaded before it so
+  // the loads' latency hides behind the hash (OURO_TAIL_PRELOAD; A/B)
+  uint32_t cl[16];
+  int32_t focert = 0, fkes = 0;
+  const bool claim = (opts & (which ? kOptLeaderClaim : kOptEtaClaim)) != 0;
+  if (OURO_TAIL_PRELOAD) {
+    ld_words8(beta, res + kLatBeta + 16 * which);
+    ld_words8(beta + 8, res + kLatBeta + 16 * which + 8);
+    if (claim) ld_words(cl, (which ? b.leader_output : b.eta_output) + 64 * i, 4);
+    focert = fl(kCoreOcert);
+    fkes = fl(kCoreKes);
+  }
+  // the eta nonce's two candidates (the eta Gamma core's, wide_cores.h
+  // eta_nonce_candidates): which one depends on ok
+  uint32_t n0[8], n1[8];
+  if (OURO_TAIL_PRELOAD && (opts & kOptEtaNonce)) {
+    ld_words8(n0, res + kLatNonce);
+    ld_words8(n1, res + kLatNonce + 8);
+  }
   lstamp(9);
   const bool ceq = vrf_challenge_ok_wave(Henc, Genc, Uenc, Venc, c);
   lstamp(10);
   const bool ok = (fu & fv & fg & kFlagOk) && ceq;
-  ld_words8(beta, res + kLatBeta + 16 * which);
-  ld_words8(beta + 8, res + kLatBeta + 16 * which + 8);
+  if (!OURO_TAIL_PRELOAD) {
+    ld_words8(beta, res + kLatBeta + 16 * which);
+    ld_words8(beta + 8, res + kLatBeta + 16 * which + 8);
+  }
 #pragma unroll
   for (int k = 0; k < 16; k++) beta[k] = ok ? beta[k] : 0u;
   uint32_t bit = ok ? (which ? 0x08u : 0x04u) : 0u;
-  bit |= hdr_claim_bit(b, i, opts, which, ok, beta);
+  if (OURO_TAIL_PRELOAD) {
+    if (ok && claim) {
+      uint32_t diff = 0;
+#pragma unroll
+      for (int k = 0; k < 16; k++) diff |= cl[k] ^ beta[k];
+      if (!diff) bit |= which ? 0x20u : 0x10u;
+    }
+  } else {
+    bit |= hdr_claim_bit(b, i, opts, which, ok, beta);
+  }
   if (!sc_is_canonical(pi + 12)) bit |= which ? OURO_HDR_LEADER_S_UNREDUCED : OURO_HDR_ETA_S_UNREDUCED;
   uint8_t* dst = which ? beta_leader : beta_eta;
   if ((lane & 31u) == 0 && dst) st_words(dst + 64 * i, beta, 4);
@@ -1100,14 +1133,19 @@ __device__ __forceinline__ void hdr_tail_wide(const ouro_tpraos_batch& b, size_t
   if (lane == 0 && (opts & kOptEtaNonce)) {
     const bool pick0 = (opts & kOptEtaClaim) || ok;
     uint32_t h[8];
-    ld_words8(h, res + kLatNonce + (pick0 ? 0 : 8));
+    if (OURO_TAIL_PRELOAD) {
+#pragma unroll
+      for (int k = 0; k < 8; k++) h[k] = pick0 ? n0[k] : n1[k];
+    } else {
+      ld_words8(h, res + kLatNonce + (pick0 ? 0 : 8));
+    }
     st_words(b.eta_nonce + 32 * i, h, 2);
   }
   const uint32_t other = (uint32_t)__builtin_amdgcn_readlane((int)bit, 32);
   if (lane == 0) {
     uint32_t v = bit | other;
-    if (fl(kCoreOcert) & kFlagOk) v |= 0x01u;
-    if (fl(kCoreKes) & kFlagOk) v |= 0x02u;
+    if ((OURO_TAIL_PRELOAD ? focert : fl(kCoreOcert)) & kFlagOk) v |= 0x01u;
+    if ((OURO_TAIL_PRELOAD ? fkes : fl(kCoreKes)) & kFlagOk) v |= 0x02u;
     verdict[i] = (uint8_t)v;
   }
 }

@@ -3,6 +3,8 @@ ouro_integrity_verify_cbor) on one GPU: chunk size, chunks in flight and
 gather threads (OURO_CBOR_CHUNK / _SLOTS / _COPY_THREADS, read per call),
 over n synthetic node-configuration raw headers in pageable host memory.
 Prints one JSON object per configuration (best of `reps` calls).
+CBOR_SWEEP_RAMP_AB=1: instead, the chunk ramp (OURO_CBOR_RAMP) on and off at
+the default chunk / slots / threads, alternated.
     python tools/cbor_sweep.py [n] [reps]"""
 import ctypes
 import itertools
@@ -56,6 +58,22 @@ def main():
                 (131072, 3, 8), (131072, 4, 8), (49152, 8, 8)],
         "kes": [(65536, 2, 8), (65536, 3, 8), (65536, 4, 8), (49152, 4, 8), (98304, 3, 8)],
     }
+    if os.environ.get("CBOR_SWEEP_RAMP_AB"):  # the chunk ramp on / off at the defaults
+        for kind, fn in (("hdr", hdr), ("kes", kes)):
+            for ramp in ("1", "0", "1", "0"):
+                os.environ["OURO_CBOR_RAMP"] = ramp
+                assert fn() == 0, lib.ouro_last_error()
+                ts = []
+                for _ in range(reps):
+                    t0 = time.perf_counter()
+                    assert fn() == 0, lib.ouro_last_error()
+                    ts.append(time.perf_counter() - t0)
+                lib.ouro_debug_cbor_stats(stats.ctypes.data)
+                ok = bool((st == 0).all() and (((v & 0x3F) == 0x3F) if kind == "hdr" else v == 1).all())
+                print(json.dumps({"kind": kind, "ramp": int(ramp), "ms": round(min(ts) * 1e3, 2),
+                                  "M_per_s": round(n / min(ts) / 1e6, 3),
+                                  "chunks": int(stats[3]), "all_valid": ok}), flush=True)
+        return
     for kind, fn in (("hdr", hdr), ("kes", kes)):
         for chunk, slots, threads in grid[kind]:
             os.environ["OURO_CBOR_CHUNK"] = str(chunk)
