@@ -126,6 +126,9 @@ void dh_fe_invert_vartime_cap10(uint8_t* out, const uint8_t* a) {
 void dh_fe_invert_vartime_sel(uint8_t* out, const uint8_t* a) {
   fe_to_bytes(out, fe_invert_vartime<10, true>(fe_from_bytes(a)));
 }
+void dh_fe_invert_vartime_spec(uint8_t* out, const uint8_t* a) {
+  fe_to_bytes(out, fe_invert_vartime<30, true, true>(fe_from_bytes(a)));
+}
 // the same from raw limbs (< 2^31 each: unreduced representations)
 void dh_fe_invert_vartime_limbs(uint8_t* out, const uint32_t* limbs) {
   fe f = fe_make(limbs[0], limbs[1], limbs[2], limbs[3], limbs[4], limbs[5], limbs[6], limbs[7],

@@ -1832,10 +1832,12 @@ size_t env_size(const char* name, size_t dflt, size_t lo, size_t hi) {
 }
 
 // Headers in chunk j when `left` headers (this chunk's included) remain.
-// ramp: the first chunks a quarter and a half of `per`, so the first kernel
-// starts after a short gather and upload, and the last ones halving down to a
-// quarter, so the chip is not left running one full chunk's kernel alone at
-// the end (OURO_CBOR_RAMP=0: all `per`).
+// ramp (OURO_CBOR_RAMP=1, A/B): the first chunks a quarter and a half of
+// `per`, so the first kernel starts after a short gather and upload, and the
+// last ones halving down to a quarter, so the chip is not left running one
+// full chunk's kernel alone at the end.  It lost: 77.5 -> 85.3 ms per 1M
+// headers (profiles/r05o/cbor_ramp_ab.jsonl) -- a small chunk's kernel runs
+// at a fraction of the chip with nothing beside it; off by default.
 size_t raw_chunk_target(size_t j, size_t left, size_t per, bool ramp) {
   if (!ramp) return per;
   size_t t = j == 0 ? per / 4 : (j == 1 ? per / 2 : per);
@@ -1845,7 +1847,7 @@ size_t raw_chunk_target(size_t j, size_t left, size_t per, bool ramp) {
 
 int raw_chunks(const RawCall& c, size_t per, std::vector<RawChunk>* out) {
   out->clear();
-  const bool ramp = env_size("OURO_CBOR_RAMP", 1, 0, 1) != 0;
+  const bool ramp = env_size("OURO_CBOR_RAMP", 0, 0, 1) != 0;
   RawChunk k{0, 0, 0};
   size_t target = raw_chunk_target(0, c.n, per, ramp);
   for (size_t i = 0; i < c.n; i++) {

@@ -61,10 +61,12 @@ OURO_FI uint32_t sgcd_neg_inv(uint32_t f) {
 // of g cancelled per step (<= 10: a one-Newton-step inverse of f, which is
 // recomputed at nearly every step -- ~133 swaps in ~137 steps per inversion
 // -- instead of three; the step count stays ~137 for random operands)
+// kSpec (with kSel): the inverse of g computed ahead of the swap test, kept
+// for f when the step swaps (off the step's dependent chain).
 // kSel: the swap as selects and the inverse recomputed at every step, so a
 // step has no branch but the loop's own (the wave inversion runs this on the
 // scalar unit, where each taken branch costs an instruction refetch)
-template <int kCap = 30, bool kSel = false>
+template <int kCap = 30, bool kSel = false, bool kSpec = false>
 OURO_FI int32_t sgcd_divsteps30(int32_t eta, uint32_t f, uint32_t g, SgcdMat& t) {
   uint32_t u = 1, v = 0, q = 0, r = 1;
   uint32_t nfi = sgcd_neg_inv<kCap>(f);  // -1 / f mod 2^kCap, recomputed when f changes
@@ -79,6 +81,9 @@ OURO_FI int32_t sgcd_divsteps30(int32_t eta, uint32_t f, uint32_t g, SgcdMat& t)
       eta -= zeros;
       i -= zeros;
       if (i == 0) break;
+      // the inverse of g (f after a swap), computed before the swap test so
+      // it overlaps it (kSpec), else of the new f after the swap
+      const uint32_t nig = kSpec ? sgcd_neg_inv<kCap>(g) : 0u;
       const bool sw = eta < 0;
       const uint32_t f1 = sw ? g : f, g1 = sw ? 0u - f : g;
       const uint32_t u1 = sw ? q : u, q1 = sw ? 0u - u : q;
@@ -90,7 +95,8 @@ OURO_FI int32_t sgcd_divsteps30(int32_t eta, uint32_t f, uint32_t g, SgcdMat& t)
       q = q1;
       v = v1;
       r = r1;
-      const uint32_t ni = sgcd_neg_inv<kCap>(f);
+      if (kSpec) nfi = sw ? nig : nfi;
+      const uint32_t ni = kSpec ? nfi : sgcd_neg_inv<kCap>(f);
       int limit = (eta + 1) > i ? i : (eta + 1);
       if (kCap < 30) limit = limit > kCap ? kCap : limit;
       const uint32_t w = (g * ni) & (0xffffffffu >> (32 - limit));
@@ -202,7 +208,7 @@ OURO_FI void sgcd_add_p(int32_t d[9], int32_t sign) {  // d += p if sign (0 / -1
 }
 
 // z^-1 mod p (0 for z = 0), variable time (kCap: sgcd_divsteps30)
-template <int kCap = 30, bool kSel = false>
+template <int kCap = 30, bool kSel = false, bool kSpec = false>
 OURO_HD inline fe fe_invert_vartime(const fe& z) {
   uint32_t zw[8];
   fe_to_words(zw, z);
@@ -223,7 +229,7 @@ OURO_HD inline fe fe_invert_vartime(const fe& z) {
 #pragma unroll 1
   for (int it = 0; it < 32; it++) {
     SgcdMat t;
-    eta = sgcd_divsteps30<kCap, kSel>(eta, (uint32_t)f[0], (uint32_t)g[0], t);
+    eta = sgcd_divsteps30<kCap, kSel, kSpec>(eta, (uint32_t)f[0], (uint32_t)g[0], t);
     sgcd_update_de(d, e, t);
     sgcd_update_fg(f, g, t);
     int32_t nz = 0;

@@ -237,7 +237,7 @@ __global__ void __launch_bounds__(64) k_inv_timing(uint64_t seed, int iters,
 // the same chain with only the batches' 30-divstep matrices (modinv.h
 // sgcd_divsteps30 on the low words, f / g advanced by the matrix mod 2^32):
 // what the wave inversion's scalar part costs without the limb updates
-template <int kCap, bool kSel, bool kVec = false>
+template <int kCap, bool kSel, bool kVec = false, bool kSpec = false>
 __global__ void __launch_bounds__(64) k_divsteps_timing(uint64_t seed, int iters,
                                                        unsigned long long* out) {
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -251,7 +251,7 @@ __global__ void __launch_bounds__(64) k_divsteps_timing(uint64_t seed, int iters
   for (int k = 0; k < iters * 18; k++) {
     SgcdMat t;
     if (kVec) eta = sgcd_divsteps30_vec<kCap>(eta, f, g, t);
-    else eta = sgcd_divsteps30<kCap, kSel>(eta, f, g, t);
+    else eta = sgcd_divsteps30<kCap, kSel, kSpec>(eta, f, g, t);
     const uint32_t nf = (uint32_t)t.u * f + (uint32_t)t.v * g;
     const uint32_t ng = (uint32_t)t.q * f + (uint32_t)t.r * g;
     f = (nf >> 30 | 1u) ^ (uint32_t)k;  // keep f odd, vary the words
@@ -273,7 +273,7 @@ __global__ void __launch_bounds__(64) k_divsteps_timing(uint64_t seed, int iters
 extern "C" {
 // us per 18 batches of divsteps matrices (one inversion's worth); mode 0 cap
 // 30, 1 cap 10, 2 cap 10 branch-free, 3 cap 30 branch-free, 4 cap 30 on the
-// VALU, 5 cap 10 on the VALU
+// VALU, 5 cap 10 on the VALU, 6 cap 30 branch-free with the speculative inverse
 double ouro_wide_divsteps_us(int waves, int iters, int mode, uint64_t seed) {
   unsigned long long* d = nullptr;
   if (hipMalloc(&d, sizeof(unsigned long long) * 2 * waves) != hipSuccess) return -1;
@@ -284,7 +284,8 @@ double ouro_wide_divsteps_us(int waves, int iters, int mode, uint64_t seed) {
     case 2: hipLaunchKernelGGL((k_divsteps_timing<10, true>), gr, bl, 0, 0, seed, iters, d); break;
     case 3: hipLaunchKernelGGL((k_divsteps_timing<30, true>), gr, bl, 0, 0, seed, iters, d); break;
     case 4: hipLaunchKernelGGL((k_divsteps_timing<30, false, true>), gr, bl, 0, 0, seed, iters, d); break;
-    default: hipLaunchKernelGGL((k_divsteps_timing<10, false, true>), gr, bl, 0, 0, seed, iters, d); break;
+    case 5: hipLaunchKernelGGL((k_divsteps_timing<10, false, true>), gr, bl, 0, 0, seed, iters, d); break;
+    default: hipLaunchKernelGGL((k_divsteps_timing<30, true, false, true>), gr, bl, 0, 0, seed, iters, d); break;
   }
   std::vector<unsigned long long> h(2 * (size_t)waves);
   double r = -1;

@@ -78,7 +78,8 @@ def _check(raws, spkp, ea=None, la=None, epoch_nonce=None, triple=None):
 @pytest.fixture
 def small_chunks():
     """The pipeline cut into many chunks (each env var is read per call)."""
-    saved = {k: os.environ.get(k) for k in ("OURO_CBOR_CHUNK", "OURO_CBOR_SLOTS")}
+    saved = {k: os.environ.get(k) for k in ("OURO_CBOR_CHUNK", "OURO_CBOR_SLOTS",
+                                             "OURO_CBOR_RAMP")}
     yield
     for k, v in saved.items():
         if v is None:
@@ -99,16 +100,36 @@ def test_golden_corruptions_truncations(gpu_lib, kats):
     assert (st != H.PACK_OK).any() and (v[st != H.PACK_OK] == 0).all()
 
 
+def _ramp_chunks(n, per, ramp=True):
+    """chunk count of kernels.hip raw_chunks / raw_chunk_target (the golden
+    headers are far below the 96 MiB byte cap)"""
+    count, j, i = 0, 0, 0
+    while i < n:
+        t = per
+        if ramp:
+            t = per // 4 if j == 0 else (per // 2 if j == 1 else per)
+            left = n - i
+            if left <= per + per // 2:
+                t = min(t, max(per // 4, left // 2))
+            t = max(t, 256)
+        i += t
+        j += 1
+        count += 1
+    return count
+
+
 @pytest.mark.gpu
-@pytest.mark.parametrize("chunk,slots", [(256, 1), (256, 3), (512, 8), (1024, 2)])
-def test_golden_in_small_chunks(gpu_lib, kats, small_chunks, chunk, slots):
+@pytest.mark.parametrize("chunk,slots,ramp", [(256, 1, 1), (256, 3, 0), (512, 8, 1),
+                                              (1024, 2, 1), (1024, 2, 0)])
+def test_golden_in_small_chunks(gpu_lib, kats, small_chunks, chunk, slots, ramp):
     raws, ea, la = _golden_cases(kats, stride=2)
     os.environ["OURO_CBOR_CHUNK"] = str(chunk)
     os.environ["OURO_CBOR_SLOTS"] = str(slots)
+    os.environ["OURO_CBOR_RAMP"] = str(ramp)
     _check(raws, SPKP, ea, la)
     stats = np.zeros(6)
     gpu_lib.ouro_debug_cbor_stats(stats.ctypes.data)
-    assert stats[3] == -(-len(raws) // chunk) and stats[4] == slots
+    assert stats[3] == _ramp_chunks(len(raws), chunk, bool(ramp)) and stats[4] == slots
 
 
 @pytest.mark.gpu

@@ -21,7 +21,7 @@ def main():
                  3: "early_cap10_branchfree", 4: "early_cap30_branchfree",
                  5: "early_cap30_valu", 6: "early_cap10_valu"}
     ds_modes = {0: "cap30", 1: "cap10", 2: "cap10_branchfree", 3: "cap30_branchfree",
-                4: "cap30_valu", 5: "cap10_valu"}
+                4: "cap30_valu", 5: "cap10_valu", 6: "cap30_branchfree_spec"}
     res, ds = {}, {}
     lib.ouro_wide_divsteps_us.restype = ctypes.c_double
     lib.ouro_wide_divsteps_us.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int,
