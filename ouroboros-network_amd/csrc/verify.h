@@ -373,6 +373,10 @@ constexpr uint32_t dsm_cfg(int nw1, int nw2, bool useB, int tab1 = 0, int tab2 =
 // A doubling of the lane chain: its products in lockstep (ge25519.h
 // ge_dbl_lockstep, 1, the default since round 4) or as written in ge_p2_dbl
 // (0, A/B).
+// the same for the chain's additions (ge25519.h ge_add_lockstep; A/B)
+#ifndef OURO_ADD_LOCKSTEP
+#define OURO_ADD_LOCKSTEP 0
+#endif
 #ifndef OURO_DBL_LOCKSTEP
 #define OURO_DBL_LOCKSTEP 1
 #endif
@@ -515,8 +519,9 @@ OURO_FI void dsm_body(Slot lane, const int32_t* btab, uint32_t cfg) {
         fresh = false;
         continue;
       }
-      t = kQuad ? ge_add_cached_quad(ge_p1p1_to_p3_quad(t), q, neg)
-                : ge_add_cached(ge_p1p1_to_p3(t), q, neg, src >= 2);
+      if constexpr (kQuad) t = ge_add_cached_quad(ge_p1p1_to_p3_quad(t), q, neg);
+      else if constexpr (OURO_ADD_LOCKSTEP) t = ge_add_lockstep(t, q, neg, src >= 2);
+      else t = ge_add_cached(ge_p1p1_to_p3(t), q, neg, src >= 2);
     }
   }
   ge_p2 r = kQuad ? ge_p1p1_to_p2_quad(t) : ge_p1p1_to_p2(t);
