@@ -5,7 +5,9 @@ AddressSanitizer + UBSan build with the matching runtime preloaded --
   * the oracle (gcc, oracle/build/liboracle_asan.so),
   * the CBOR slicer (gcc, lib/libouro_pack_asan.so: csrc/pack.cpp alone),
   * the kernels' lane routines compiled for the host with the bound tracker
-    (clang via hipcc, lib/libouro_devhost_asan.so).
+    (clang via hipcc, lib/libouro_devhost_asan.so),
+  * the product's host path -- host_path.hip, host_fast.h, the task pool --
+    behind a test-only shim (clang via hipcc, lib/libouro_hostpath_asan.so).
 Any sanitizer report fails the test (UBSan is built non-recoverable)."""
 import glob
 import os
@@ -41,6 +43,7 @@ def _run(preload, env_extra, tests):
     out = r.stdout + r.stderr
     assert r.returncode == 0, out[-4000:]
     assert "AddressSanitizer" not in out and "runtime error:" not in out, out[-4000:]
+    assert " passed" in out, out[-2000:]  # not everything skipped
     return out
 
 
@@ -68,3 +71,11 @@ def test_lane_routines_under_asan_ubsan():
     _make(PKG, "lib/libouro_devhost_asan.so")  # prebuilt by __graft_entry__.build()
     _run(_clang_asan(), {"OURO_DEVHOST_LIB": os.path.join(PKG, "lib", "libouro_devhost_asan.so")},
          ["tests/test_devcode_host.py"])
+
+
+@pytest.mark.skipif(_clang_asan() is None, reason="clang ASan runtime not in the ROCm llvm")
+def test_host_path_under_asan_ubsan():
+    _make(PKG, "lib/libouro_hostpath_asan.so")
+    _run(_clang_asan(),
+         {"OURO_HOSTPATH_ASAN_LIB": os.path.join(PKG, "lib", "libouro_hostpath_asan.so")},
+         ["tests/test_hostpath_asan.py"])
