@@ -121,20 +121,34 @@ OURO_FI ge_p1p1 ge_add_cached(const ge_p3& p, const ge_cached& q, bool neg,
 // addition's four (three for an affine q) in lockstep (fe_mul_xn), the same
 // operands in the same order as the two calls (the same bounds), like the
 // doubling's ge_dbl_lockstep (A/B switch OURO_ADD_LOCKSTEP, verify.h)
+// kPair: the products two at a time (fewer live registers) instead of all at once
+template <bool kPair = false>
 OURO_FI ge_p1p1 ge_add_lockstep(const ge_p1p1& t, const ge_cached& q, bool neg, bool affine_q) {
   const fe f1[4] = {t.T, t.Z, t.T, t.X}, g1[4] = {t.X, t.Y, t.Z, t.Y};
   fe p[4];
-  fe_mul_xn<4>(p, f1, g1);  // X = T X, Y = Z Y, Z = T Z, T = X Y
+  if (kPair) {  // X = T X, Y = Z Y, Z = T Z, T = X Y
+    fe_mul_xn<2>(p, f1, g1);
+    fe_mul_xn<2>(p + 2, f1 + 2, g1 + 2);
+  } else {
+    fe_mul_xn<4>(p, f1, g1);
+  }
   const fe qa = fe_select(q.YminusX, q.YplusX, neg);
   const fe qb = fe_select(q.YplusX, q.YminusX, neg);
   fe o[4];
+  const fe f2[4] = {fe_add(p[1], p[0]), fe_sub(p[1], p[0]), p[3], p[2]};
+  const fe g2[4] = {qa, qb, q.T2d, q.Z2};
   if (affine_q) {
-    const fe f2[3] = {fe_add(p[1], p[0]), fe_sub(p[1], p[0]), p[3]}, g2[3] = {qa, qb, q.T2d};
-    fe_mul_xn<3>(o, f2, g2);
+    if (kPair) {
+      fe_mul_xn<2>(o, f2, g2);
+      o[2] = fe_mul(f2[2], g2[2]);
+    } else {
+      fe_mul_xn<3>(o, f2, g2);
+    }
     o[3] = fe_carry(fe_add(p[2], p[2]));
+  } else if (kPair) {
+    fe_mul_xn<2>(o, f2, g2);
+    fe_mul_xn<2>(o + 2, f2 + 2, g2 + 2);
   } else {
-    const fe f2[4] = {fe_add(p[1], p[0]), fe_sub(p[1], p[0]), p[3], p[2]};
-    const fe g2[4] = {qa, qb, q.T2d, q.Z2};
     fe_mul_xn<4>(o, f2, g2);
   }
   const fe Dp = fe_add(o[3], o[2]), Dm = fe_sub(o[3], o[2]);

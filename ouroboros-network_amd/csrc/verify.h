@@ -373,9 +373,10 @@ constexpr uint32_t dsm_cfg(int nw1, int nw2, bool useB, int tab1 = 0, int tab2 =
 // A doubling of the lane chain: its products in lockstep (ge25519.h
 // ge_dbl_lockstep, 1, the default since round 4) or as written in ge_p2_dbl
 // (0, A/B).
-// the same for the chain's additions (ge25519.h ge_add_lockstep; A/B)
+// the same for the chain's additions (ge25519.h ge_add_lockstep): 1 = four
+// products at a time, 2 = two, 0 = as written (round 4)
 #ifndef OURO_ADD_LOCKSTEP
-#define OURO_ADD_LOCKSTEP 0
+#define OURO_ADD_LOCKSTEP 1
 #endif
 #ifndef OURO_DBL_LOCKSTEP
 #define OURO_DBL_LOCKSTEP 1
@@ -520,7 +521,7 @@ OURO_FI void dsm_body(Slot lane, const int32_t* btab, uint32_t cfg) {
         continue;
       }
       if constexpr (kQuad) t = ge_add_cached_quad(ge_p1p1_to_p3_quad(t), q, neg);
-      else if constexpr (OURO_ADD_LOCKSTEP) t = ge_add_lockstep(t, q, neg, src >= 2);
+      else if constexpr (OURO_ADD_LOCKSTEP) t = ge_add_lockstep<OURO_ADD_LOCKSTEP == 2>(t, q, neg, src >= 2);
       else t = ge_add_cached(ge_p1p1_to_p3(t), q, neg, src >= 2);
     }
   }
