@@ -155,8 +155,52 @@ struct ShaGlobalTail {
     const uint32_t hi = __builtin_amdgcn_alignbit(d2, d1, sh);  // bytes q+4..q+7
     return ((uint64_t)__builtin_bswap32(lo) << 32) | __builtin_bswap32(hi);
   }
+  // the sixteen words at q0, q0 + 8, ..., q0 + 120 (one tail block) from
+  // eight dwordx4 loads and one dword at dword alignment instead of 33 dword
+  // loads; a dwordx4 is issued only when its last dword starts before the
+  // end, else its dwords one by one under word_be's rule, so it never reads
+  // further past the end than word_be does (OURO_SHA_BLOCK_LOAD)
+  OURO_FI void block_be(uint64_t W[16], uint32_t q0, uint32_t tl) const {
+    const uintptr_t a = reinterpret_cast<uintptr_t>(msg) + q0;
+    const uintptr_t end = reinterpret_cast<uintptr_t>(msg) + tl;
+    const uintptr_t base = a & ~uintptr_t(3);
+    const uint32_t sh = (uint32_t)(a & 3) * 8;
+    uint32_t d[33];
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+      const uintptr_t p = base + 16 * (uintptr_t)j;
+      if (p + 12 < end) {
+        const int4 v = ldg4(reinterpret_cast<const void*>(p));
+        d[4 * j] = (uint32_t)v.x;
+        d[4 * j + 1] = (uint32_t)v.y;
+        d[4 * j + 2] = (uint32_t)v.z;
+        d[4 * j + 3] = (uint32_t)v.w;
+      } else {
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+          d[4 * j + k] = p + 4 * k < end ? (uint32_t)ldg1(reinterpret_cast<const void*>(p + 4 * k)) : 0u;
+      }
+    }
+    d[32] = base + 128 < end ? (uint32_t)ldg1(reinterpret_cast<const void*>(base + 128)) : 0u;
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+      const uint32_t lo = __builtin_amdgcn_alignbit(d[2 * k + 1], d[2 * k], sh);
+      const uint32_t hi = __builtin_amdgcn_alignbit(d[2 * k + 2], d[2 * k + 1], sh);
+      W[k] = ((uint64_t)__builtin_bswap32(lo) << 32) | __builtin_bswap32(hi);
+    }
+  }
 #endif
 };
+#ifndef OURO_SHA_BLOCK_LOAD
+#define OURO_SHA_BLOCK_LOAD 0
+#endif
+template <class T, class = void>
+struct has_block_be : std::false_type {};
+#if defined(__HIP_DEVICE_COMPILE__)
+template <class T>
+struct has_block_be<T, decltype((void)std::declval<const T&>().block_be(nullptr, 0u, 0u))>
+    : std::true_type {};
+#endif
 
 // A tail in global memory that the WAVE stages into LDS with coalesced loads
 // (round 5, OURO_KES_STAGE; the throughput Sum6KES kernel's leaf message).
@@ -355,11 +399,14 @@ OURO_FI void sha512_prefixed(uint64_t out[8], const uint32_t* prefix, const Tail
   // remaining blocks read only the tail
 #pragma unroll 1
   for (uint32_t b = kStaticBlocks; b < nb; b++) {
-    uint64_t W[16];
+    uint64_t W[16], raw[16];
+    if constexpr (OURO_SHA_BLOCK_LOAD && has_block_be<Tail>::value) tail.block_be(raw, b * 128 - PL, tl);
 #pragma unroll
     for (int w = 0; w < 16; w++) {
       const uint32_t p0 = b * 128 + w * 8;
-      uint64_t r = sha_pad_word(sha_tail_word(tail, p0 - PL, tl), p0, total);
+      uint64_t r;
+      if constexpr (OURO_SHA_BLOCK_LOAD && has_block_be<Tail>::value) r = sha_pad_word(raw[w], p0, total);
+      else r = sha_pad_word(sha_tail_word(tail, p0 - PL, tl), p0, total);
       const uint32_t widx = b * 16 + w;
       if (widx == nb * 16 - 1) r = (uint64_t)total << 3;
       else if (widx == nb * 16 - 2) r = 0;
