@@ -192,7 +192,7 @@ struct ShaGlobalTail {
 #endif
 };
 #ifndef OURO_SHA_BLOCK_LOAD
-#define OURO_SHA_BLOCK_LOAD 0
+#define OURO_SHA_BLOCK_LOAD 1
 #endif
 template <class T, class = void>
 struct has_block_be : std::false_type {};
