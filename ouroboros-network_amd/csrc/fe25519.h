@@ -1053,9 +1053,11 @@ OURO_FI bool fe_isnegative(const fe& f) {
 // other, so the one-chain form issues dependent multiply-adds back to back
 // (6.9 SIMD cycles each at 2 waves against 4.4 for two chains,
 // profiles/r04/valu_costs.json).  A/B switch for the chains only (the
-// doublings' squarings are already interleaved, ge_dbl_lockstep).
+// doublings' squarings are already interleaved, ge_dbl_lockstep).  Two
+// since round 5: with the additions in lockstep it took the header kernel
+// -1.25 / -0.55 % in two A/Bs (profiles/r05y, r05z; mixed in round 4).
 #ifndef OURO_POW_SQ_CHAINS
-#define OURO_POW_SQ_CHAINS 1
+#define OURO_POW_SQ_CHAINS 2
 #endif
 OURO_FI fe fe_sq_pow(const fe& f) {
   if constexpr (OURO_POW_SQ_CHAINS == 2) {
