@@ -268,6 +268,42 @@ __device__ __forceinline__ fe fw_to_fe(int32_t x, int row = 0) {
   return f;
 }
 
+// fw_to_fe of the element in this lane's own row, on every lane at once: the
+// row's sixteen limbs gathered with ds_bpermute, then fw_to_fe's arithmetic
+// in vector registers, so the four rows convert in one pass instead of four
+// scalar ones (encode2_wide, OURO_ENC_ROWS)
+__device__ __forceinline__ fe fw_to_fe_own_row(int32_t x) {
+  const int base = (int)(threadIdx.x & 48u);
+  uint32_t h[16];
+  int32_t c = 0;
+#pragma unroll
+  for (int k = 0; k < 16; k++) {
+    const int32_t pk = k == 0 ? 0xffed : (k == 15 ? 0x7fff : 0xffff);
+    const int32_t t = __builtin_amdgcn_ds_bpermute((base + k) << 2, x) + 4 * pk + c;
+    h[k] = (uint32_t)t & 0xffffu;
+    c = t >> 16;
+  }
+#pragma unroll
+  for (int pass = 0; pass < 2; pass++) {
+    uint32_t cc = (uint32_t)c * 38u;
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+      const uint32_t t = h[k] + cc;
+      h[k] = t & 0xffffu;
+      cc = t >> 16;
+    }
+    c = (int32_t)cc;
+  }
+  uint32_t w[8];
+#pragma unroll
+  for (int k = 0; k < 8; k++) w[k] = h[2 * k] | (h[2 * k + 1] << 16);
+  const uint32_t top = w[7] >> 31;  // 2^255 = 19
+  w[7] &= 0x7fffffffu;
+  fe f = fe_from_words(w);
+  f.v[0] += 19u * top;
+  return f;
+}
+
 __device__ __forceinline__ int32_t fw_one(const Lanes& L) { return L.j == 0 ? 1 : 0; }
 
 // ---- exponentiations -------------------------------------------------------------

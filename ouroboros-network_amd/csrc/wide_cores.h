@@ -483,6 +483,13 @@ __device__ __forceinline__ void vrf_v_full_wide(uint32_t Henc[8], uint32_t Venc[
 
 // canonical encodings from this row's affine coordinate of x and y (rows
 // rx / ry of c): y with x's parity in bit 255 (ge25519.h ge_encode_with_inv)
+// The encodings' coordinates made canonical in one vector pass, every row
+// its own element (wide.h fw_to_fe_own_row; 1, since round 5: the V2 item's
+// encodings 3.1 -> 1.3 us, profiles/r05af) or one after another on the
+// scalar path (0, A/B)
+#ifndef OURO_ENC_ROWS
+#define OURO_ENC_ROWS 1
+#endif
 __device__ __forceinline__ void enc_from_rows(uint32_t out[8], int32_t c, int rx, int ry) {
   uint32_t xw[8];
   fe_to_words(out, fw_to_fe(c, ry));
@@ -495,7 +502,15 @@ __device__ __forceinline__ void encode1_wide(uint32_t enc[8], const pw& P) {
   const Lanes L = lanes();
   const int32_t zi = fw_invert_sel(P.Z, L);
   const int32_t c = fw_mul(L.odd ? P.Y : P.X, zi, L);
-  enc_from_rows(enc, c, 0, 1);
+  if (OURO_ENC_ROWS) {  // x and y canonical in one vector pass (encode2_wide)
+    uint32_t w[8];
+    fe_to_words(w, fw_to_fe_own_row(c));
+#pragma unroll
+    for (int k = 0; k < 8; k++) enc[k] = (uint32_t)__builtin_amdgcn_readlane((int)w[k], 16);
+    enc[7] ^= ((uint32_t)__builtin_amdgcn_readlane((int)w[0], 0) & 1u) << 31;
+  } else {
+    enc_from_rows(enc, c, 0, 1);
+  }
 }
 // encode(H) and encode(V) with one inversion: 1 / (ZH ZV), then 1 / ZH and
 // 1 / ZV (rows 0 / 1), then xH, yH, xV, yV (rows 0..3), all on the wave
@@ -506,8 +521,21 @@ __device__ __forceinline__ void encode2_wide(uint32_t Henc[8], uint32_t Venc[8],
   lstamp(6);
   const fw4 zi = fw_gather(fw_mul(inv, L.odd ? H.Z : V.Z, L));  // r0 = 1/ZH, r1 = 1/ZV
   const int32_t c = fw_mul(sel4(H.X, H.Y, V.X, V.Y, L), L.high ? zi.r1 : zi.r0, L);
-  enc_from_rows(Henc, c, 0, 1);
-  enc_from_rows(Venc, c, 2, 3);
+  if (OURO_ENC_ROWS) {
+    // all four coordinates canonical at once (each row its own), then read out
+    uint32_t w[8];
+    fe_to_words(w, fw_to_fe_own_row(c));
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      Henc[k] = (uint32_t)__builtin_amdgcn_readlane((int)w[k], 16);  // row 1: yH
+      Venc[k] = (uint32_t)__builtin_amdgcn_readlane((int)w[k], 48);  // row 3: yV
+    }
+    Henc[7] ^= ((uint32_t)__builtin_amdgcn_readlane((int)w[0], 0) & 1u) << 31;   // xH's sign
+    Venc[7] ^= ((uint32_t)__builtin_amdgcn_readlane((int)w[0], 32) & 1u) << 31;  // xV's sign
+  } else {
+    enc_from_rows(Henc, c, 0, 1);
+    enc_from_rows(Venc, c, 2, 3);
+  }
 }
 
 // The Gamma core of the split form in two parts: the acceptance checks and
