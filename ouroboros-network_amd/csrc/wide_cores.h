@@ -84,6 +84,14 @@ __device__ __forceinline__ void vstamp_print() {
 #endif
 }
 
+// Row elements made canonical in one vector pass, every row its own element
+// (wide.h fw_to_fe_own_row): the encodings' coordinates and Elligator2's
+// three zero tests (1, since round 5: the V2 item's encodings 3.1 -> 1.3 us,
+// profiles/r05af), or one after another on the scalar path (0, A/B)
+#ifndef OURO_ENC_ROWS
+#define OURO_ENC_ROWS 1
+#endif
+
 // z^(2^252 - 3) of a lane-local element on the wave
 __device__ __forceinline__ fe pow22523_wide(const fe& z) {
   return fw_to_fe(fw_pow22523(fe_to_fw(z, lanes())));
@@ -159,8 +167,17 @@ __device__ __forceinline__ pw elligator2_wide(const uint32_t r[8], const Lanes& 
   const int32_t vxx = fw_mul_rep(fw_sq_rep(beta, L), W, L);      // beta^2 W
   // the root's 4th root of unity: vxx = num (1), -num (-1), num i (i) or -num i
   const int32_t d = sel4(vxx - num, vxx + num, vxx - c.r2, vxx - num, L);
-  const bool lam_p1 = fw_row_iszero(d, 0), lam_m1 = fw_row_iszero(d, 1);
-  const bool lam_pi = fw_row_iszero(d, 2);
+  bool lam_p1, lam_m1, lam_pi;
+  if (OURO_ENC_ROWS) {  // the three tests in one vector pass, each row its own
+    const uint32_t z = fe_iszero(fw_to_fe_own_row(d)) ? 1u : 0u;
+    lam_p1 = __builtin_amdgcn_readlane((int)z, 0) != 0;
+    lam_m1 = __builtin_amdgcn_readlane((int)z, 16) != 0;
+    lam_pi = __builtin_amdgcn_readlane((int)z, 32) != 0;
+  } else {
+    lam_p1 = fw_row_iszero(d, 0);
+    lam_m1 = fw_row_iszero(d, 1);
+    lam_pi = fw_row_iszero(d, 2);
+  }
   const bool nonsq = !(lam_p1 || lam_m1);
   const fe Ff = fe_select(fe_select(fe_one_minus_i(), fe_one_plus_i(), lam_pi),
                           fe_select(fe_one(), fe_sqrtm1(), lam_p1), nonsq);
@@ -483,13 +500,6 @@ __device__ __forceinline__ void vrf_v_full_wide(uint32_t Henc[8], uint32_t Venc[
 
 // canonical encodings from this row's affine coordinate of x and y (rows
 // rx / ry of c): y with x's parity in bit 255 (ge25519.h ge_encode_with_inv)
-// The encodings' coordinates made canonical in one vector pass, every row
-// its own element (wide.h fw_to_fe_own_row; 1, since round 5: the V2 item's
-// encodings 3.1 -> 1.3 us, profiles/r05af) or one after another on the
-// scalar path (0, A/B)
-#ifndef OURO_ENC_ROWS
-#define OURO_ENC_ROWS 1
-#endif
 __device__ __forceinline__ void enc_from_rows(uint32_t out[8], int32_t c, int rx, int ry) {
   uint32_t xw[8];
   fe_to_words(out, fw_to_fe(c, ry));
