@@ -268,9 +268,50 @@ __global__ void __launch_bounds__(64) k_divsteps_timing(uint64_t seed, int iters
 #endif
 }
 
+// One wave per input: the latency mode's Elligator2 (hash-to-curve with the
+// cofactor cleared) and its one-point encoding, exactly as the V / V2 items
+// run them (wide_cores.h elligator2_wide, encode1_wide), for the oracle
+// comparison in tests/test_gpu_wide.py.  r: 32 bytes per input, top bit clear.
+__global__ void __launch_bounds__(64) k_wide_elligator2(int n, const uint8_t* r, uint8_t* out) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  using namespace wide;
+  const int i = (int)blockIdx.x;
+  if (i >= n) return;
+  const Lanes L = lanes();
+  uint32_t rw[8], enc[8];
+#pragma unroll
+  for (int k = 0; k < 8; k++) rw[k] = reinterpret_cast<const uint32_t*>(r + 32 * (size_t)i)[k];
+  rw[7] &= 0x7fffffffu;
+  encode1_wide(enc, elligator2_wide(rw, L));
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int k = 0; k < 8; k++) reinterpret_cast<uint32_t*>(out + 32 * (size_t)i)[k] = enc[k];
+  }
+#endif
+}
+
 }  // namespace
 
 extern "C" {
+// Elligator2 + encoding of n host inputs on the device (one wave each);
+// 0, -1 on bad arguments, -2 on a HIP error
+int ouro_wide_elligator2(int n, const uint8_t* r, uint8_t* out) {
+  if (n <= 0 || !r || !out) return -1;
+  uint8_t *d_r = nullptr, *d_o = nullptr;
+  const size_t bytes = 32 * (size_t)n;
+  int rc = 0;
+  if (hipMalloc(&d_r, bytes) != hipSuccess || hipMalloc(&d_o, bytes) != hipSuccess) rc = -2;
+  if (!rc && hipMemcpy(d_r, r, bytes, hipMemcpyHostToDevice) != hipSuccess) rc = -2;
+  if (!rc) {
+    hipLaunchKernelGGL(k_wide_elligator2, dim3(n), dim3(64), 0, 0, n, d_r, d_o);
+    if (hipDeviceSynchronize() != hipSuccess || hipGetLastError() != hipSuccess) rc = -2;
+  }
+  if (!rc && hipMemcpy(out, d_o, bytes, hipMemcpyDeviceToHost) != hipSuccess) rc = -2;
+  if (d_r) (void)hipFree(d_r);
+  if (d_o) (void)hipFree(d_o);
+  return rc;
+}
+
 // us per 18 batches of divsteps matrices (one inversion's worth); mode 0 cap
 // 30, 1 cap 10, 2 cap 10 branch-free, 3 cap 30 branch-free, 4 cap 30 on the
 // VALU, 5 cap 10 on the VALU, 6 cap 30 branch-free with the speculative inverse

@@ -2,7 +2,9 @@
 lane-local routines it replaces, on the device: conversions, products,
 squaring chains, z^(2^252-3), doubling, addition/subtraction, [s]P against
 double-and-add, the identity, and the latency mode's [s]H item (wide_vrf.h).  One wave per case (random + edge field
-elements: p - 1, 0); csrc/wide_test.hip is a test-only library."""
+elements: p - 1, 0); csrc/wide_test.hip is a test-only library.  The
+latency items' Elligator2 and encoding are also checked against the oracle
+directly (test_wide_elligator2_matches_oracle)."""
 import ctypes
 import os
 
@@ -27,3 +29,31 @@ def test_wide_arithmetic_matches_lane_routines(gpu_lib, seed):
     res = out.reshape(waves, len(NAMES))
     bad = {NAMES[t]: int((res[:, t] != 1).sum()) for t in range(len(NAMES))}
     assert all(v == 0 for v in bad.values()), (bad, dbg.tolist())
+
+
+@pytest.mark.gpu
+def test_wide_elligator2_matches_oracle(gpu_lib):
+    """The latency items' hash-to-curve (wide_cores.h elligator2_wide, cofactor
+    cleared) and one-point encoding (encode1_wide: the vector-pass conversion
+    and the three zero tests) against the oracle's Elligator2
+    (oracle/vrf03.c orc_elligator2_from_uniform, pinned to libsodium's
+    crypto_core_ed25519_from_uniform in test_oracle.py), byte for byte.
+    Inputs as the VRF hands them over (top bit clear): zero, small values,
+    the non-canonical range p .. 2^255 - 1 and seeded random strings."""
+    import oracle_ffi as O
+
+    p = 2**255 - 19
+    vals = [0, 1, 2, 3, 4, 5, p - 1, p, p + 1, p + 7, 2**255 - 1]
+    rs = [v.to_bytes(32, "little") for v in vals]
+    rng = np.random.default_rng(11)
+    for _ in range(245):
+        r = bytearray(rng.bytes(32))
+        r[31] &= 0x7F
+        rs.append(bytes(r))
+    n = len(rs)
+    lib = ctypes.CDLL(LIB)
+    lib.ouro_wide_elligator2.argtypes = [ctypes.c_int, ctypes.c_char_p, ctypes.c_void_p]
+    out = ctypes.create_string_buffer(32 * n)
+    assert lib.ouro_wide_elligator2(n, b"".join(rs), out) == 0
+    bad = [i for i in range(n) if out.raw[32 * i:32 * i + 32] != O.elligator2(rs[i])]
+    assert not bad, [rs[i].hex() for i in bad[:4]]
