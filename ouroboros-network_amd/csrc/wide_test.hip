@@ -290,9 +290,46 @@ __global__ void __launch_bounds__(64) k_wide_elligator2(int n, const uint8_t* r,
 #endif
 }
 
+// One wave per input: the latency encodings' inversion (wide_inv.h
+// fe_invert_wave, the divsteps with the operand updates over the lanes) on a
+// 256-bit input reduced as fe_from_words reads it; canonical output words.
+__global__ void __launch_bounds__(64) k_wide_invert(int n, const uint32_t* z, uint32_t* out) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const int i = (int)blockIdx.x;
+  if (i >= n) return;
+  uint32_t w[8];
+#pragma unroll
+  for (int k = 0; k < 8; k++) w[k] = z[8 * (size_t)i + k];
+  const fe r = fe_invert_wave(fe_from_words(w));
+  fe_to_words(w, r);
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int k = 0; k < 8; k++) out[8 * (size_t)i + k] = w[k];
+  }
+#endif
+}
+
 }  // namespace
 
 extern "C" {
+// z^-1 mod p of n host inputs (32 bytes each) on the device, one wave each;
+// 0, -1 on bad arguments, -2 on a HIP error
+int ouro_wide_invert(int n, const uint8_t* z, uint8_t* out) {
+  if (n <= 0 || !z || !out) return -1;
+  uint32_t *d_z = nullptr, *d_o = nullptr;
+  const size_t bytes = 32 * (size_t)n;
+  int rc = 0;
+  if (hipMalloc(&d_z, bytes) != hipSuccess || hipMalloc(&d_o, bytes) != hipSuccess) rc = -2;
+  if (!rc && hipMemcpy(d_z, z, bytes, hipMemcpyHostToDevice) != hipSuccess) rc = -2;
+  if (!rc) {
+    hipLaunchKernelGGL(k_wide_invert, dim3(n), dim3(64), 0, 0, n, d_z, d_o);
+    if (hipDeviceSynchronize() != hipSuccess || hipGetLastError() != hipSuccess) rc = -2;
+  }
+  if (!rc && hipMemcpy(out, d_o, bytes, hipMemcpyDeviceToHost) != hipSuccess) rc = -2;
+  if (d_z) (void)hipFree(d_z);
+  if (d_o) (void)hipFree(d_o);
+  return rc;
+}
 // Elligator2 + encoding of n host inputs on the device (one wave each);
 // 0, -1 on bad arguments, -2 on a HIP error
 int ouro_wide_elligator2(int n, const uint8_t* r, uint8_t* out) {

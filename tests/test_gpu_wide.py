@@ -4,7 +4,8 @@ squaring chains, z^(2^252-3), doubling, addition/subtraction, [s]P against
 double-and-add, the identity, and the latency mode's [s]H item (wide_vrf.h).  One wave per case (random + edge field
 elements: p - 1, 0); csrc/wide_test.hip is a test-only library.  The
 latency items' Elligator2 and encoding are also checked against the oracle
-directly (test_wide_elligator2_matches_oracle)."""
+directly (test_wide_elligator2_matches_oracle), and their inversion against
+exact Python integers (test_wide_invert_matches_python)."""
 import ctypes
 import os
 
@@ -57,3 +58,30 @@ def test_wide_elligator2_matches_oracle(gpu_lib):
     assert lib.ouro_wide_elligator2(n, b"".join(rs), out) == 0
     bad = [i for i in range(n) if out.raw[32 * i:32 * i + 32] != O.elligator2(rs[i])]
     assert not bad, [rs[i].hex() for i in bad[:4]]
+
+
+@pytest.mark.gpu
+def test_wide_invert_matches_python(gpu_lib):
+    """The latency encodings' inversion (wide_inv.h fe_invert_wave: divsteps
+    with the operand updates on the lanes, early exit, 0 -> 0) against exact
+    Python integers, pow(z, p - 2, p), on inputs read as fe_from_words does
+    (bit 255 ignored): 0, 1, 2, p - 1, p (= 0), p + 1 .. 2^255 - 1
+    (non-canonical), powers of two and seeded random words."""
+    p = 2**255 - 19
+    vals = [0, 1, 2, 19, p - 2, p - 1, p, p + 1, p + 18, 2**255 - 1, 2**254, 2**128, 2**64 - 1]
+    rng = np.random.default_rng(12)
+    for _ in range(243):
+        vals.append(int.from_bytes(rng.bytes(32), "little"))
+    n = len(vals)
+    zb = b"".join(v.to_bytes(32, "little") for v in vals)
+    lib = ctypes.CDLL(LIB)
+    lib.ouro_wide_invert.argtypes = [ctypes.c_int, ctypes.c_char_p, ctypes.c_void_p]
+    out = ctypes.create_string_buffer(32 * n)
+    assert lib.ouro_wide_invert(n, zb, out) == 0
+    bad = []
+    for i, v in enumerate(vals):
+        z = (v & (2**255 - 1)) % p
+        want = pow(z, p - 2, p)  # 0 for z = 0, as the kernel documents
+        if int.from_bytes(out.raw[32 * i:32 * i + 32], "little") != want:
+            bad.append(hex(v))
+    assert not bad, bad[:4]
