@@ -309,9 +309,66 @@ __global__ void __launch_bounds__(64) k_wide_invert(int n, const uint32_t* z, ui
 #endif
 }
 
+// One wave per input: [s mod L]P on the wave (wide.h pw_scalarmult: the
+// latency chains' table, windows and additions) and its encoding
+// (encode1_wide), P decoded on the lane; ok[i] = 0 when P does not decode.
+__global__ void __launch_bounds__(64) k_wide_scalarmult(int n, const uint32_t* pe, const uint32_t* sc,
+                                                        uint32_t* out, int32_t* ok) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  using namespace wide;
+  const int i = (int)blockIdx.x;
+  if (i >= n) return;
+  const Lanes L = lanes();
+  uint32_t w[8], sr[8], s[8], enc[8];
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    w[k] = pe[8 * (size_t)i + k];
+    sr[k] = sc[8 * (size_t)i + k];
+  }
+  ge_p3 P;
+  const bool dec = ge_decode(&P, w, false);
+  sc_reduce256(s, sr);
+  TabW tab;
+  tab_build(tab, pw_from_p3(dec ? P : ge_p3_identity(), L), d2_wide(L), L);
+  encode1_wide(enc, pw_scalarmult(tab, s, L));
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int k = 0; k < 8; k++) out[8 * (size_t)i + k] = enc[k];
+    ok[i] = dec ? 1 : 0;
+  }
+#endif
+}
+
 }  // namespace
 
 extern "C" {
+// [s mod L]P for n host (P encoding, s) pairs on the device, one wave each;
+// 0, -1 on bad arguments, -2 on a HIP error
+int ouro_wide_scalarmult(int n, const uint8_t* pe, const uint8_t* sc, uint8_t* out, int32_t* ok) {
+  if (n <= 0 || !pe || !sc || !out || !ok) return -1;
+  uint32_t *d_p = nullptr, *d_s = nullptr, *d_o = nullptr;
+  int32_t* d_ok = nullptr;
+  const size_t bytes = 32 * (size_t)n;
+  int rc = 0;
+  if (hipMalloc(&d_p, bytes) != hipSuccess || hipMalloc(&d_s, bytes) != hipSuccess ||
+      hipMalloc(&d_o, bytes) != hipSuccess || hipMalloc(&d_ok, sizeof(int32_t) * n) != hipSuccess)
+    rc = -2;
+  if (!rc && (hipMemcpy(d_p, pe, bytes, hipMemcpyHostToDevice) != hipSuccess ||
+              hipMemcpy(d_s, sc, bytes, hipMemcpyHostToDevice) != hipSuccess))
+    rc = -2;
+  if (!rc) {
+    hipLaunchKernelGGL(k_wide_scalarmult, dim3(n), dim3(64), 0, 0, n, d_p, d_s, d_o, d_ok);
+    if (hipDeviceSynchronize() != hipSuccess || hipGetLastError() != hipSuccess) rc = -2;
+  }
+  if (!rc && (hipMemcpy(out, d_o, bytes, hipMemcpyDeviceToHost) != hipSuccess ||
+              hipMemcpy(ok, d_ok, sizeof(int32_t) * n, hipMemcpyDeviceToHost) != hipSuccess))
+    rc = -2;
+  if (d_p) (void)hipFree(d_p);
+  if (d_s) (void)hipFree(d_s);
+  if (d_o) (void)hipFree(d_o);
+  if (d_ok) (void)hipFree(d_ok);
+  return rc;
+}
 // z^-1 mod p of n host inputs (32 bytes each) on the device, one wave each;
 // 0, -1 on bad arguments, -2 on a HIP error
 int ouro_wide_invert(int n, const uint8_t* z, uint8_t* out) {

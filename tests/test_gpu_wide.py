@@ -5,7 +5,9 @@ double-and-add, the identity, and the latency mode's [s]H item (wide_vrf.h).  On
 elements: p - 1, 0); csrc/wide_test.hip is a test-only library.  The
 latency items' Elligator2 and encoding are also checked against the oracle
 directly (test_wide_elligator2_matches_oracle), and their inversion against
-exact Python integers (test_wide_invert_matches_python)."""
+exact Python integers (test_wide_invert_matches_python); the wave [s]P and
+its encoding against exact affine arithmetic, torsion components included
+(test_wide_scalarmult_matches_python)."""
 import ctypes
 import os
 
@@ -85,3 +87,40 @@ def test_wide_invert_matches_python(gpu_lib):
         if int.from_bytes(out.raw[32 * i:32 * i + 32], "little") != want:
             bad.append(hex(v))
     assert not bad, bad[:4]
+
+
+@pytest.mark.gpu
+def test_wide_scalarmult_matches_python(gpu_lib):
+    """The latency chains' [s]P on the wave (wide.h pw_scalarmult: table,
+    signed width-4 windows, additions, doublings) and encode1_wide against
+    exact affine arithmetic in Python (edge_cases.smul), s reduced mod L as
+    the kernel reads it: prime-order points, the identity, an order-8 point and
+    mixed-order points (a torsion component the chain must carry exactly),
+    scalars 0, 1, L - 1, L, L + 1, 2^256 - 1 and seeded random ones."""
+    import edge_cases as E
+
+    rng = np.random.default_rng(13)
+    rnd = lambda: int.from_bytes(rng.bytes(32), "little")  # noqa: E731
+    pts = [E.BASE, (0, 1), E.T8, ((-E.BASE[0]) % E.P, E.BASE[1])]
+    for _ in range(6):
+        pts.append(E.smul(rnd() % E.L, E.BASE))
+    pts.append(E.add(E.smul(rnd() % E.L, E.BASE), E.T8))
+    pts.append(E.add(E.BASE, E.smul(3, E.T8)))
+    scal = [0, 1, E.L - 1, E.L, E.L + 1, 2**256 - 1]
+    cases = [(pt, s) for pt in pts[:4] for s in scal]
+    for pt in pts:
+        for _ in range(3):
+            cases.append((pt, rnd()))
+    n = len(cases)
+    pe = b"".join(E.enc_pt(pt) for pt, _ in cases)
+    sc = b"".join(s.to_bytes(32, "little") for _, s in cases)
+    lib = ctypes.CDLL(LIB)
+    lib.ouro_wide_scalarmult.argtypes = [ctypes.c_int, ctypes.c_char_p, ctypes.c_char_p,
+                                         ctypes.c_void_p, ctypes.c_void_p]
+    out = ctypes.create_string_buffer(32 * n)
+    ok = np.zeros(n, dtype=np.int32)
+    assert lib.ouro_wide_scalarmult(n, pe, sc, out, ok.ctypes.data) == 0
+    assert ok.all()
+    bad = [i for i, (pt, s) in enumerate(cases)
+           if out.raw[32 * i:32 * i + 32] != E.enc_pt(E.smul(s % E.L, pt))]
+    assert not bad, [(E.enc_pt(cases[i][0]).hex(), hex(cases[i][1])) for i in bad[:3]]
