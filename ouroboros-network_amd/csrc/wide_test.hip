@@ -339,9 +339,94 @@ __global__ void __launch_bounds__(64) k_wide_scalarmult(int n, const uint32_t* p
 #endif
 }
 
+// One wave per message: the latency items' wave SHA-512 (sha512.h
+// sha512_prefixed_wave) over a 64-byte prefix (R || A) and a global-memory
+// tail of len[i] bytes (stride 1024), as the Ed25519 scalars items hash.
+__global__ void __launch_bounds__(64) k_wide_sha_prefixed(int n, const uint32_t* pre, const uint8_t* msg,
+                                                          const uint32_t* len, uint32_t* out) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const int i = (int)blockIdx.x;
+  if (i >= n) return;
+  uint32_t p[16], d[16];
+#pragma unroll
+  for (int k = 0; k < 16; k++) p[k] = pre[16 * (size_t)i + k];
+  uint64_t H[8];
+  sha512_prefixed_wave<64, 64>(H, p, ShaGlobalTail{msg + 1024 * (size_t)i}, len[i]);
+  sha512_digest_words(d, H);
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int k = 0; k < 16; k++) out[16 * (size_t)i + k] = d[k];
+  }
+#endif
+}
+// Two 130-byte messages per wave, one per half (the tail's challenge form,
+// sha512_prefixed_wave<130, 32>); msg: 33 words per message (last 2 bytes used)
+__global__ void __launch_bounds__(64) k_wide_sha130_pairs(int pairs, const uint32_t* msg, uint32_t* out) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const int i = (int)blockIdx.x;
+  if (i >= pairs) return;
+  const size_t m = 2 * (size_t)i + (threadIdx.x >> 5);
+  uint32_t hp[33], d[16];
+#pragma unroll
+  for (int k = 0; k < 33; k++) hp[k] = msg[33 * m + k];
+  uint64_t H[8];
+  sha512_prefixed_wave<130, 32>(H, hp, ShaNoTail{}, 0);
+  sha512_digest_words(d, H);
+  if ((threadIdx.x & 31u) == 0) {
+#pragma unroll
+    for (int k = 0; k < 16; k++) out[16 * m + k] = d[k];
+  }
+#endif
+}
+
 }  // namespace
 
 extern "C" {
+// SHA-512(pre_i || msg_i[0..len_i)) for n messages on the device, one wave
+// each (pre: 64 B each; msg: 1024-B stride, len_i <= 943); 0 / -1 / -2
+int ouro_wide_sha512_prefixed(int n, const uint8_t* pre, const uint8_t* msg, const uint32_t* len,
+                              uint8_t* out) {
+  if (n <= 0 || !pre || !msg || !len || !out) return -1;
+  for (int i = 0; i < n; i++)
+    if (len[i] > 943) return -1;  // the wave form's 8 blocks
+  uint32_t *d_p = nullptr, *d_l = nullptr, *d_o = nullptr;
+  uint8_t* d_m = nullptr;
+  int rc = 0;
+  if (hipMalloc(&d_p, 64 * (size_t)n) != hipSuccess || hipMalloc(&d_m, 1024 * (size_t)n) != hipSuccess ||
+      hipMalloc(&d_l, 4 * (size_t)n) != hipSuccess || hipMalloc(&d_o, 64 * (size_t)n) != hipSuccess)
+    rc = -2;
+  if (!rc && (hipMemcpy(d_p, pre, 64 * (size_t)n, hipMemcpyHostToDevice) != hipSuccess ||
+              hipMemcpy(d_m, msg, 1024 * (size_t)n, hipMemcpyHostToDevice) != hipSuccess ||
+              hipMemcpy(d_l, len, 4 * (size_t)n, hipMemcpyHostToDevice) != hipSuccess))
+    rc = -2;
+  if (!rc) {
+    hipLaunchKernelGGL(k_wide_sha_prefixed, dim3(n), dim3(64), 0, 0, n, d_p, d_m, d_l, d_o);
+    if (hipDeviceSynchronize() != hipSuccess || hipGetLastError() != hipSuccess) rc = -2;
+  }
+  if (!rc && hipMemcpy(out, d_o, 64 * (size_t)n, hipMemcpyDeviceToHost) != hipSuccess) rc = -2;
+  if (d_p) (void)hipFree(d_p);
+  if (d_m) (void)hipFree(d_m);
+  if (d_l) (void)hipFree(d_l);
+  if (d_o) (void)hipFree(d_o);
+  return rc;
+}
+// SHA-512 of 2 * pairs 130-byte messages (33 words each), two per wave; 0 / -1 / -2
+int ouro_wide_sha512_130_pairs(int pairs, const uint8_t* msg, uint8_t* out) {
+  if (pairs <= 0 || !msg || !out) return -1;
+  uint32_t *d_m = nullptr, *d_o = nullptr;
+  const size_t nm = 2 * (size_t)pairs;
+  int rc = 0;
+  if (hipMalloc(&d_m, 132 * nm) != hipSuccess || hipMalloc(&d_o, 64 * nm) != hipSuccess) rc = -2;
+  if (!rc && hipMemcpy(d_m, msg, 132 * nm, hipMemcpyHostToDevice) != hipSuccess) rc = -2;
+  if (!rc) {
+    hipLaunchKernelGGL(k_wide_sha130_pairs, dim3(pairs), dim3(64), 0, 0, pairs, d_m, d_o);
+    if (hipDeviceSynchronize() != hipSuccess || hipGetLastError() != hipSuccess) rc = -2;
+  }
+  if (!rc && hipMemcpy(out, d_o, 64 * nm, hipMemcpyDeviceToHost) != hipSuccess) rc = -2;
+  if (d_m) (void)hipFree(d_m);
+  if (d_o) (void)hipFree(d_o);
+  return rc;
+}
 // [s mod L]P for n host (P encoding, s) pairs on the device, one wave each;
 // 0, -1 on bad arguments, -2 on a HIP error
 int ouro_wide_scalarmult(int n, const uint8_t* pe, const uint8_t* sc, uint8_t* out, int32_t* ok) {

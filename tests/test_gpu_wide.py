@@ -7,7 +7,8 @@ latency items' Elligator2 and encoding are also checked against the oracle
 directly (test_wide_elligator2_matches_oracle), and their inversion against
 exact Python integers (test_wide_invert_matches_python); the wave [s]P and
 its encoding against exact affine arithmetic, torsion components included
-(test_wide_scalarmult_matches_python)."""
+(test_wide_scalarmult_matches_python); the wave SHA-512 against hashlib
+(test_wide_sha512_matches_hashlib)."""
 import ctypes
 import os
 
@@ -124,3 +125,40 @@ def test_wide_scalarmult_matches_python(gpu_lib):
     bad = [i for i, (pt, s) in enumerate(cases)
            if out.raw[32 * i:32 * i + 32] != E.enc_pt(E.smul(s % E.L, pt))]
     assert not bad, [(E.enc_pt(cases[i][0]).hex(), hex(cases[i][1])) for i in bad[:3]]
+
+
+@pytest.mark.gpu
+def test_wide_sha512_matches_hashlib(gpu_lib):
+    """The latency items' wave SHA-512 (sha512.h sha512_prefixed_wave: every
+    block's schedule on its own lane, the rounds from LDS) against hashlib:
+    a 64-byte prefix plus a global-memory tail of every length around the
+    block and padding boundaries up to the wave form's 8 blocks, and the
+    tail's two-messages-per-wave form over 130-byte challenge strings."""
+    import hashlib
+
+    rng = np.random.default_rng(14)
+    lens = sorted({0, 1, 7, 8, 46, 47, 48, 49, 63, 64, 65, 110, 111, 112, 113, 127, 128,
+                   175, 176, 177, 239, 240, 241, 367, 368, 544, 623, 624, 751, 752, 879, 880, 943})
+    n = len(lens)
+    pre = rng.bytes(64 * n)
+    msg = bytearray(1024 * n)
+    for i, ln in enumerate(lens):
+        msg[1024 * i:1024 * i + ln] = rng.bytes(ln)
+    lib = ctypes.CDLL(LIB)
+    lib.ouro_wide_sha512_prefixed.argtypes = [ctypes.c_int, ctypes.c_char_p, ctypes.c_char_p,
+                                              ctypes.c_void_p, ctypes.c_void_p]
+    ln_arr = np.array(lens, dtype=np.uint32)
+    out = ctypes.create_string_buffer(64 * n)
+    assert lib.ouro_wide_sha512_prefixed(n, pre, bytes(msg), ln_arr.ctypes.data, out) == 0
+    bad = [ln for i, ln in enumerate(lens)
+           if out.raw[64 * i:64 * i + 64]
+           != hashlib.sha512(pre[64 * i:64 * i + 64] + bytes(msg[1024 * i:1024 * i + ln])).digest()]
+    assert not bad, bad
+
+    pairs = 16
+    msgs = [rng.bytes(130) for _ in range(2 * pairs)]
+    lib.ouro_wide_sha512_130_pairs.argtypes = [ctypes.c_int, ctypes.c_char_p, ctypes.c_void_p]
+    out2 = ctypes.create_string_buffer(64 * 2 * pairs)
+    assert lib.ouro_wide_sha512_130_pairs(pairs, b"".join(m + b"\0\0" for m in msgs), out2) == 0
+    bad2 = [i for i, m in enumerate(msgs) if out2.raw[64 * i:64 * i + 64] != hashlib.sha512(m).digest()]
+    assert not bad2, bad2
