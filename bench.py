@@ -27,6 +27,7 @@ import json
 import math
 import os
 import subprocess
+import socket
 import sys
 import time
 
@@ -637,17 +638,20 @@ def _plan_phases(hb, iters: int, nonce: bool):
     """Where a window's wall time goes, to explain the latency tail (VERDICT
     r03 item 5): the plan's submit (copy into pinned staging + the launch
     calls) and wait (until the results are in the caller's buffers) timed on
-    the host, and the GPU time of the window (input copy kernel, latency
-    kernel; "gpu_graph" keeps its round-4 name) from events the plan records
-    around its launches (OURO_PLAN_TIMING; a separate pass, so the
-    headline windows carry no events).  host_gap = wall - gpu: launch latency
-    + completion wake-up + the host copies."""
+    the host, and the GPU time of the window (input copy kernel's start to
+    the last header's end; "gpu_graph" keeps its round-4 name) from
+    s_memrealtime stamps the kernels write into the plan's pinned done block
+    (OURO_PLAN_TIMING at plan create; since round 6 no runtime events: an
+    event pair per window made the runtime stall one submit in ~250 for
+    ~125 us, profiles/r06b/submit_probe.json).  host_gap = wall - gpu:
+    launch latency + completion wake-up + the host copies."""
     from ouroboros_network_amd.tpraos import HeaderPlan
 
+    from ouroboros_network_amd import _native
+
     body_bytes = int(hb.body_len.astype(np.int64).sum())
-    plan = HeaderPlan(len(hb), body_bytes)
-    old = os.environ.get("OURO_PLAN_TIMING")
-    os.environ["OURO_PLAN_TIMING"] = "1"
+    with _native.knob_env(OURO_PLAN_TIMING="1"):  # read when the plan is created
+        plan = HeaderPlan(len(hb), body_bytes)
     try:
         out = plan.run(hb, nonce=nonce)
         s = hb.c_struct(out[3] if nonce else None)
@@ -669,10 +673,6 @@ def _plan_phases(hb, iters: int, nonce: bool):
                                        ctypes.byref(lus))
             ph[k] = (t1 - t0, t2 - t1, gms.value * 1e-3, cus.value * 1e-6, lus.value * 1e-6)
     finally:
-        if old is None:
-            os.environ.pop("OURO_PLAN_TIMING", None)
-        else:
-            os.environ["OURO_PLAN_TIMING"] = old
         plan.close()
     wall = ph[:, 0] + ph[:, 1]
     gap = wall - ph[:, 2]
@@ -687,9 +687,9 @@ def _plan_phases(hb, iters: int, nonce: bool):
                                     "submit": round(ph[i, 0] * 1e6, 1),
                                     "wait": round(ph[i, 1] * 1e6, 1),
                                     "gpu_graph": round(ph[i, 2] * 1e6, 1)} for i in worst],
-            "note": "events around the window's launches (OURO_PLAN_TIMING) in a separate pass; "
-                    "host_gap = wall - gpu_graph (launch latency, completion wake-up, "
-                    "host copies)"}
+            "note": "GPU span from the kernels' s_memrealtime stamps in the plan's done block "
+                    "(OURO_PLAN_TIMING, a separate pass; no runtime events); host_gap = wall - "
+                    "gpu_graph (launch latency, completion wake-up, host copies)"}
 
 
 def _pcts(lat):
@@ -788,13 +788,10 @@ def e2e_leg(hdr, n: int, reps: int = 3):
     res = {"workload": f"configs[3] batch of {n} headers in pageable host memory, "
                        "ouro_tpraos_verify_batch (H2D + kernel + D2H)",
            "h2d_bytes": int(in_bytes), "d2h_bytes": int(129 * n)}
-    saved = os.environ.get("OURO_HOST_CHUNK")
-    try:
-        for name, chunk in (("pipelined", saved), ("one_piece", "0")):
-            if chunk is None:
-                os.environ.pop("OURO_HOST_CHUNK", None)
-            else:
-                os.environ["OURO_HOST_CHUNK"] = chunk
+    from ouroboros_network_amd import _native
+
+    for name, chunk in (("pipelined", os.environ.get("OURO_HOST_CHUNK")), ("one_piece", "0")):
+        with _native.knob_env(OURO_HOST_CHUNK=chunk):
             v, be, bl = verify_headers(hb)  # warm: device/pinned buffers grown
             t = []
             for _ in range(reps):
@@ -802,14 +799,9 @@ def e2e_leg(hdr, n: int, reps: int = 3):
                 v, be, bl = verify_headers(hb)
                 t.append(time.perf_counter() - t0)
             best = min(t)
-            res[name] = {"headers_per_s": round(n / best, 1), "ms": round(best * 1e3, 2),
-                         "equals_device_path": bool((v == dv).all() and (be == dbe).all()
-                                                    and (bl == dbl).all())}
-    finally:
-        if saved is None:
-            os.environ.pop("OURO_HOST_CHUNK", None)
-        else:
-            os.environ["OURO_HOST_CHUNK"] = saved
+        res[name] = {"headers_per_s": round(n / best, 1), "ms": round(best * 1e3, 2),
+                     "equals_device_path": bool((v == dv).all() and (be == dbe).all()
+                                                and (bl == dbl).all())}
     return res
 
 
@@ -1300,9 +1292,7 @@ def single_item_leg(ed, hdr, iters: int = 300):
     shim = _native.load_shim()
 
     def route(r):
-        old = os.environ.get("OURO_SINGLE_ITEM")
-        os.environ["OURO_SINGLE_ITEM"] = r
-        try:
+        with _native.knob_env(OURO_SINGLE_ITEM=r):
             return {
                 "ouro_ed25519_verify": lat(lambda i: lib.ouro_ed25519_verify(
                     items[i][0], items[i][1], 32, items[i][2])),
@@ -1311,22 +1301,10 @@ def single_item_leg(ed, hdr, iters: int = 300):
                 "crypto_vrf_ietfdraft03_verify (opt-in shim)": lat(
                     lambda i: shim.crypto_vrf_ietfdraft03_verify(out, vitems[i][0], vitems[i][1],
                                                                  vitems[i][2], 32))}
-        finally:
-            if old is None:
-                os.environ.pop("OURO_SINGLE_ITEM", None)
-            else:
-                os.environ["OURO_SINGLE_ITEM"] = old
 
     def lanes_route():
-        old = os.environ.get("OURO_HOST_IMPL")
-        os.environ["OURO_HOST_IMPL"] = "lanes"
-        try:
+        with _native.knob_env(OURO_HOST_IMPL="lanes"):
             return route("host")
-        finally:
-            if old is None:
-                os.environ.pop("OURO_HOST_IMPL", None)
-            else:
-                os.environ["OURO_HOST_IMPL"] = old
 
     res = {"workload": f"{iters} single-item calls, valid synthetic items, one thread",
            "routing": "single items run on the library's host path by default "
@@ -1429,7 +1407,8 @@ def main():
         from ouroboros_network_amd.shard import check_rank_devices
 
         topo = [None] * world
-        dist.all_gather_object(topo, {"rank": rank, "device": gpu, "bus_id": pci_bus_id(device)})
+        dist.all_gather_object(topo, {"rank": rank, "device": gpu, "bus_id": pci_bus_id(device),
+                                      "host": socket.gethostname()})
         check_rank_devices(topo, args.gpus, allow_shared=args.dist_backend != "nccl")
 
     from ouroboros_network_amd.shard import all_gather_results, pack_results

@@ -21,11 +21,24 @@ extern "C" {
 int ouro_debug_host_path(unsigned long long *single_items,
                          unsigned long long *recomputed_batches);
 
+/* Re-read the library's environment switches (OURO_SINGLE_ITEM,
+ * OURO_ON_DEVICE_ERROR, OURO_WIDE_SMALL_MAX, OURO_HOST_*, OURO_CBOR_*,
+ * OURO_LAT_*, OURO_PLAN_*; csrc/knobs.h).  The library reads them once, on
+ * first use, and never on a call path: a process that changes one (tests,
+ * bench.py A/B passes) calls this afterwards.  Plans keep the values they
+ * were created with. */
+void ouro_debug_reload_knobs(void);
+
 /* TIMING PROBE (bench.py latency phases) of the plan's last waited-for
- * window, when OURO_PLAN_TIMING was set in the environment at its submit (-1
- * otherwise): gpu_ms = events recorded around its launches (input copy, the
- * latency kernel, output); copy_us / launch_us = host time of submit's copy
- * into the pinned block and of the launch calls.  Any pointer may be NULL. */
+ * window, when OURO_PLAN_TIMING was set in the environment when the plan was
+ * created (-1 otherwise): gpu_ms = the window's GPU span, from the input copy
+ * kernel's start to the last header's end, read from s_memrealtime stamps the
+ * kernels write into the plan's pinned done block (no runtime events: events
+ * recorded every window made the runtime stall one submit in ~250 for ~125
+ * us); the forms without the done word (OURO_PLAN_FLAG=0 / OURO_PLAN_STAGE
+ * != 2) time it with events around the launches instead.  copy_us /
+ * launch_us = host time of submit's copy into the pinned block and of the
+ * launch calls.  Any pointer may be NULL. */
 int ouro_debug_plan_timing(ouro_tpraos_plan *plan, float *gpu_ms, float *copy_us,
                            float *launch_us);
 

@@ -6,6 +6,7 @@ library is missing or cannot load, every call raises ``NativeUnavailable``.
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
 import os
 import sys
@@ -126,6 +127,7 @@ SIGNATURES = {
                                      _P, _P, _P]),
     "ouro_debug_cbor_stats": (_I, [_P]),
     "ouro_debug_test_hooks": (_I, []),
+    "ouro_debug_reload_knobs": (None, []),
     "ouro_integrity_verify_cbor_device": (_I, [_P, _P, _SZ, _P, _P, _SZ, ctypes.c_uint64, _P,
                                                _SZ, _P, _P]),
     "ouro_sum6kes_verify_batch": (_I, [_SZ, _P, _P, _P, _P, _P, _P, _P]),
@@ -231,6 +233,36 @@ TEST_LIB_PATH = os.path.join(_HERE, "lib", "libouro_verify_test.so")
 def test_hooks() -> bool:
     """True when the loaded library is the test-hook build (OURO_TEST_HOOKS)."""
     return bool(load().ouro_debug_test_hooks())
+
+
+def reload_knobs() -> None:
+    """Re-read the library's environment switches (csrc/knobs.h): the library
+    reads them once and never on a call path, so a process that changes one
+    calls this afterwards (ouro_debug_reload_knobs)."""
+    if _lib is not None:
+        _lib.ouro_debug_reload_knobs()
+
+
+@contextlib.contextmanager
+def knob_env(**env):
+    """Set environment switches (None = unset) for a block, the library
+    re-reading them on entry and exit."""
+    saved = {k: os.environ.get(k) for k in env}
+    try:
+        for k, v in env.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = str(v)
+        reload_knobs()
+        yield
+    finally:
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+        reload_knobs()
 
 
 def check(rc: int, what: str) -> int:

@@ -18,6 +18,7 @@
 
 #include "host_fast.h"
 #include "host_path.h"
+#include "knobs.h"
 #include "launch.h"
 #include "leader.h"
 #include "task_pool.h"
@@ -101,10 +102,7 @@ const BaseTables& base_tables() {
 namespace {
 // OURO_HOST_IMPL=lanes: the kernels' lane routines compiled for the host (the
 // round-4 host path) instead of ouro_cpu -- an A/B switch (bench.py single_item)
-bool host_lanes() {
-  const char* e = getenv("OURO_HOST_IMPL");
-  return e && strcmp(e, "lanes") == 0;
-}
+bool host_lanes() { return ouro_knobs::get().host_lanes.load(std::memory_order_relaxed) != 0; }
 }  // namespace
 
 namespace ouro_host {
@@ -122,7 +120,7 @@ const int32_t* btab() {
 int threads_for(size_t n) {
   const int cpus = ouro_pool::usable_cpus();
   int cap = 64;
-  if (const char* e = getenv("OURO_HOST_THREADS")) cap = std::max(1, atoi(e));
+  if (const int t = ouro_knobs::get().host_threads.load(std::memory_order_relaxed)) cap = std::max(1, t);
   const size_t by_items = (n + 15) / 16;
   return (int)std::max<size_t>(1, std::min<size_t>({(size_t)cpus, (size_t)cap, by_items}));
 }

@@ -22,6 +22,7 @@
 #include "../../include/ouro_verify.h"
 #include "cbor.h"
 #include "host_path.h"
+#include "knobs.h"
 #include "launch.h"
 #include "leader.h"
 #include "task_pool.h"
@@ -718,7 +719,7 @@ int plan(DeviceState* ds, int id, size_t n, hipStream_t stream, int* grid, int32
 #define OURO_TEST_HOOKS 0
 #endif
 #if OURO_TEST_HOOKS
-bool injected_device_error() { return getenv("OURO_TEST_DEVICE_ERROR") != nullptr; }
+bool injected_device_error() { return ouro_knobs::get().test_device_error.load(std::memory_order_relaxed); }
 #else
 constexpr bool injected_device_error() { return false; }
 #endif
@@ -737,8 +738,7 @@ int launch_check() {
 // device memory, so they return the error.
 std::atomic<unsigned long long> g_host_single{0}, g_host_recompute{0};
 bool recompute_on_error() {
-  const char* e = getenv("OURO_ON_DEVICE_ERROR");
-  return !(e && strcmp(e, "fail") == 0);
+  return !ouro_knobs::get().on_device_error_fail.load(std::memory_order_relaxed);
 }
 template <class F>
 int or_host(int rc, F&& recompute) {
@@ -753,30 +753,27 @@ int or_host(int rc, F&& recompute) {
 // Single items run on the host path (one GPU round trip is ~220-420 us, the
 // host path ~1.5x libsodium); OURO_SINGLE_ITEM=gpu sends them to the device
 // (A/B, bench.py single_item).
-bool single_on_gpu() {
-  const char* e = getenv("OURO_SINGLE_ITEM");
-  return e && strcmp(e, "gpu") == 0;
-}
+bool single_on_gpu() { return ouro_knobs::get().single_on_gpu.load(std::memory_order_relaxed); }
 
 // Small batches (n <= OURO_WIDE_SMALL_MAX, default 2048; 0 = never) run one
 // item per wave (kernels_lat.hip k_ed25519_wide / k_vrf03_wide): a single
 // item's latency is then one wave's chain, not one lane's.
-size_t wide_small_max() {
-  if (const char* e = getenv("OURO_WIDE_SMALL_MAX")) return (size_t)strtoull(e, nullptr, 0);
-  return 2048;
-}
+size_t wide_small_max() { return ouro_knobs::get().wide_small_max.load(std::memory_order_relaxed); }
 int wide_grid(size_t n) { return (int)std::min<size_t>(n, 8192); }
 
 // ---- device-pointer launches (shared by the host-buffer and device APIs) ----
 // The split kernels (pre / dsm at OURO_DSM_WAVES / post) instead of the
-// one-pass k_tpraos_verify, k_ed25519_verify and k_sum6kes_verify:
-// OURO_SPLIT=0/1 in the environment, read per launch (default
-// OURO_SPLIT_DEFAULT).
+// one-pass k_tpraos_verify, k_ed25519_verify and k_sum6kes_verify (measured
+// and rejected): fixed at compile time in the product
+// (OURO_SPLIT_DEFAULT); only the test-hook build lets OURO_SPLIT=1 select them
+// (tests/test_gpu_variants.py keeps them bit-exact).
 #ifndef OURO_SPLIT_DEFAULT
 #define OURO_SPLIT_DEFAULT 0
 #endif
 bool split_launch() {
-  if (const char* e = getenv("OURO_SPLIT")) return atoi(e) != 0;
+#if OURO_TEST_HOOKS
+  if (ouro_knobs::get().split.load(std::memory_order_relaxed)) return true;
+#endif
   return OURO_SPLIT_DEFAULT != 0;
 }
 // One Ed25519-shaped item per task: chunks of 4 resident grids of the pre
@@ -923,32 +920,20 @@ int launch_leader(hipStream_t st, size_t n, const uint8_t* beta, const uint64_t*
 // as many CUs (own L1, TA and instruction fetch per wave) instead of packing
 // four onto each CU.
 int lat_block() {
-  if (const char* e = getenv("OURO_LAT_BLOCK")) {
-    const int v = atoi(e);
-    if (v == 64 || v == 128 || v == 256) return v;
-  }
-  return kLatBlock;
+  const int v = ouro_knobs::get().lat_block.load(std::memory_order_relaxed);
+  return v == 64 || v == 128 || v == 256 ? v : kLatBlock;
 }
 
 // Latency-mode cores on lane quads (1, default) or one lane per core
 // (OURO_LAT_QUAD=0, for A/B).
-int lat_quad() {
-  if (const char* e = getenv("OURO_LAT_QUAD")) return atoi(e) != 0;
-  return 1;
-}
+int lat_quad() { return ouro_knobs::get().lat_quad.load(std::memory_order_relaxed) != 0; }
 
 // Latency-mode cores run on one wave each (wide_cores.h): a mask over
 // tpraos.h HdrCore + kCoreGe/kCoreGl, default all eight (OURO_LAT_WIDE; 0 =
 // every core on lane quads, for A/B).
-int lat_wide_mask() {
-  if (const char* e = getenv("OURO_LAT_WIDE")) return (int)(strtol(e, nullptr, 0) & 0xff);
-  return 0xff;
-}
+int lat_wide_mask() { return ouro_knobs::get().lat_wide.load(std::memory_order_relaxed) & 0xff; }
 
-int lat_fuse() {
-  if (const char* e = getenv("OURO_LAT_FUSE")) return atoi(e) != 0;
-  return 1;
-}
+int lat_fuse() { return ouro_knobs::get().lat_fuse.load(std::memory_order_relaxed) != 0; }
 
 // latency mode: eight cores per header (x4 lanes in quad mode), then the
 // finish; n and the option bits read from d_n[0..1].
@@ -985,9 +970,13 @@ int lat_shape(size_t n_cap, LatShape* s) {
   const size_t wide_waves = (size_t)(fused ? lat_fused_items_host() : nwide) * n_cap;
   const size_t wide_blocks = (wide_waves * 64 + blk - 1) / blk;
   const size_t quad_items = (size_t)(kLatCores - nwide) * n_cap;
-  // timing probe: OURO_LAT_SKIP = mask of cores left out (verdicts then wrong)
-  const char* skip_env = getenv("OURO_LAT_SKIP");
-  const int skip = skip_env ? (int)(strtol(skip_env, nullptr, 0) & 0xff) : 0;
+  // timing probe: OURO_LAT_SKIP = mask of cores left out (verdicts then
+  // wrong), honoured by the test-hook build only
+#if OURO_TEST_HOOKS
+  const int skip = ouro_knobs::get().lat_skip.load(std::memory_order_relaxed) & 0xff;
+#else
+  const int skip = 0;
+#endif
   s->g1 = (int)wide_blocks + grid(quad_items << (quad ? 2 : 0), kCores);
   s->g2 = grid(n_cap << (quad ? 2 : 0), kFinish);
   s->blk = blk;
@@ -995,7 +984,7 @@ int lat_shape(size_t n_cap, LatShape* s) {
   s->wide_lanes = (int)(wide_blocks * blk / 64);
   s->fused = fused;
   s->flags = (uint32_t)(quad | (skip << 8) | (wmask << 16) | (fused ? 1 << 24 : 0) |
-                        (getenv("OURO_LAT_STAMPS") ? 1 << 25 : 0));
+                        (ouro_knobs::get().lat_stamps.load(std::memory_order_relaxed) ? 1 << 25 : 0));
   s->btab = ds->btab;
   return OURO_OK;
 }
@@ -1381,8 +1370,8 @@ int pipe_chunk(PipeSlot& p, const ouro_tpraos_batch* b, size_t lo, size_t m, con
 // headers per chunk: one full grid of the header kernel (OURO_HOST_CHUNK
 // overrides; 0 = the whole batch in one piece)
 size_t host_chunk(DeviceState* ds) {
-  if (const char* e = getenv("OURO_HOST_CHUNK")) return (size_t)strtoull(e, nullptr, 10);
-  return (size_t)ds->max_blocks[kHdr] * kBlock;
+  const long long v = ouro_knobs::get().host_chunk.load(std::memory_order_relaxed);
+  return v >= 0 ? (size_t)v : (size_t)ds->max_blocks[kHdr] * kBlock;
 }
 
 int hdr_batch_pipelined(const ouro_tpraos_batch* b, size_t chunk, const HdrOut& o) {
@@ -1823,12 +1812,10 @@ size_t raw_out_bytes(const RawCall& c, const RawOut& o, size_t m) {
 }
 
 // Every span inside raw (as ouro_tpraos_pack_cbor demands), and the chunks.
-size_t env_size(const char* name, size_t dflt, size_t lo, size_t hi) {
-  if (const char* e = getenv(name)) {
-    const size_t v = (size_t)strtoull(e, nullptr, 10);
-    if (v >= lo && v <= hi) return v;
-  }
-  return dflt;
+// a raw-CBOR knob (knobs.h; 0 = unset) if inside [lo, hi], else the default
+size_t knob_size(const std::atomic<size_t>& k, size_t dflt, size_t lo, size_t hi) {
+  const size_t v = k.load(std::memory_order_relaxed);
+  return v && v >= lo && v <= hi ? v : dflt;
 }
 
 // Headers in chunk j when `left` headers (this chunk's included) remain.
@@ -1847,7 +1834,7 @@ size_t raw_chunk_target(size_t j, size_t left, size_t per, bool ramp) {
 
 int raw_chunks(const RawCall& c, size_t per, std::vector<RawChunk>* out) {
   out->clear();
-  const bool ramp = env_size("OURO_CBOR_RAMP", 0, 0, 1) != 0;
+  const bool ramp = ouro_knobs::get().cbor_ramp.load(std::memory_order_relaxed) == 1;
   RawChunk k{0, 0, 0};
   size_t target = raw_chunk_target(0, c.n, per, ramp);
   for (size_t i = 0; i < c.n; i++) {
@@ -1997,13 +1984,13 @@ int raw_run(const RawCall& c, const std::vector<RawChunk>& chunks) {
   // chunks in flight: the header kernel wants ~3 grids of work queued (6 x
   // 64 K headers); the Sum6KES kernel is PCIe-bound, 4 suffice
   // (profiles/r05a/cbor_sweep.jsonl)
-  const int S = (int)env_size("OURO_CBOR_SLOTS", c.kind == kRawKes ? 4 : 6, 1, kRawMaxSlots);
+  const int S = (int)knob_size(ouro_knobs::get().cbor_slots, c.kind == kRawKes ? 4 : 6, 1, kRawMaxSlots);
   for (int k = 0; k < S; k++) {
     RawSlot& s = p.s[k];
     if (!s.st) OURO_HIP(hipStreamCreateWithFlags(&s.st, hipStreamNonBlocking));
     if (!s.done) OURO_HIP(hipEventCreateWithFlags(&s.done, hipEventDisableTiming));
   }
-  const int width = (int)env_size("OURO_CBOR_COPY_THREADS", 8, 1, 64);
+  const int width = (int)knob_size(ouro_knobs::get().cbor_copy_threads, 8, 1, 64);
   size_t ci = 0;
   for (; ci < chunks.size() && !rc; ci++) {
     RawSlot& s = p.s[ci % S];
@@ -2078,7 +2065,7 @@ int raw_verify(const RawCall& c) {
   if ((c.ea == nullptr) != (c.la == nullptr))
     return fail(OURO_EINVAL, "give both VRF input arrays or neither");
   std::vector<RawChunk> chunks;
-  const size_t per = env_size("OURO_CBOR_CHUNK", 65536, 256, (size_t)1 << 24);
+  const size_t per = knob_size(ouro_knobs::get().cbor_chunk, 65536, 256, (size_t)1 << 24);
   int rc = raw_chunks(c, per, &chunks);
   if (rc) return rc;
   return or_host(raw_run(c, chunks), [&] { return raw_host(c); });
@@ -2121,6 +2108,8 @@ int ouro_tpraos_verify_cbor(const uint8_t* raw, size_t raw_bytes, const uint64_t
 // DIAGNOSTIC: 1 in the test-hook build (lib/libouro_verify_test.so), 0 in the product
 int ouro_debug_test_hooks(void) { return OURO_TEST_HOOKS; }
 
+void ouro_debug_reload_knobs(void) { ouro_knobs::reload(); }
+
 // DIAGNOSTIC: the calling thread's last raw-CBOR call (ms and counts)
 int ouro_debug_cbor_stats(double* out6) {
   if (!out6) return fail(OURO_EINVAL, "null buffer");
@@ -2162,8 +2151,17 @@ int ouro_leader_check_batch_device(void* stream, size_t n, const uint8_t* beta,
 // A plan's window read straight from its pinned input block by a copy kernel
 // (OURO_PLAN_STAGE >= 1; A/B against the DMA copy node): one 16-B load per
 // thread, every load of the window in flight at once.
+// stamp (a plan's timing probe, OURO_PLAN_TIMING; else null): the copy's start
+// in s_memrealtime ticks (100 MHz), written to the plan's pinned done block.
+__device__ __forceinline__ void plan_stamp(uint64_t* stamp) {
+  if (stamp && blockIdx.x == 0 && threadIdx.x == 0)
+    __hip_atomic_store(stamp, (uint64_t)__builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+}
 __global__ void __launch_bounds__(256) k_plan_stage(const uint4* __restrict__ src,
-                                                    uint4* __restrict__ dst, size_t n16) {
+                                                    uint4* __restrict__ dst, size_t n16,
+                                                    uint64_t* stamp) {
+  plan_stamp(stamp);
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n16) dst[i] = src[i];
 }
@@ -2179,7 +2177,8 @@ struct PlanRanges {
 };
 __global__ void __launch_bounds__(256) k_plan_stage_ranges(const uint4* __restrict__ src,
                                                            uint4* __restrict__ dst,
-                                                           PlanRanges r) {
+                                                           PlanRanges r, uint64_t* stamp) {
+  plan_stamp(stamp);
   uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   for (uint32_t k = 0; k < r.count; k++) {
     if (t < r.len16[k]) {
@@ -2229,8 +2228,15 @@ struct ouro_tpraos_plan {
   bool failed = false;           // its launch failed: wait recomputes it on the host path
   // TIMING PROBE (OURO_PLAN_TIMING set at submit; bench.py latency phases):
   // events around the window's launches on the plan's stream
+  // (without the done word, the A/B forms: events around the launches; with
+  // it, the kernels' own s_memrealtime stamps in the done block -- events
+  // recorded every window made the runtime stall one submit in ~250 for
+  // ~125 us, profiles/r06b/submit_probe.json)
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   bool timed = false;
+  uint64_t* stamps = nullptr;  // device view of the done block's stamps (timing + flag)
+  const volatile uint64_t* stamps_host = nullptr;
+  bool timing = false;  // OURO_PLAN_TIMING at create
   float last_gpu_ms = -1.0f;
   float copy_us = -1.0f, launch_us = -1.0f;  // host side of its last submit
   int stage = 2;  // OURO_PLAN_STAGE at capture (plan_build)
@@ -2280,11 +2286,12 @@ int plan_enqueue(ouro_tpraos_plan* p) {
     for (uint32_t k = 0; k < p->ranges.count; k++) units += p->ranges.len16[k];
     hipLaunchKernelGGL(k_plan_stage_ranges, dim3((units + 255) / 256), dim3(256), 0, p->st,
                        static_cast<const uint4*>(p->hin), reinterpret_cast<uint4*>(p->d_in),
-                       p->ranges);
+                       p->ranges, p->stamps);
   } else if (p->stage == 1 || p->stage == 2) {
     const size_t n16 = p->in_bytes / 16;  // in_bytes is a multiple of 16
     hipLaunchKernelGGL(k_plan_stage, dim3((unsigned)((n16 + 255) / 256)), dim3(256), 0, p->st,
-                       static_cast<const uint4*>(p->hin), reinterpret_cast<uint4*>(p->d_in), n16);
+                       static_cast<const uint4*>(p->hin), reinterpret_cast<uint4*>(p->d_in), n16,
+                       p->stamps);
   } else if (p->stage <= 0) {
     OURO_HIP(hipMemcpyAsync(p->d_in, p->h_in, p->in_bytes, hipMemcpyHostToDevice, p->st));
   }
@@ -2336,10 +2343,12 @@ int plan_build(ouro_tpraos_plan* p) {
   // ~5 us each, the rest is the graph's node-to-node dispatch); 3 = no input
   // copy either: the latency kernel reads the pinned block over PCIe (A/B).
   // OURO_PLAN_GRAPH=1: capture them into a hipGraph (the form before r04m).
-  if (const char* e = getenv("OURO_PLAN_STAGE")) p->stage = atoi(e);
-  if (const char* e = getenv("OURO_PLAN_SPIN")) p->spin = atoi(e);
-  if (const char* e = getenv("OURO_PLAN_GRAPH")) p->use_graph = atoi(e) != 0;
-  if (const char* e = getenv("OURO_PLAN_TRIM")) p->trim = atoi(e) != 0;
+  const ouro_knobs::Knobs& kn = ouro_knobs::get();
+  p->stage = kn.plan_stage.load(std::memory_order_relaxed);
+  p->spin = kn.plan_spin.load(std::memory_order_relaxed);
+  p->use_graph = kn.plan_graph.load(std::memory_order_relaxed) != 0;
+  p->trim = kn.plan_trim.load(std::memory_order_relaxed) != 0;
+  p->timing = kn.plan_timing.load(std::memory_order_relaxed) != 0;
   if (p->stage >= 1) OURO_HIP(hipHostGetDevicePointer(&p->hin, p->h_in, 0));
   uint8_t* d = p->stage >= 3 ? static_cast<uint8_t*>(p->hin) : p->d_in;
   ouro_tpraos_batch& b = p->dev_batch;
@@ -2380,14 +2389,20 @@ int plan_build(ouro_tpraos_plan* p) {
   p->dbl = dbl;
   if ((rc = lat_shape(p->cap, &p->shape))) return rc;
   {
-    const char* e = getenv("OURO_PLAN_FLAG");
-    p->flag = p->stage == 2 && p->shape.fused && !(e && atoi(e) == 0);
+    p->flag = p->stage == 2 && p->shape.fused && kn.plan_flag.load(std::memory_order_relaxed) != 0;
     if (p->flag) {
       uint8_t* w = p->h_out + p->out_bytes - 64;
       void* wd = nullptr;
       OURO_HIP(hipHostGetDevicePointer(&wd, w, 0));
       p->done_dev = static_cast<uint32_t*>(wd);
       p->done_host = reinterpret_cast<const volatile uint32_t*>(w);
+      if (p->timing) {
+        // the done block: word 0 the done word; u64 1 the latency kernel's
+        // start, u64 2 the last tail's end, u64 3 the copy kernel's start
+        p->stamps = reinterpret_cast<uint64_t*>(static_cast<uint8_t*>(wd) + 8);
+        p->stamps_host = reinterpret_cast<const volatile uint64_t*>(w + 8);
+        p->shape.flags |= 1u << 26;
+      }
     }
   }
   if (!p->use_graph) return OURO_OK;
@@ -2507,7 +2522,7 @@ int ouro_tpraos_plan_submit(ouro_tpraos_plan* p, const ouro_tpraos_batch* b) {
       b->ocert_sigma, b->kes_t,           b->kes_sig,     w.span() ? b->body + w.lo : nullptr,
       w.off.data(),  b->body_len,         b->eta_output,  b->leader_output, b->slot,
       b->epoch_nonce};
-  p->timed = getenv("OURO_PLAN_TIMING") != nullptr;
+  p->timed = p->timing;
   const auto tc0 = std::chrono::steady_clock::now();
   if (b->slot) src[kFEtaAlpha] = src[kFLeaderAlpha] = nullptr;  // derived on the device
   else src[kFEpochNonce] = nullptr;
@@ -2540,7 +2555,7 @@ int ouro_tpraos_plan_submit(ouro_tpraos_plan* p, const ouro_tpraos_batch* b) {
   if (p->timed)
     p->copy_us = std::chrono::duration<float, std::micro>(std::chrono::steady_clock::now() - tc0).count();
 #if OURO_TEST_HOOKS
-  if (p->gen && getenv("OURO_TEST_PLAN_POISON") && (rc = plan_poison(p))) return rc;
+  if (p->gen && ouro_knobs::get().test_plan_poison.load() && (rc = plan_poison(p))) return rc;
 #endif
   // every launch a new generation, so no counter an earlier launch left
   // behind (one that never completed) is ever counted again
@@ -2556,15 +2571,16 @@ int ouro_tpraos_plan_submit(ouro_tpraos_plan* p, const ouro_tpraos_batch* b) {
   // output block (not the done word) set to a sentinel before the launch, so
   // a wait that returned before the kernel's stores were visible would hand
   // back the sentinel instead of the oracle's verdicts and outputs
-  if (getenv("OURO_TEST_PLAN_SENTINEL")) memset(p->h_out, 0xEE, p->out_bytes - 64);
+  if (ouro_knobs::get().test_plan_sentinel.load()) memset(p->h_out, 0xEE, p->out_bytes - 64);
 #endif
   const bool injected = injected_device_error();
   hipError_t e = hipSetDevice(p->dev);
-  if (p->timed && !p->ev0 && e == hipSuccess) {
+  const bool events = p->timed && !p->stamps;
+  if (events && !p->ev0 && e == hipSuccess) {
     e = hipEventCreate(&p->ev0);
     if (e == hipSuccess) e = hipEventCreate(&p->ev1);
   }
-  if (p->timed && e == hipSuccess) e = hipEventRecord(p->ev0, p->st);
+  if (events && e == hipSuccess) e = hipEventRecord(p->ev0, p->st);
   const auto tl0 = std::chrono::steady_clock::now();
   if (e == hipSuccess && !injected) {
     if (p->exec) e = hipGraphLaunch(p->exec, p->st);
@@ -2572,7 +2588,7 @@ int ouro_tpraos_plan_submit(ouro_tpraos_plan* p, const ouro_tpraos_batch* b) {
   }
   if (p->timed)
     p->launch_us = std::chrono::duration<float, std::micro>(std::chrono::steady_clock::now() - tl0).count();
-  if (p->timed && e == hipSuccess) e = hipEventRecord(p->ev1, p->st);
+  if (events && e == hipSuccess) e = hipEventRecord(p->ev1, p->st);
   if (e != hipSuccess || injected) {
     fail(OURO_EDEVICE, std::string("plan launch: ") +
                            (e != hipSuccess ? hipGetErrorString(e) : "injected device error"));
@@ -2607,7 +2623,7 @@ int ouro_tpraos_plan_wait(ouro_tpraos_plan* p, uint8_t* verdict, uint8_t* beta_e
         __builtin_ia32_pause();
       }
       std::atomic_thread_fence(std::memory_order_acquire);
-      if (e == hipSuccess && p->timed) e = hipEventSynchronize(p->ev1);
+      if (e == hipSuccess && p->timed && !p->stamps) e = hipEventSynchronize(p->ev1);
     } else if (e == hipSuccess && p->spin) {
       // poll the stream instead of the runtime's wait, which may sleep on the
       // completion interrupt
@@ -2625,7 +2641,13 @@ int ouro_tpraos_plan_wait(ouro_tpraos_plan* p, uint8_t* verdict, uint8_t* beta_e
     return or_host(rc, [&] { return ouro_host::hdr_batch(&hb, verdict, beta_eta, beta_leader); });
   }
   p->last_gpu_ms = -1.0f;
-  if (p->timed) (void)hipEventElapsedTime(&p->last_gpu_ms, p->ev0, p->ev1);
+  if (p->timed && p->stamps) {
+    // the copy kernel's start to the last header's end, 100 MHz ticks
+    const uint64_t t0 = p->stamps_host[0], t2 = p->stamps_host[2];
+    p->last_gpu_ms = t2 > t0 ? (float)((double)(t2 - t0) * 1e-5) : -1.0f;
+  } else if (p->timed) {
+    (void)hipEventElapsedTime(&p->last_gpu_ms, p->ev0, p->ev1);
+  }
   const uint8_t* o = p->h_out + align16(p->cap);
   memcpy(verdict, p->h_out, n);
   if (beta_eta) memcpy(beta_eta, o, 64 * n);

@@ -475,7 +475,14 @@ __global__ void __launch_bounds__(kBlock, OURO_LAT_WAVES) k_tpraos_cores(ouro_tp
   const uint32_t wmask = ((uint32_t)mode >> 16) & 0xffu;
   const int nwide = __builtin_popcount(wmask);
   const bool fused = ((uint32_t)mode >> 24) & 1u;
+  // bit 26: a plan's timing probe (OURO_PLAN_TIMING): s_memrealtime at the
+  // start (first workgroup) and at the window's end into the done block
+  const bool stamps = (((uint32_t)mode >> 26) & 1u) && done;
   const size_t gtid = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (stamps && gtid == 0)
+    __hip_atomic_store(reinterpret_cast<uint64_t*>(done) + 2,
+                       (uint64_t)__builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
   const size_t wide_lanes = (size_t)wide_waves * 64;
   if (gtid < wide_lanes && fused) {  // wave-uniform
     const size_t wv = gtid >> 6, i = wv / kFusedItems;
@@ -496,8 +503,13 @@ __global__ void __launch_bounds__(kBlock, OURO_LAT_WAVES) k_tpraos_cores(ouro_tp
       if ((threadIdx.x & 63u) == 0) {
         const uint32_t prev =
             __hip_atomic_fetch_add(win_ctr, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_SYSTEM);
-        if (prev + 1u == (uint32_t)n)
+        if (prev + 1u == (uint32_t)n) {
+          if (stamps)
+            __hip_atomic_store(reinterpret_cast<uint64_t*>(done) + 3,
+                               (uint64_t)__builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
           __hip_atomic_store(done, gen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
       }
     }
     return;

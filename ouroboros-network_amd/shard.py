@@ -91,10 +91,14 @@ def verify_sharded(batch, verify: Callable = None, group=None):
 def check_rank_devices(infos, expected_world: int, allow_shared: bool = False) -> None:
     """The multi-GPU line is only valid on a real N-GPU world (VERDICT r04 item
     6): `infos` is one dict per rank (all_gather_object of
-    {"rank", "device", "bus_id"}); raise RuntimeError unless the process group
-    has exactly `expected_world` ranks, their ranks are 0..N-1, and -- unless
-    `allow_shared` (the gloo rehearsal with ranks on one GPU) -- every rank
-    drives a distinct GPU (distinct PCI bus ids)."""
+    {"rank", "device", "bus_id", "host"}); raise RuntimeError unless the
+    process group has exactly `expected_world` ranks, their ranks are
+    0..N-1, and -- unless `allow_shared` (the gloo rehearsal with ranks on one
+    GPU) -- every rank drives a distinct GPU.  A GPU is identified by its
+    node AND its PCI bus id (or local index when torch exposes no bus id):
+    every node of a multi-node world has the same bus ids, so ranks on
+    different hosts never share a GPU.  `host` defaults to one
+    node for callers that do not record it."""
     world = len(infos)
     if world != expected_world:
         raise RuntimeError(f"world size {world} != --gpus {expected_world}")
@@ -103,7 +107,8 @@ def check_rank_devices(infos, expected_world: int, allow_shared: bool = False) -
         raise RuntimeError(f"ranks {ranks} are not 0..{world - 1}")
     if allow_shared:
         return
-    ids = [str(i.get("bus_id") or f"device{i['device']}") for i in infos]
+    ids = [(str(i.get("host") or ""), str(i.get("bus_id") or f"device{i['device']}"))
+           for i in infos]
     if len(set(ids)) != world:
-        dup = sorted({x for x in ids if ids.count(x) > 1})
+        dup = sorted({"/".join(x).lstrip("/") for x in ids if ids.count(x) > 1})
         raise RuntimeError(f"ranks share GPUs {dup}: a {world}-GPU line needs {world} devices")

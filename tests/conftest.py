@@ -32,6 +32,34 @@ def _hook_tests_need_the_test_build(request):
         pytest.skip("needs the test-hook build (run by tests/test_gpu_hooks.py)")
 
 
+def _reload_knobs():
+    from ouroboros_network_amd import _native
+
+    _native.reload_knobs()
+
+
+@pytest.fixture
+def monkeypatch():
+    """pytest's monkeypatch, whose environment changes the library sees: it
+    reads its switches once (csrc/knobs.h) and is told to re-read them after
+    every setenv / delenv and after the undo."""
+    mp = pytest.MonkeyPatch()
+    setenv, delenv = mp.setenv, mp.delenv
+
+    def _setenv(name, value, prepend=None):
+        setenv(name, value, prepend)
+        _reload_knobs()
+
+    def _delenv(name, raising=True):
+        delenv(name, raising)
+        _reload_knobs()
+
+    mp.setenv, mp.delenv = _setenv, _delenv
+    yield mp
+    mp.undo()
+    _reload_knobs()
+
+
 def _recomputed(lib):
     import ctypes
 

@@ -258,3 +258,61 @@ def test_header_batch_saturates_kes_t():
     assert hb.kes_t.dtype == np.uint32
     assert list(hb.kes_t) == [5, 0xFFFFFFFF, 0xFFFFFFFF]
     assert list(hb.slice(1, 3).kes_t) == [0xFFFFFFFF, 0xFFFFFFFF]
+
+
+def test_no_getenv_on_call_paths():
+    """the library reads its environment switches once
+    (csrc/knobs.cpp, on first use or ouro_debug_reload_knobs) -- no other
+    translation unit of the product calls getenv, so no call path reads the
+    environment (a setenv racing a getenv is undefined behaviour, and a stray
+    variable could switch kernels between calls).  numa.cpp's sysfs root and
+    the task pool's size are read once at their first use (function-local
+    statics), the opt-in shims' error mode once per process."""
+    csrc = os.path.join(ROOT, "ouroboros-network_amd", "csrc")
+    product = ["kernels.hip", "kernels_lat.hip", "host_path.hip", "pack.cpp"]
+    for f in product:
+        text = re.sub(r"//[^\n]*", "", open(os.path.join(csrc, f)).read())
+        assert "getenv" not in text, f"{f} calls getenv"
+    knobs = open(os.path.join(csrc, "knobs.cpp")).read()
+    assert len(set(re.findall(r"\"(OURO_[A-Z_0-9]+)\"", knobs))) >= 25
+    # the split kernels (rejected A/B) are not selectable in the product
+    kern = open(os.path.join(csrc, "kernels.hip")).read()
+    body = kern[kern.index("bool split_launch()"):]
+    body = body[:body.index("\n}\n")]
+    assert "#if OURO_TEST_HOOKS" in body
+
+
+def test_knobs_read_once_and_on_reload(tmp_path):
+    """A switch changed after the library's first call is NOT seen until
+    ouro_debug_reload_knobs: OURO_SINGLE_ITEM=gpu routes single items to the
+    (here absent) device -- an error -- only after the reload."""
+    import subprocess
+    import sys
+
+    import torch
+
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is present: the device route would succeed")
+    code = r"""
+import ctypes, os, sys
+sys.path.insert(0, %r)
+from ouroboros_network_amd import _native
+lib = _native.load()
+sys.path.insert(0, %r)
+import oracle_ffi as O
+pk, sig, msg = O.synth_ed25519(1, first=5)
+args = (sig[0].ctypes.data, msg[0].ctypes.data, 32, pk[0].ctypes.data)
+assert lib.ouro_ed25519_verify(*args) == 0
+os.environ["OURO_SINGLE_ITEM"] = "gpu"
+assert lib.ouro_ed25519_verify(*args) == 0      # not re-read
+lib.ouro_debug_reload_knobs()
+assert lib.ouro_ed25519_verify(*args) != 0      # the device route, no device here
+del os.environ["OURO_SINGLE_ITEM"]
+lib.ouro_debug_reload_knobs()
+assert lib.ouro_ed25519_verify(*args) == 0
+print("ok")
+""" % (ROOT, os.path.join(ROOT, "tests"))
+    env = {k: v for k, v in os.environ.items() if not k.startswith("OURO_")}
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0 and "ok" in r.stdout, r.stdout + r.stderr

@@ -77,15 +77,25 @@ def _check(raws, spkp, ea=None, la=None, epoch_nonce=None, triple=None):
 
 @pytest.fixture
 def small_chunks():
-    """The pipeline cut into many chunks (each env var is read per call)."""
+    """The pipeline cut into many chunks: `set(CHUNK=..., SLOTS=..., RAMP=...)`
+    sets OURO_CBOR_* and has the library re-read its switches (knobs.h)."""
+    from ouroboros_network_amd import _native
+
     saved = {k: os.environ.get(k) for k in ("OURO_CBOR_CHUNK", "OURO_CBOR_SLOTS",
                                              "OURO_CBOR_RAMP")}
-    yield
+
+    def set_(**kw):
+        for k, v in kw.items():
+            os.environ["OURO_CBOR_" + k] = str(v)
+        _native.reload_knobs()
+
+    yield set_
     for k, v in saved.items():
         if v is None:
             os.environ.pop(k, None)
         else:
             os.environ[k] = v
+    _native.reload_knobs()
 
 
 @pytest.mark.gpu
@@ -123,9 +133,7 @@ def _ramp_chunks(n, per, ramp=True):
                                               (1024, 2, 1), (1024, 2, 0)])
 def test_golden_in_small_chunks(gpu_lib, kats, small_chunks, chunk, slots, ramp):
     raws, ea, la = _golden_cases(kats, stride=2)
-    os.environ["OURO_CBOR_CHUNK"] = str(chunk)
-    os.environ["OURO_CBOR_SLOTS"] = str(slots)
-    os.environ["OURO_CBOR_RAMP"] = str(ramp)
+    small_chunks(CHUNK=chunk, SLOTS=slots, RAMP=ramp)
     _check(raws, SPKP, ea, la)
     stats = np.zeros(6)
     gpu_lib.ouro_debug_cbor_stats(stats.ctypes.data)
@@ -178,7 +186,7 @@ def test_buffer_layouts(gpu_lib, kats, small_chunks):
         at += len(raws[k])
     buf = np.frombuffer(b"".join(parts), np.uint8)
     ln = np.array([len(r) for r in raws], np.uint32)
-    os.environ["OURO_CBOR_CHUNK"] = "256"
+    small_chunks(CHUNK=256)
     v, st = _check(raws, SPKP, ea, la, triple=(buf, off, ln))
     # one span twice (rows 0 and 1 the same header)
     off2, ln2 = off.copy(), ln.copy()
@@ -197,8 +205,7 @@ def test_integrity_in_small_chunks(gpu_lib, kats, small_chunks):
     raws, _, _ = _golden_cases(kats, stride=3)
     want_ok, want_st = H.verify_integrity_cbor(raws, SPKP, host=True)
     for chunk, slots in ((256, 2), (4096, 6)):
-        os.environ["OURO_CBOR_CHUNK"] = str(chunk)
-        os.environ["OURO_CBOR_SLOTS"] = str(slots)
+        small_chunks(CHUNK=chunk, SLOTS=slots)
         ok, st = H.verify_integrity_cbor(raws, SPKP)
         np.testing.assert_array_equal(ok, want_ok)
         np.testing.assert_array_equal(st, want_st)
@@ -242,9 +249,7 @@ def test_device_error_recomputes_on_the_host_path(gpu_lib, kats, small_chunks):
     if not _native.test_hooks():
         pytest.skip("the library was built without test hooks")
     raws, ea, la = _golden_cases(kats, stride=11)
-    os.environ["OURO_TEST_DEVICE_ERROR"] = "1"
-    os.environ["OURO_CBOR_CHUNK"] = "256"
-    try:
+    with _native.knob_env(OURO_TEST_DEVICE_ERROR="1", OURO_CBOR_CHUNK="256"):
         _check(raws, SPKP, ea, la)
         nraws, _ = C.seeded_raw(kats, b"\x07" * 32, 8, spkp=SPKP)
         _check(nraws, SPKP, epoch_nonce=b"\x07" * 32)
@@ -253,8 +258,6 @@ def test_device_error_recomputes_on_the_host_path(gpu_lib, kats, small_chunks):
         np.testing.assert_array_equal(ok, hok)
         msg = gpu_lib.ouro_last_error().decode()
         assert "recomputed on the host path" in msg, msg
-    finally:
-        os.environ.pop("OURO_TEST_DEVICE_ERROR", None)
 
 
 @pytest.mark.gpu

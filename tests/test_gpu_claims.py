@@ -137,11 +137,10 @@ def _poisoned_submit():
     """The plan test hook (kernels.hip plan_poison; the test build only),
     reached through the environment: every submit while it is set first
     poisons the counters."""
-    os.environ["OURO_TEST_PLAN_POISON"] = "1"
-    try:
+    from ouroboros_network_amd import _native
+
+    with _native.knob_env(OURO_TEST_PLAN_POISON="1"):
         yield
-    finally:
-        del os.environ["OURO_TEST_PLAN_POISON"]
 
 
 @pytest.mark.hooks
@@ -189,13 +188,14 @@ def test_plan_results_never_stale(gpu_lib, kats):
     b = HC.seeded(kats, bytes(range(32)), copies=4).slice(0, 40)
     wa, wb = O.tpraos_verify_batch_nonce(a), O.tpraos_verify_batch_nonce(b)
     plan = T.HeaderPlan(64, 64 * 1400)
-    os.environ["OURO_TEST_PLAN_SENTINEL"] = "1"
+    from ouroboros_network_amd import _native
+
     try:
-        for k in range(200):
-            batch, want = (a, wa) if k % 2 == 0 else (b, wb)
-            got = plan.run(batch, nonce=True)
-            for g, w in zip(got, want):
-                np.testing.assert_array_equal(g, w)
+        with _native.knob_env(OURO_TEST_PLAN_SENTINEL="1"):
+            for k in range(200):
+                batch, want = (a, wa) if k % 2 == 0 else (b, wb)
+                got = plan.run(batch, nonce=True)
+                for g, w in zip(got, want):
+                    np.testing.assert_array_equal(g, w)
     finally:
-        del os.environ["OURO_TEST_PLAN_SENTINEL"]
         plan.close()

@@ -8,6 +8,7 @@ item 8): a process that inherits those variables is unaffected by them.  In
 this (parent) process the marked tests skip themselves (conftest.py).
 """
 import os
+import re
 import subprocess
 import sys
 
@@ -38,4 +39,9 @@ def test_hook_tests_on_the_test_build(gpu_lib):
         cwd=ROOT, env=env, capture_output=True, text=True, timeout=900)
     tail = (r.stdout + r.stderr)[-4000:]
     assert r.returncode == 0, tail
-    assert " passed" in r.stdout and " skipped" not in r.stdout.split("\n")[-2], tail
+    # the summary line wherever pytest puts it: tests passed and
+    # none of the selected ones skipped
+    summary = [ln for ln in r.stdout.splitlines() if re.search(r"\d+ passed", ln)]
+    assert summary, tail
+    assert int(re.search(r"(\d+) passed", summary[-1]).group(1)) >= 10, tail
+    assert not re.search(r"\d+ skipped", summary[-1]), tail

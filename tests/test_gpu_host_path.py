@@ -27,18 +27,11 @@ from edge_cases import ed25519_edge_cases, vrf_edge_cases
 pytestmark = [pytest.mark.gpu, pytest.mark.device_error]
 
 
-@contextlib.contextmanager
 def env(**kv):
-    old = {k: os.environ.get(k) for k in kv}
-    os.environ.update({k: str(v) for k, v in kv.items()})
-    try:
-        yield
-    finally:
-        for k, v in old.items():
-            if v is None:
-                os.environ.pop(k, None)
-            else:
-                os.environ[k] = v
+    """the switches set for a block, the library re-reading them (knobs.h)"""
+    from ouroboros_network_amd import _native
+
+    return _native.knob_env(**kv)
 
 
 def recomputed(lib):

@@ -237,13 +237,10 @@ def single_route(request):
     """Single items on both routes (VERDICT r04 hygiene): the host path (the
     default since round 4) and the GPU (OURO_SINGLE_ITEM=gpu), so the -m gpu
     set exercises the device's single-item route too."""
-    old = os.environ.get("OURO_SINGLE_ITEM")
-    os.environ["OURO_SINGLE_ITEM"] = request.param
-    yield request.param
-    if old is None:
-        os.environ.pop("OURO_SINGLE_ITEM", None)
-    else:
-        os.environ["OURO_SINGLE_ITEM"] = old
+    from ouroboros_network_amd import _native
+
+    with _native.knob_env(OURO_SINGLE_ITEM=request.param):
+        yield request.param
 
 
 def test_single_item_abi(gpu_lib, kats, single_route):

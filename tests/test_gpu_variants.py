@@ -2,7 +2,9 @@
 the GPU (their measurements: DESIGN.md §4 "Measured design alternatives"):
 
 * OURO_SPLIT=1 -- the split kernels (pre / dsm at 4 waves per SIMD / post)
-  for headers, Ed25519 and Sum6KES (rejected on time, kept bit-exact);
+  for headers, Ed25519 and Sum6KES (rejected on time, kept bit-exact); the
+  product fixes the choice at compile time, so these run on the test-hook
+  build (tests/test_gpu_hooks.py);
 * OURO_PLAN_STAGE=0 / 1 / 2 / 3 -- a latency plan's window copies (2, the
   default: copy kernel in, results written by the latency kernel straight
   into the pinned block), with and without the eta nonce output;
@@ -30,6 +32,7 @@ def _corrupt(rng, a, frac=8):
     return idx
 
 
+@pytest.mark.hooks  # the product fixes OURO_SPLIT at compile time
 def test_split_headers_match_oracle(gpu_lib, kats, monkeypatch):
     from ouroboros_network_amd import tpraos as T
 
@@ -48,6 +51,7 @@ def test_split_headers_match_oracle(gpu_lib, kats, monkeypatch):
         np.testing.assert_array_equal(g, w)
 
 
+@pytest.mark.hooks  # the product fixes OURO_SPLIT at compile time
 def test_split_ed25519_and_kes_match_oracle(gpu_lib, monkeypatch):
     from ouroboros_network_amd import Ed25519DSIGN, Sum6KES
 

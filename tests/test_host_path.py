@@ -35,25 +35,19 @@ LIB = os.path.join(ROOT, "ouroboros-network_amd", "lib", "libouro_verify.so")
 def lib(request):
     from ouroboros_network_amd import _native
 
-    old = os.environ.get("OURO_HOST_IMPL")
-    os.environ["OURO_HOST_IMPL"] = request.param
-    yield _native.load()
-    if old is None:
-        os.environ.pop("OURO_HOST_IMPL", None)
-    else:
-        os.environ["OURO_HOST_IMPL"] = old
+    lib = _native.load()
+    with _native.knob_env(OURO_HOST_IMPL=request.param):
+        yield lib
 
 
 @pytest.fixture(params=["fast", "lanes"])
 def impl(request):
     """the host path's implementation for tests that call through Python"""
-    old = os.environ.get("OURO_HOST_IMPL")
-    os.environ["OURO_HOST_IMPL"] = request.param
-    yield request.param
-    if old is None:
-        os.environ.pop("OURO_HOST_IMPL", None)
-    else:
-        os.environ["OURO_HOST_IMPL"] = old
+    from ouroboros_network_amd import _native
+
+    _native.load()
+    with _native.knob_env(OURO_HOST_IMPL=request.param):
+        yield request.param
 
 
 def test_host_entries_check_their_spans(lib):

@@ -194,6 +194,23 @@ def _topology_worker(rank, world, port, out_dir, shared):
         json.dump(res, f)
 
 
+def test_rank_devices_across_nodes():
+    """two nodes have the same PCI bus ids and local indices; a
+    world spanning them is valid (a GPU is (host, bus id)), while two ranks
+    on one host and one bus id still share a GPU."""
+    from ouroboros_network_amd.shard import check_rank_devices
+
+    two_nodes = [{"rank": r, "device": r % 2, "bus_id": f"0000:{5 + r % 2:02x}:00.0",
+                  "host": f"node{r // 2}"} for r in range(4)]
+    check_rank_devices(two_nodes, 4)
+    no_bus = [{"rank": r, "device": 0, "bus_id": None, "host": f"node{r}"} for r in range(2)]
+    check_rank_devices(no_bus, 2)
+    same = [dict(two_nodes[0]), dict(two_nodes[1]), dict(two_nodes[2]), dict(two_nodes[3])]
+    same[2]["host"] = "node0"
+    with pytest.raises(RuntimeError, match="share GPUs"):
+        check_rank_devices(same, 4)
+
+
 @pytest.mark.parametrize("world", [2, 3])
 @pytest.mark.parametrize("shared", [False, True])
 def test_bench_rank_device_checks_gloo(tmp_path, world, shared):
