@@ -1106,7 +1106,7 @@ def integrity_leg(n: int, npools: int, device, reps: int = 3):
                                       "note": "host slicer + PCIe + kernel + D2H"}}
 
 
-def cbor_abi_leg(n: int, npools: int, device, reps: int = 3):
+def cbor_abi_leg(n: int, npools: int, device, reps: int = 3, multi_devices=None):
     """Raw wire CBOR in PAGEABLE host memory -> verdicts in ONE C-ABI call, no
     torch in the timed region: what
     the reference's bulk callers -- ChainDB suffix re-validation
@@ -1119,6 +1119,10 @@ def cbor_abi_leg(n: int, npools: int, device, reps: int = 3):
       tpraos     ouro_tpraos_verify_cbor (the raw-CBOR pipeline: gather into
                  pinned staging, upload, device slicer, header kernel, results)
       integrity  ouro_integrity_verify_cbor on the same bytes (Sum6KES only)
+    and, as res["inproc_cbor"], the one-process multi-device forms
+    (ouro_tpraos_verify_cbor_multi / ouro_integrity_verify_cbor_multi) over
+    `multi_devices` -- every visible device; [0, 0] on a one-GPU box, two
+    pooled workers sharing it.
     Wall clock around the ctypes call; never `value` (PCIe-inclusive)."""
     import torch
 
@@ -1155,6 +1159,33 @@ def cbor_abi_leg(n: int, npools: int, device, reps: int = 3):
                        "host memory, node configuration (mkSeed on the device from each "
                        "header's slot and eta0), one C-ABI call each",
            "raw_bytes_per_header": rl}
+    devs = np.ascontiguousarray(multi_devices or [0], np.int32)
+
+    def tpraos_multi():
+        _native.check(lib.ouro_tpraos_verify_cbor_multi(
+            P(devs), int(devs.size), P(buf), buf.size, P(off), P(ln), n, 129600, P(e0), None,
+            None, P(status), P(verdict), P(be), P(bl), P(en)), "ouro_tpraos_verify_cbor_multi")
+
+    def integrity_multi():
+        _native.check(lib.ouro_integrity_verify_cbor_multi(
+            P(devs), int(devs.size), P(buf), buf.size, P(off), P(ln), n, 129600, P(status),
+            P(verdict)), "ouro_integrity_verify_cbor_multi")
+
+    multi = {"devices": devs.tolist(),
+             "note": "one process, contiguous shards on pooled NUMA-bound workers, one per "
+                     "listed device (SURVEY.md §8(e)); on a one-GPU box [0, 0] (two shards "
+                     "sharing the GPU)"}
+    for name, fn, ok in (("tpraos", tpraos_multi, lambda: ((verdict & 0x3F) == 0x3F).all()),
+                         ("integrity", integrity_multi, lambda: (verdict == 1).all())):
+        fn()
+        verdict[:] = 0
+        ts = []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            fn()
+            ts.append(time.perf_counter() - t0)
+        multi[name] = {"headers_per_s": round(n / min(ts), 1), "ms": round(min(ts) * 1e3, 2),
+                       "all_valid": bool(ok() and (status == 0).all())}
     for name, fn, ok in (("tpraos", tpraos, lambda: ((verdict & 0x3F) == 0x3F).all()),
                          ("integrity", integrity, lambda: (verdict == 1).all())):
         fn()  # warm: pinned staging and device buffers grown, pool threads started
@@ -1172,6 +1203,7 @@ def cbor_abi_leg(n: int, npools: int, device, reps: int = 3):
                      "chunks": int(st[k][3]), "slots": int(st[k][4]),
                      "copy_threads": int(st[k][5]),
                      "all_valid": bool(ok() and (status == 0).all())}
+    res["inproc_cbor"] = multi
     return res
 
 
@@ -1200,6 +1232,12 @@ def byron_leg(n: int, threads: int, reps: int = 3):
     tp = min(_timed(lambda: B.pack_byron_cbor(arg, magic, nthreads=threads)) for _ in range(reps))
     v, st = B.verify_byron_cbor(arg, magic)  # warm
     tv = min(_timed(lambda: B.verify_byron_cbor(arg, magic)) for _ in range(reps))
+    import torch
+
+    ndev = torch.cuda.device_count()
+    mdevs = list(range(ndev)) if ndev > 1 else [0, 0]
+    vm, _ = B.verify_byron_cbor(arg, magic, devices=mdevs)  # warm
+    tm = min(_timed(lambda: B.verify_byron_cbor(arg, magic, devices=mdevs)) for _ in range(reps))
     m = min(n, 4096)
     t0 = time.perf_counter()
     for r in raws[:m]:
@@ -1209,8 +1247,12 @@ def byron_leg(n: int, threads: int, reps: int = 3):
             "boundary_headers": int((st == B.PACK_EBB).sum()),
             "pack_headers_per_s": round(n / tp, 1), "pack_threads": threads,
             "verify_cbor_headers_per_s": round(n / tv, 1),
+            "verify_cbor_multi": {"devices": mdevs, "headers_per_s": round(n / tm, 1),
+                                  "equals_one_device": bool((vm == v).all())},
             "python_slicer_headers_per_s": round(m / tpy, 1),
-            "note": "golden Byron headers repeated; pageable host memory in, verdicts out"}
+            "note": "golden Byron headers repeated; pageable host memory in, verdicts out; "
+                    "since round 6 on the raw-CBOR pipeline (pinned staging, device Byron "
+                    "slicer, ByronDSIGN kernel, 4 chunks in flight)"}
 
 
 def _timed(fn) -> float:
@@ -1673,7 +1715,12 @@ def main():
                 out["inproc"] = {"error": str(e)}
         if not args.no_e2e and world == 1:
             try:
-                out["cbor_abi"] = cbor_abi_leg(n, args.pools, device)
+                # the one-process multi-device entries over every visible
+                # device ([0, 0] on a one-GPU box: two pooled workers)
+                ndev = torch.cuda.device_count()
+                mdevs = list(range(ndev)) if ndev > 1 else [0, 0]
+                out["cbor_abi"] = cbor_abi_leg(n, args.pools, device, multi_devices=mdevs)
+                out["inproc_cbor"] = out["cbor_abi"].pop("inproc_cbor")
             except Exception as e:  # noqa: BLE001
                 out["cbor_abi"] = {"error": str(e)}
         if not args.no_e2e and world == 1:
@@ -1683,7 +1730,7 @@ def main():
                 out["integrity_cbor"] = {"error": str(e)}
         if not args.no_e2e and world == 1:
             try:
-                out["byron_cbor"] = byron_leg(1 << 18, cpu["usable"])
+                out["byron_cbor"] = byron_leg(1 << 20, cpu["usable"])
             except Exception as e:  # noqa: BLE001
                 out["byron_cbor"] = {"error": str(e)}
         if not args.no_latency and world == 1:

@@ -342,7 +342,15 @@ int ouro_integrity_verify_cbor(const uint8_t *raw, size_t raw_bytes, const uint6
  * in flight, default 6 -- 4 for ouro_integrity_verify_cbor --, at most 8;
  * OURO_CBOR_COPY_THREADS gather threads, default 8).  Synchronous; a device error recomputes the batch on the host
  * path.  OURO_EINVAL for a span outside raw_bytes, NULLs, a zero period or
- * only one of the two alpha arrays. */
+ * only one of the two alpha arrays.
+ * Footprint: the pipeline's buffers belong to the calling
+ * thread's pooled context and are kept for its next call -- per slot pinned
+ * staging of ~1.125 x the chunk's raw bytes, device buffers for the raw
+ * bytes, the slicer's arena and the results, and the kernel's scratch; at the
+ * default 65,536-header chunk of ~1 KB headers about 75 MB pinned and 180 MB
+ * of device memory per slot in use (6 slots for headers, 4 for integrity),
+ * once per context that has made such a call.  OURO_CBOR_CHUNK and
+ * OURO_CBOR_SLOTS shrink it. */
 int ouro_tpraos_verify_cbor(const uint8_t *raw, size_t raw_bytes, const uint64_t *off,
                             const uint32_t *len, size_t n, uint64_t slots_per_kes_period,
                             const uint8_t *epoch_nonce, const uint8_t *eta_alpha,
@@ -408,6 +416,12 @@ int ouro_byron_pack_cbor(const uint8_t *raw, size_t raw_bytes, const uint64_t *o
 int ouro_byron_verify_cbor(const uint8_t *raw, size_t raw_bytes, const uint64_t *off,
                            const uint32_t *len, size_t n, int64_t protocol_magic,
                            uint8_t *status, uint8_t *verdict);
+/* (How ouro_byron_verify_cbor runs, since round 6: on the raw-CBOR pipeline
+ * of ouro_tpraos_verify_cbor -- chunks gathered into pinned NUMA-local
+ * staging, the device Byron slicer (the same cbor_byron.h parse as
+ * ouro_byron_pack_cbor) and the ByronDSIGN Ed25519 kernel per chunk, 4
+ * chunks in flight; a device error recomputes the batch on the host path.
+ * OURO_EINVAL as for ouro_byron_pack_cbor.) */
 
 /* The host-side UPDN fold (ledger-specs; the per-header step of
  * SL.updateChainDepState after the crypto): for i = 0..n-1
@@ -436,9 +450,14 @@ int ouro_tpraos_verify_batch_lowlat(const ouro_tpraos_batch *b, uint8_t *verdict
  * listing of that device) -- with its own streams and pinned staging (the
  * pipelined path of ouro_tpraos_verify_batch), writing straight into the
  * caller's buffers (no collective is needed inside one process).  A device
- * may be listed more than once (two pipelines on one GPU).  Calls are
- * serialised process-wide; the first shard error is returned after every
- * shard has finished.  Same results as ouro_tpraos_verify_batch. */
+ * may be listed more than once (two pipelines on one GPU).  The workers are
+ * pooled per device: a call borrows one per shard and returns it when every
+ * shard has finished, so concurrent callers (ChainSync windows beside
+ * ChainDB's suffix re-validation) run at once on workers of their own --
+ * nothing is serialised process-wide since round 6.  The first shard error
+ * is returned after every shard has finished (a shard's device error is
+ * recomputed on the host path like any host-buffer batch).  Same results as
+ * ouro_tpraos_verify_batch. */
 int ouro_device_count(void);
 /* NUMA placement (each GPU's pinned staging NUMA-local).
  * ouro_device_numa_node: the node of the device's PCI function in sysfs
@@ -454,6 +473,34 @@ int ouro_device_numa_node(int device);
 int ouro_bind_thread_to_device(int device);
 int ouro_tpraos_verify_batch_multi(const ouro_tpraos_batch *b, const int *devices, int ndev,
                                    uint8_t *verdict, uint8_t *beta_eta, uint8_t *beta_leader);
+/* The raw-CBOR entries over several GPUs of one process -- what the bulk
+ * callers of an 8-GPU node hold: ChainDB's re-validation of a stored suffix
+ * (ouroboros-consensus/src/Ouroboros/Consensus/Storage/ChainDB/Impl/
+ * LgrDB.hs:350-368) and ImmutableDB / VolatileDB integrity
+ * (.../Storage/ImmutableDB/Impl/Validation.hs:358-365,
+ * .../Storage/VolatileDB/Impl/Parser.hs:66-85).  Arguments and results as
+ * ouro_tpraos_verify_cbor / ouro_integrity_verify_cbor /
+ * ouro_byron_verify_cbor, plus the device list (NULL: every visible
+ * device; a device may be listed more than once).  Headers are cut into
+ * contiguous shards of ceil(n / ndev), shard k runs the one-device pipeline
+ * (chunks, pinned NUMA-local staging, several chunks in flight) on a pooled
+ * worker of devices[k] bound to that GPU's NUMA node, and writes straight into
+ * the caller's buffers.  Every span is checked before any shard starts
+ * (OURO_EINVAL); OURO_ENODEV for a device index outside the visible ones. */
+int ouro_tpraos_verify_cbor_multi(const int *devices, int ndev, const uint8_t *raw,
+                                  size_t raw_bytes, const uint64_t *off, const uint32_t *len,
+                                  size_t n, uint64_t slots_per_kes_period,
+                                  const uint8_t *epoch_nonce, const uint8_t *eta_alpha,
+                                  const uint8_t *leader_alpha, uint8_t *status, uint8_t *verdict,
+                                  uint8_t *beta_eta, uint8_t *beta_leader, uint8_t *eta_nonce);
+int ouro_integrity_verify_cbor_multi(const int *devices, int ndev, const uint8_t *raw,
+                                     size_t raw_bytes, const uint64_t *off, const uint32_t *len,
+                                     size_t n, uint64_t slots_per_kes_period, uint8_t *status,
+                                     uint8_t *verdict);
+int ouro_byron_verify_cbor_multi(const int *devices, int ndev, const uint8_t *raw,
+                                 size_t raw_bytes, const uint64_t *off, const uint32_t *len,
+                                 size_t n, int64_t protocol_magic, uint8_t *status,
+                                 uint8_t *verdict);
 
 /* A plan for repeated fixed-capacity batches: pinned staging, device buffers
  * and the latency kernel's launch shape fixed at create; each run issues the

@@ -126,6 +126,11 @@ SIGNATURES = {
     "ouro_tpraos_verify_cbor": (_I, [_P, _SZ, _P, _P, _SZ, ctypes.c_uint64, _P, _P, _P, _P, _P,
                                      _P, _P, _P]),
     "ouro_debug_cbor_stats": (_I, [_P]),
+    "ouro_tpraos_verify_cbor_multi": (_I, [_P, _I, _P, _SZ, _P, _P, _SZ, ctypes.c_uint64, _P, _P,
+                                           _P, _P, _P, _P, _P, _P]),
+    "ouro_integrity_verify_cbor_multi": (_I, [_P, _I, _P, _SZ, _P, _P, _SZ, ctypes.c_uint64, _P,
+                                              _P]),
+    "ouro_byron_verify_cbor_multi": (_I, [_P, _I, _P, _SZ, _P, _P, _SZ, ctypes.c_int64, _P, _P]),
     "ouro_debug_test_hooks": (_I, []),
     "ouro_debug_reload_knobs": (None, []),
     "ouro_integrity_verify_cbor_device": (_I, [_P, _P, _SZ, _P, _P, _SZ, ctypes.c_uint64, _P,

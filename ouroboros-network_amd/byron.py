@@ -370,16 +370,29 @@ def pack_byron_cbor(raw_headers, protocol_magic: Union[int, str],
         status=status[:n], _keep=(arena, buf))
 
 
-def verify_byron_cbor(raw_headers, protocol_magic: Union[int, str]):
+def verify_byron_cbor(raw_headers, protocol_magic: Union[int, str], devices=None):
     """Raw Byron headers -> (verdict bool array, status array) in one call
-    (ouro_byron_verify_cbor): a regular header is valid when its block
-    signature verifies, an epoch-boundary header always (PBFT.hs:327-328)."""
+    (ouro_byron_verify_cbor: the raw-CBOR pipeline -- pinned staging, the
+    device Byron slicer, the ByronDSIGN kernel): a regular header is valid
+    when its block signature verifies, an epoch-boundary header always
+    (PBFT.hs:327-328).  devices (a list of device indices, or "all"):
+    ouro_byron_verify_cbor_multi, contiguous shards over those GPUs."""
     lib = _native.load()
     buf, off, ln = _raw_arg(raw_headers)
     n = int(off.size)
     status = np.zeros(max(n, 1), np.uint8)
     verdict = np.zeros(max(n, 1), np.uint8)
-    if n:
+    if n and devices is not None:
+        d = None if devices == "all" else np.ascontiguousarray(list(devices), np.int32)
+        if d is not None and d.size == 0:
+            raise ValueError("devices: at least one")
+        rc = lib.ouro_byron_verify_cbor_multi(None if d is None else ptr(d),
+                                              0 if d is None else int(d.size), ptr(buf),
+                                              buf.size, ptr(off), ptr(ln), n,
+                                              _magic_arg(protocol_magic), ptr(status),
+                                              ptr(verdict))
+        _native.check(rc, "ouro_byron_verify_cbor_multi")
+    elif n:
         rc = lib.ouro_byron_verify_cbor(ptr(buf), buf.size, ptr(off), ptr(ln), n,
                                         _magic_arg(protocol_magic), ptr(status), ptr(verdict))
         _native.check(rc, "ouro_byron_verify_cbor")

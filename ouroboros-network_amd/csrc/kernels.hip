@@ -9,6 +9,7 @@
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
+#include <functional>
 #include <cstdio>
 #include <cstring>
 #include <map>
@@ -21,6 +22,7 @@
 
 #include "../../include/ouro_verify.h"
 #include "cbor.h"
+#include "cbor_byron.h"
 #include "host_path.h"
 #include "knobs.h"
 #include "launch.h"
@@ -380,6 +382,31 @@ __global__ void __launch_bounds__(kBlock) k_tpraos_pack(const uint8_t* __restric
                      ? (uint8_t)OURO_PACK_ESPAN
                      : cbor::pack_one(raw, o0, l0, spkp, o, i);
     if (st != OURO_PACK_OK) cbor::zero_row(o, i);
+    status[i] = st;
+  }
+}
+
+// The Byron slicer (cbor_byron.h byron_pack_one, the host slicer's parse) on
+// the device, one lane per header, over a chunk staged densely by raw_stage:
+// header i's bytes at off[i] = the lengths' prefix sum, so its message slot
+// (len + kByronMsgExtra bytes, ouro_byron_pack_cbor's layout) starts at
+// off[i] + kByronMsgExtra * i.  A rejected row is zeroed (msg_len 0).
+__global__ void __launch_bounds__(kBlock) k_byron_pack(const uint8_t* __restrict__ raw,
+                                                       size_t raw_bytes,
+                                                       const uint64_t* __restrict__ off,
+                                                       const uint32_t* __restrict__ len, size_t n,
+                                                       int64_t magic, cbor::ByronOut o,
+                                                       uint8_t* __restrict__ status) {
+  const size_t tid = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const size_t nth = (size_t)gridDim.x * blockDim.x;
+  for (size_t i = tid; i < n; i += nth) {
+    const uint64_t o0 = off[i];
+    const uint32_t l0 = len[i];
+    o.msg_off[i] = o0 + cbor::kByronMsgExtra * i;
+    uint8_t st = (o0 > raw_bytes || raw_bytes - o0 < l0)
+                     ? (uint8_t)OURO_PACK_ESPAN
+                     : cbor::byron_pack_one(raw, o0, l0, magic, o, i);
+    if (st != OURO_PACK_OK) cbor::byron_zero_row(o, i);
     status[i] = st;
   }
 }
@@ -1194,25 +1221,6 @@ int ouro_byron_ed25519_verify_batch(size_t n, const uint8_t* pk, const uint8_t* 
   });
 }
 
-int ouro_byron_verify_cbor(const uint8_t* raw, size_t raw_bytes, const uint64_t* off,
-                           const uint32_t* len, size_t n, int64_t protocol_magic,
-                           uint8_t* status, uint8_t* verdict) {
-  if (n == 0) return OURO_OK;
-  if (!status || !verdict || !len) return fail(OURO_EINVAL, "null argument");
-  const size_t nb = ouro_byron_pack_bytes(n, len);
-  std::unique_ptr<uint8_t[]> arena(new (std::nothrow) uint8_t[nb]);  // not zeroed: the slicer writes every row
-  if (!arena) return fail(OURO_EDEVICE, "ouro_byron_verify_cbor: out of host memory");
-  ouro_byron_batch b;
-  int rc = ouro_byron_pack_cbor(raw, raw_bytes, off, len, n, protocol_magic, arena.get(), nb, &b,
-                                status, 0);
-  if (rc) return fail(rc, "ouro_byron_pack_cbor: bad arguments");
-  // rejected rows are zero with msg_len 0; their verdicts are masked below
-  if ((rc = ouro_byron_ed25519_verify_batch(n, b.pk, b.sig, b.msg, b.msg_off, b.msg_len, verdict)))
-    return rc;
-  for (size_t i = 0; i < n; i++)
-    verdict[i] = status[i] == OURO_PACK_EBB ? 1 : (status[i] == OURO_PACK_OK && verdict[i]);
-  return OURO_OK;
-}
 
 int ouro_vrf03_verify_batch(size_t n, const uint8_t* pk, const uint8_t* proof, const uint8_t* alpha,
                             const uint64_t* alpha_off, const uint32_t* alpha_len, uint8_t* beta,
@@ -1754,7 +1762,7 @@ namespace {
 constexpr size_t a16(size_t x) { return (x + 15) & ~(size_t)15; }
 constexpr size_t kRawChunkBytes = (size_t)96 << 20;
 
-enum RawKind { kRawHdr = 0, kRawKes = 1 };
+enum RawKind { kRawHdr = 0, kRawKes = 1, kRawByron = 2 };
 struct RawCall {
   RawKind kind;
   const uint8_t* raw;
@@ -1768,6 +1776,7 @@ struct RawCall {
   uint8_t* status;
   uint8_t* verdict;
   uint8_t *be, *bl, *nonce;      // optional outputs (header kind)
+  int64_t magic = -1;            // Byron: the configured ProtocolMagicId (-1: each header's)
 };
 struct RawChunk {
   size_t lo, m, bytes;
@@ -1804,7 +1813,7 @@ RawOut raw_out(size_t m) {
 }
 // bytes of the result block copied back
 size_t raw_out_bytes(const RawCall& c, const RawOut& o, size_t m) {
-  if (c.kind == kRawKes) return o.verdict + m;
+  if (c.kind != kRawHdr) return o.verdict + m;
   if (c.nonce) return o.slot;
   if (c.bl) return o.nonce;
   if (c.be) return o.bl;
@@ -1917,12 +1926,32 @@ int raw_launch(RawSlot& s, const RawCall& c, const RawChunk& k) {
   uint8_t* din = static_cast<uint8_t*>(s.d_in.p);
   uint8_t* dout = static_cast<uint8_t*>(s.d_out.p);
   OURO_HIP(hipMemcpyAsync(din, s.h_in, L.total, hipMemcpyHostToDevice, s.st));
+  const size_t blocks = std::min<size_t>((k.m + kBlock - 1) / kBlock, 4096);
+  if (c.kind == kRawByron) {
+    // the device Byron slicer into the slot's arena, then the Ed25519 kernel
+    // with ByronDSIGN acceptance (cardano-crypto: SURVEY.md App. B.5)
+    const cbor::ByronLayout bl = cbor::byron_layout(k.m, k.bytes + cbor::kByronMsgExtra * k.m);
+    if ((rc = ensure(s.d_arena, bl.total + 64))) return rc;
+    const cbor::ByronOut o = cbor::byron_arena_out(cbor::arena_base(s.d_arena.p), bl);
+    hipLaunchKernelGGL(k_byron_pack, dim3((unsigned)blocks), dim3(kBlock), 0, s.st, din + L.raw,
+                       k.bytes, reinterpret_cast<const uint64_t*>(din + L.off),
+                       reinterpret_cast<const uint32_t*>(din + L.len), k.m, c.magic, o,
+                       dout + O.status);
+    if ((rc = launch_check())) return rc;
+    if ((rc = launch_ed(s.st, k.m, o.pk, o.sig, o.msg, o.msg_off, o.msg_len, dout + O.verdict, 1)))
+      return rc;
+    OURO_HIP(hipMemcpyAsync(s.h_out, dout, back, hipMemcpyDeviceToHost, s.st));
+    OURO_HIP(hipEventRecord(s.done, s.st));
+    s.lo = k.lo;
+    s.m = k.m;
+    s.busy = true;
+    return OURO_OK;
+  }
   uint64_t* dslot = reinterpret_cast<uint64_t*>(dout + O.slot);
   const bool seeds = c.kind == kRawHdr && !alphas;
   const cbor::Out o = cbor::arena_out(cbor::arena_base(s.d_arena.p), k.m, seeds ? dslot : nullptr,
                                       nullptr);
   const uint8_t* draw = din + L.raw;
-  const size_t blocks = std::min<size_t>((k.m + kBlock - 1) / kBlock, 4096);
   hipLaunchKernelGGL(k_tpraos_pack, dim3((unsigned)blocks), dim3(kBlock), 0, s.st, draw, k.bytes,
                      reinterpret_cast<const uint64_t*>(din + L.off),
                      reinterpret_cast<const uint32_t*>(din + L.len), k.m, c.spkp, o,
@@ -1962,6 +1991,13 @@ int raw_drain(RawSlot& s, const RawCall& c) {
   const uint8_t* st = s.h_out + O.status;
   const uint8_t* v = s.h_out + O.verdict;
   memcpy(c.status + s.lo, st, s.m);
+  if (c.kind == kRawByron) {
+    // PBFT accepts an epoch-boundary header without a signature
+    // (ouroboros-consensus/src/Ouroboros/Consensus/Protocol/PBFT.hs:327-328)
+    for (size_t i = 0; i < s.m; i++)
+      c.verdict[s.lo + i] = st[i] == OURO_PACK_EBB ? 1 : (st[i] == OURO_PACK_OK && v[i] ? 1 : 0);
+    return OURO_OK;
+  }
   // a header the slicer rejected is invalid (its zeroed row cannot verify;
   // masked so that no bit at all is set for it)
   for (size_t i = 0; i < s.m; i++) c.verdict[s.lo + i] = st[i] == OURO_PACK_OK ? v[i] : 0;
@@ -1983,8 +2019,8 @@ int raw_run(const RawCall& c, const std::vector<RawChunk>& chunks) {
   RawPipe& p = ctx_of(dev).raw;
   // chunks in flight: the header kernel wants ~3 grids of work queued (6 x
   // 64 K headers); the Sum6KES kernel is PCIe-bound, 4 suffice
-  // (profiles/r05a/cbor_sweep.jsonl)
-  const int S = (int)knob_size(ouro_knobs::get().cbor_slots, c.kind == kRawKes ? 4 : 6, 1, kRawMaxSlots);
+  // (profiles/r05a/cbor_sweep.jsonl), and so is Byron's Ed25519
+  const int S = (int)knob_size(ouro_knobs::get().cbor_slots, c.kind == kRawHdr ? 6 : 4, 1, kRawMaxSlots);
   for (int k = 0; k < S; k++) {
     RawSlot& s = p.s[k];
     if (!s.st) OURO_HIP(hipStreamCreateWithFlags(&s.st, hipStreamNonBlocking));
@@ -2023,7 +2059,28 @@ int raw_run(const RawCall& c, const std::vector<RawChunk>& chunks) {
 
 // the host path over the same batch: host slicer + host verification, in
 // chunks (no batch-sized arena), results straight into the caller's buffers
+int raw_host_byron(const RawCall& c) {
+  const size_t C = 1 << 16;
+  for (size_t lo = 0; lo < c.n; lo += C) {
+    const size_t m = std::min(C, c.n - lo);
+    const size_t nb = ouro_byron_pack_bytes(m, c.len + lo);
+    std::unique_ptr<uint8_t[]> arena(new (std::nothrow) uint8_t[nb]);  // every row written
+    if (!arena) return fail(OURO_EDEVICE, "raw Byron host path: out of host memory");
+    ouro_byron_batch b;
+    int rc = ouro_byron_pack_cbor(c.raw, c.raw_bytes, c.off + lo, c.len + lo, m, c.magic,
+                                  arena.get(), nb, &b, c.status + lo, 0);
+    if (rc) return fail(rc, "ouro_byron_pack_cbor: bad arguments");
+    if ((rc = ouro_host::ed_batch(m, b.pk, b.sig, b.msg, b.msg_off, b.msg_len, c.verdict + lo, 1)))
+      return fail(rc, "raw Byron host path failed");
+    for (size_t i = lo; i < lo + m; i++)
+      c.verdict[i] = c.status[i] == OURO_PACK_EBB ? 1
+                                                  : (c.status[i] == OURO_PACK_OK && c.verdict[i]);
+  }
+  return OURO_OK;
+}
+
 int raw_host(const RawCall& c) {
+  if (c.kind == kRawByron) return raw_host_byron(c);
   const size_t C = 1 << 16;
   const size_t cap = std::min(C, c.n);
   const size_t nb = ouro_tpraos_pack_bytes(cap);
@@ -2060,8 +2117,11 @@ int raw_host(const RawCall& c) {
 
 int raw_verify(const RawCall& c) {
   if (c.n == 0) return OURO_OK;
-  if (!c.raw || !c.off || !c.len || !c.status || !c.verdict || c.spkp == 0)
-    return fail(OURO_EINVAL, "null argument / zero period");
+  if (!c.raw || !c.off || !c.len || !c.status || !c.verdict)
+    return fail(OURO_EINVAL, "null argument");
+  if (c.kind != kRawByron && c.spkp == 0) return fail(OURO_EINVAL, "zero slots per KES period");
+  if (c.kind == kRawByron && (c.magic < -1 || c.magic > (int64_t)0xffffffffll))
+    return fail(OURO_EINVAL, "protocol magic outside Word32 (or -1)");
   if ((c.ea == nullptr) != (c.la == nullptr))
     return fail(OURO_EINVAL, "give both VRF input arrays or neither");
   std::vector<RawChunk> chunks;
@@ -2102,6 +2162,22 @@ int ouro_tpraos_verify_cbor(const uint8_t* raw, size_t raw_bytes, const uint64_t
                             uint8_t* beta_eta, uint8_t* beta_leader, uint8_t* eta_nonce) {
   RawCall c{kRawHdr, raw, raw_bytes, off, len, n, slots_per_kes_period, epoch_nonce, eta_alpha,
             leader_alpha, status, verdict, beta_eta, beta_leader, eta_nonce};
+  return raw_verify(c);
+}
+
+// Raw Byron headers -> PBFT's block-signature verdicts (ouroboros-consensus/
+// src/Ouroboros/Consensus/Protocol/PBFT.hs:332-338; the storage integrity
+// check ouroboros-consensus-byron/src/Ouroboros/Consensus/Byron/Ledger/
+// Integrity.hs:24-35) through the raw-CBOR pipeline above: chunks gathered
+// into pinned NUMA-local staging, the device Byron slicer (k_byron_pack, the
+// host slicer's cbor_byron.h parse), then the Ed25519 kernel with ByronDSIGN
+// acceptance.  An epoch-boundary header is 1 (status OURO_PACK_EBB); a
+// rejected one 0.
+int ouro_byron_verify_cbor(const uint8_t* raw, size_t raw_bytes, const uint64_t* off,
+                           const uint32_t* len, size_t n, int64_t protocol_magic,
+                           uint8_t* status, uint8_t* verdict) {
+  RawCall c{kRawByron, raw, raw_bytes, off, len, n, 0, nullptr, nullptr, nullptr, status,
+            verdict, nullptr, nullptr, nullptr, protocol_magic};
   return raw_verify(c);
 }
 
@@ -2800,11 +2876,15 @@ int ouro_debug_contexts(int device, size_t* created, size_t* idle) {
 }  // extern "C"
 
 // ---- one process, several GPUs ----------------------------
-// A persistent worker thread per (device, k-th listing of that device): its
-// thread-local streams, device buffers and pinned staging (the pipelined host
-// path) belong to that one device and live as long as the process, so
-// repeated calls allocate nothing and a reordered device list never sends a
-// worker's buffers to another GPU.  Each worker verifies one contiguous shard
+// Persistent worker threads, pooled per device: a multi-device call borrows
+// one worker per shard (a device listed k times gets k workers) and returns
+// them when every shard is done, so two callers -- ChainSync windows and
+// ChainDB's suffix re-validation, say -- run their calls at once on workers of
+// their own instead of queueing behind one process-wide lock (VERDICT r05
+// item 2).  A worker's thread-local context -- streams, device buffers,
+// pinned staging, the raw-CBOR slots -- belongs to its one device and lives as
+// long as the process, so repeated calls allocate nothing; the worker is
+// bound to its GPU's NUMA node.  Each worker verifies one contiguous shard
 // straight into the caller's buffers; in one process no collective is needed.
 namespace {
 struct Worker {
@@ -2814,21 +2894,21 @@ struct Worker {
   int dev = 0, rc = OURO_OK;
   int numa_node = -1, bound_cpus = 0;
   std::string err;
-  ouro_tpraos_batch shard{};
-  uint8_t *verdict = nullptr, *be = nullptr, *bl = nullptr;
+  std::function<int()> job;
 
   void loop() {
     // this worker's host side -- its copies, its pinned staging (allocated
-    // below with hipHostMallocNumaUser), its callbacks -- on the GPU's node
+    // with hipHostMallocNumaUser), its gathers -- on the GPU's node
     numa_node = device_numa_node(dev);
     if (numa_node >= 0) bound_cpus = ouro_numa::bind_thread(numa_node);
     for (;;) {
       std::unique_lock<std::mutex> lk(mu);
       cv.wait(lk, [&] { return has_job; });
       has_job = false;
+      std::function<int()> f = std::move(job);
       lk.unlock();
       int r = ouro_set_device(dev);
-      if (r == OURO_OK) r = ouro_tpraos_verify_batch(&shard, verdict, be, bl);
+      if (r == OURO_OK) r = f();
       lk.lock();
       rc = r;
       err = r ? t_last_error : std::string();
@@ -2838,18 +2918,88 @@ struct Worker {
   }
 };
 
-std::mutex g_multi_mu;                              // one multi-device call at a time
-std::map<std::pair<int, int>, Worker*> g_workers;  // never freed: threads outlive every call
+struct WorkerPool {
+  std::mutex mu;
+  std::map<int, std::vector<Worker*>> idle;  // per device
+  std::vector<Worker*> all;                   // never freed: threads outlive every call
+};
+WorkerPool& worker_pool() {
+  static WorkerPool* p = new WorkerPool;
+  return *p;
+}
 
-Worker* worker(int dev, int ordinal) {
-  Worker*& w = g_workers[{dev, ordinal}];
-  if (!w) {
-    w = new Worker;
-    w->dev = dev;
-    Worker* self = w;
-    std::thread([self] { self->loop(); }).detach();
+Worker* borrow_worker(int dev) {
+  WorkerPool& P = worker_pool();
+  std::lock_guard<std::mutex> g(P.mu);
+  std::vector<Worker*>& v = P.idle[dev];
+  if (!v.empty()) {
+    Worker* w = v.back();
+    v.pop_back();
+    return w;
   }
+  Worker* w = new Worker;
+  w->dev = dev;
+  std::thread([w] { w->loop(); }).detach();
+  P.all.push_back(w);
   return w;
+}
+
+void return_worker(Worker* w) {
+  WorkerPool& P = worker_pool();
+  std::lock_guard<std::mutex> g(P.mu);
+  P.idle[w->dev].push_back(w);
+}
+
+// the device list of a multi-device call (NULL: every visible device)
+int multi_devices(const int* devices, int ndev, std::vector<int>* devs) {
+  const int count = ouro_device_count();
+  if (devices) {
+    if (ndev <= 0 || ndev > 64) return fail(OURO_EINVAL, "bad device count");
+    devs->assign(devices, devices + ndev);
+    for (int d : *devs)
+      if (d < 0 || d >= count) return fail(OURO_ENODEV, "no such device " + std::to_string(d));
+  } else {
+    for (int d = 0; d < count; d++) devs->push_back(d);
+    if (devs->empty()) return fail(OURO_ENODEV, "no device");
+  }
+  return OURO_OK;
+}
+
+// n items in contiguous shards of ceil(n / G) over the listed devices, shard
+// k = job(k's first item, its count) on a borrowed worker of devices[k]; the
+// first failing shard's code (its message prefixed with the device)
+template <class Job>
+int run_multi(const std::vector<int>& devs, size_t n, Job&& job) {
+  const size_t g = std::min<size_t>(devs.size(), n);
+  const size_t per = (n + g - 1) / g;
+  std::vector<Worker*> used;
+  for (size_t k = 0; k < g; k++) {
+    const size_t lo = k * per;
+    if (lo >= n) break;
+    const size_t m = std::min(per, n - lo);
+    Worker* w = borrow_worker(devs[k]);
+    {
+      std::lock_guard<std::mutex> lk(w->mu);
+      w->job = [&job, lo, m] { return job(lo, m); };
+      w->done = false;
+      w->has_job = true;
+    }
+    w->cv.notify_all();
+    used.push_back(w);
+  }
+  int rc = OURO_OK;
+  for (Worker* w : used) {  // wait for every shard, errors included
+    {
+      std::unique_lock<std::mutex> lk(w->mu);
+      w->cv.wait(lk, [&] { return w->done; });
+      if (w->rc && rc == OURO_OK) {
+        rc = w->rc;
+        t_last_error = "device " + std::to_string(w->dev) + ": " + w->err;
+      }
+    }
+    return_worker(w);
+  }
+  return rc;
 }
 
 ouro_tpraos_batch shard_of(const ouro_tpraos_batch& b, size_t lo, size_t m) {
@@ -2875,6 +3025,39 @@ ouro_tpraos_batch shard_of(const ouro_tpraos_batch& b, size_t lo, size_t m) {
   if (b.eta_nonce) s.eta_nonce = b.eta_nonce + 32 * lo;
   return s;
 }
+
+// shard [lo, lo + m) of a raw-CBOR call: the buffer and its offsets are
+// shared (the offsets are absolute into raw), every per-header array offset
+RawCall raw_shard(const RawCall& c, size_t lo, size_t m) {
+  RawCall s = c;
+  s.n = m;
+  s.off = c.off + lo;
+  s.len = c.len + lo;
+  if (c.ea) s.ea = c.ea + 32 * lo;
+  if (c.la) s.la = c.la + 32 * lo;
+  s.status = c.status + lo;
+  s.verdict = c.verdict + lo;
+  if (c.be) s.be = c.be + 64 * lo;
+  if (c.bl) s.bl = c.bl + 64 * lo;
+  if (c.nonce) s.nonce = c.nonce + 32 * lo;
+  return s;
+}
+
+// a raw-CBOR call over several devices: its argument checks once, then each
+// shard through the one-device pipeline (raw_verify: chunks over the worker's
+// slots, the host-path recompute of that shard after a device error)
+int raw_verify_multi(const RawCall& c, const int* devices, int ndev) {
+  if (c.n == 0) return OURO_OK;
+  if (!c.raw || !c.off || !c.len || !c.status || !c.verdict)
+    return fail(OURO_EINVAL, "null argument");
+  for (size_t i = 0; i < c.n; i++)  // every span inside raw before any shard starts
+    if (c.off[i] > c.raw_bytes || c.raw_bytes - c.off[i] < c.len[i])
+      return fail(OURO_EINVAL, "header " + std::to_string(i) + ": span outside raw_bytes");
+  std::vector<int> devs;
+  int rc = multi_devices(devices, ndev, &devs);
+  if (rc) return rc;
+  return run_multi(devs, c.n, [&](size_t lo, size_t m) { return raw_verify(raw_shard(c, lo, m)); });
+}
 }  // namespace
 
 extern "C" {
@@ -2898,13 +3081,14 @@ int ouro_bind_thread_to_device(int device) {
 }
 
 int ouro_debug_multi_workers(int* devices, int* nodes, int* cpus, int max) {
-  std::lock_guard<std::mutex> guard(g_multi_mu);
+  WorkerPool& P = worker_pool();
+  std::lock_guard<std::mutex> guard(P.mu);
   int k = 0;
-  for (auto& kv : g_workers) {
+  for (Worker* w : P.all) {
     if (k < max) {
-      if (devices) devices[k] = kv.second->dev;
-      if (nodes) nodes[k] = kv.second->numa_node;
-      if (cpus) cpus[k] = kv.second->bound_cpus;
+      if (devices) devices[k] = w->dev;
+      if (nodes) nodes[k] = w->numa_node;
+      if (cpus) cpus[k] = w->bound_cpus;
     }
     k++;
   }
@@ -2919,47 +3103,51 @@ int ouro_tpraos_verify_batch_multi(const ouro_tpraos_batch* b, const int* device
   int rc = check_hdr_batch(b);
   if (rc) return rc;
   std::vector<int> devs;
-  const int count = ouro_device_count();
-  if (devices) {
-    if (ndev <= 0 || ndev > 64) return fail(OURO_EINVAL, "bad device count");
-    devs.assign(devices, devices + ndev);
-    for (int d : devs)
-      if (d < 0 || d >= count) return fail(OURO_ENODEV, "no such device " + std::to_string(d));
-  } else {
-    for (int d = 0; d < count; d++) devs.push_back(d);
-    if (devs.empty()) return fail(OURO_ENODEV, "no device");
-  }
-  const size_t g = std::min<size_t>(devs.size(), b->n);
-  const size_t per = (b->n + g - 1) / g;
-  std::lock_guard<std::mutex> guard(g_multi_mu);
-  std::vector<Worker*> used;
-  std::map<int, int> listed;  // device -> listings so far
-  for (size_t k = 0; k < g; k++) {
-    const size_t lo = k * per;
-    if (lo >= b->n) break;
-    const size_t m = std::min(per, b->n - lo);
-    Worker* w = worker(devs[k], listed[devs[k]]++);
-    {
-      std::lock_guard<std::mutex> lk(w->mu);
-      w->shard = shard_of(*b, lo, m);
-      w->verdict = verdict + lo;
-      w->be = beta_eta ? beta_eta + 64 * lo : nullptr;
-      w->bl = beta_leader ? beta_leader + 64 * lo : nullptr;
-      w->done = false;
-      w->has_job = true;
-    }
-    w->cv.notify_all();
-    used.push_back(w);
-  }
-  for (Worker* w : used) {  // wait for every shard, errors included
-    std::unique_lock<std::mutex> lk(w->mu);
-    w->cv.wait(lk, [&] { return w->done; });
-    if (w->rc && rc == OURO_OK) {
-      rc = w->rc;
-      t_last_error = "device " + std::to_string(w->dev) + ": " + w->err;
-    }
-  }
-  return rc;
+  if ((rc = multi_devices(devices, ndev, &devs))) return rc;
+  return run_multi(devs, b->n, [&](size_t lo, size_t m) {
+    const ouro_tpraos_batch s = shard_of(*b, lo, m);
+    return ouro_tpraos_verify_batch(&s, verdict + lo, beta_eta ? beta_eta + 64 * lo : nullptr,
+                                    beta_leader ? beta_leader + 64 * lo : nullptr);
+  });
+}
+
+// The raw-CBOR entries over several devices of one process (SURVEY.md §8(e):
+// static contiguous shards, one per listed device, each on that device's
+// NUMA-bound worker with its own chunk pipeline and pinned staging; results
+// straight into the caller's buffers).
+int ouro_tpraos_verify_cbor_multi(const int* devices, int ndev, const uint8_t* raw,
+                                  size_t raw_bytes, const uint64_t* off, const uint32_t* len,
+                                  size_t n, uint64_t slots_per_kes_period,
+                                  const uint8_t* epoch_nonce, const uint8_t* eta_alpha,
+                                  const uint8_t* leader_alpha, uint8_t* status, uint8_t* verdict,
+                                  uint8_t* beta_eta, uint8_t* beta_leader, uint8_t* eta_nonce) {
+  if (n && slots_per_kes_period == 0) return fail(OURO_EINVAL, "zero slots per KES period");
+  if ((eta_alpha == nullptr) != (leader_alpha == nullptr))
+    return fail(OURO_EINVAL, "give both VRF input arrays or neither");
+  RawCall c{kRawHdr, raw, raw_bytes, off, len, n, slots_per_kes_period, epoch_nonce, eta_alpha,
+            leader_alpha, status, verdict, beta_eta, beta_leader, eta_nonce};
+  return raw_verify_multi(c, devices, ndev);
+}
+
+int ouro_integrity_verify_cbor_multi(const int* devices, int ndev, const uint8_t* raw,
+                                     size_t raw_bytes, const uint64_t* off, const uint32_t* len,
+                                     size_t n, uint64_t slots_per_kes_period, uint8_t* status,
+                                     uint8_t* verdict) {
+  if (n && slots_per_kes_period == 0) return fail(OURO_EINVAL, "zero slots per KES period");
+  RawCall c{kRawKes, raw, raw_bytes, off, len, n, slots_per_kes_period, nullptr, nullptr,
+            nullptr, status, verdict, nullptr, nullptr, nullptr};
+  return raw_verify_multi(c, devices, ndev);
+}
+
+int ouro_byron_verify_cbor_multi(const int* devices, int ndev, const uint8_t* raw,
+                                 size_t raw_bytes, const uint64_t* off, const uint32_t* len,
+                                 size_t n, int64_t protocol_magic, uint8_t* status,
+                                 uint8_t* verdict) {
+  if (protocol_magic < -1 || protocol_magic > (int64_t)0xffffffffll)
+    return fail(OURO_EINVAL, "protocol magic outside Word32 (or -1)");
+  RawCall c{kRawByron, raw, raw_bytes, off, len, n, 0, nullptr, nullptr, nullptr, status,
+            verdict, nullptr, nullptr, nullptr, protocol_magic};
+  return raw_verify_multi(c, devices, ndev);
 }
 
 }  // extern "C"

@@ -392,14 +392,28 @@ def mk_seed(universal_nonce: Optional[bytes], slot: int, epoch_nonce: Optional[b
     return bytes(a ^ b for a, b in zip(h, universal_nonce))
 
 
-def verify_integrity_cbor(raw_headers, slots_per_kes_period: int, host: bool = False):
+def _devices_arg(devices):
+    """(int array or None, count) for the *_multi entries: None = every
+    visible device"""
+    if devices is None:
+        return None, 0
+    d = np.ascontiguousarray(list(devices), np.int32)
+    if d.size == 0:
+        raise ValueError("devices: at least one")
+    return d, int(d.size)
+
+
+def verify_integrity_cbor(raw_headers, slots_per_kes_period: int, host: bool = False,
+                          devices=None):
     """verifyHeaderIntegrity over raw headers (KES only; the storage layer's
     check, ouroboros-consensus-shelley/src/Ouroboros/Consensus/Shelley/Ledger/
     Integrity.hs:20-44): returns (valid bool array, slicer status array).
     Default: ouro_integrity_verify_cbor (the raw-CBOR pipeline: header bytes
     gathered into pinned staging, the device slicer, the Sum6KES kernel).
     host=True: the same slicer, then the library's host path
-    (ouro_sum6kes_verify_batch_host) -- no device touched."""
+    (ouro_sum6kes_verify_batch_host) -- no device touched.  devices (a list
+    of device indices, or "all"): ouro_integrity_verify_cbor_multi, contiguous
+    shards over those GPUs of this process."""
     import ctypes
 
     from . import _native
@@ -411,6 +425,14 @@ def verify_integrity_cbor(raw_headers, slots_per_kes_period: int, host: bool = F
         return verdict[:0].astype(bool), status[:0]
     ptr = lambda a: a.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
     lib = _native.load()
+    if not host and devices is not None:
+        d, nd = _devices_arg(None if devices == "all" else devices)
+        rc = lib.ouro_integrity_verify_cbor_multi(ptr(d) if d is not None else None, nd,
+                                                  ptr(buf), buf.size, ptr(off), ptr(ln), n,
+                                                  slots_per_kes_period, ptr(status),
+                                                  ptr(verdict))
+        _native.check(rc, "ouro_integrity_verify_cbor_multi")
+        return verdict[:n].astype(bool), status[:n]
     if not host:
         rc = lib.ouro_integrity_verify_cbor(ptr(buf), buf.size, ptr(off), ptr(ln), n,
                                             slots_per_kes_period, ptr(status), ptr(verdict))
@@ -430,7 +452,8 @@ def verify_integrity_cbor(raw_headers, slots_per_kes_period: int, host: bool = F
 def verify_headers_cbor(raw_headers, slots_per_kes_period: int, *,
                         epoch_nonce: Optional[bytes] = None,
                         eta_alpha: Optional[np.ndarray] = None,
-                        leader_alpha: Optional[np.ndarray] = None, nonce: bool = False):
+                        leader_alpha: Optional[np.ndarray] = None, nonce: bool = False,
+                        devices=None):
     """The full TPraos header check straight from raw header CBOR in host
     memory, one call (include/ouro_verify.h ouro_tpraos_verify_cbor): the
     crypto of TPraos.updateChainDepState (ouroboros-consensus-shelley/src/
@@ -438,7 +461,9 @@ def verify_headers_cbor(raw_headers, slots_per_kes_period: int, *,
     VRF inputs: eta_alpha / leader_alpha (n x 32 each) when given, else mkSeed
     from each header's slot and epoch_nonce (None = NeutralNonce) on the
     device.  Returns (verdict, beta_eta, beta_leader, status[, eta_nonce]):
-    verdict = OURO_HDR_* bits (0 where the header does not slice)."""
+    verdict = OURO_HDR_* bits (0 where the header does not slice).
+    devices (a list of device indices, or "all"): ouro_tpraos_verify_cbor_multi,
+    contiguous shards over those GPUs of this process."""
     import ctypes
 
     from . import _native
@@ -464,9 +489,17 @@ def verify_headers_cbor(raw_headers, slots_per_kes_period: int, *,
     eta0 = None if epoch_nonce is None else np.frombuffer(bytes(epoch_nonce), np.uint8)
     if n:
         lib = _native.load()
-        rc = lib.ouro_tpraos_verify_cbor(ptr(buf), buf.size, ptr(off), ptr(ln), n,
-                                         slots_per_kes_period, ptr(eta0), ptr(ea), ptr(la),
-                                         ptr(status), ptr(verdict), ptr(be), ptr(bl), ptr(en))
-        _native.check(rc, "ouro_tpraos_verify_cbor")
+        if devices is not None:
+            d, nd = _devices_arg(None if devices == "all" else devices)
+            rc = lib.ouro_tpraos_verify_cbor_multi(ptr(d), nd, ptr(buf), buf.size, ptr(off),
+                                                   ptr(ln), n, slots_per_kes_period, ptr(eta0),
+                                                   ptr(ea), ptr(la), ptr(status), ptr(verdict),
+                                                   ptr(be), ptr(bl), ptr(en))
+            _native.check(rc, "ouro_tpraos_verify_cbor_multi")
+        else:
+            rc = lib.ouro_tpraos_verify_cbor(ptr(buf), buf.size, ptr(off), ptr(ln), n,
+                                             slots_per_kes_period, ptr(eta0), ptr(ea), ptr(la),
+                                             ptr(status), ptr(verdict), ptr(be), ptr(bl), ptr(en))
+            _native.check(rc, "ouro_tpraos_verify_cbor")
     out = (verdict[:n], be[:n], bl[:n], status[:n])
     return out + (en[:n],) if nonce else out

@@ -1,6 +1,8 @@
 /*
  * C callers of the one-call raw-CBOR entries (include/ouro_verify.h
- * ouro_tpraos_verify_cbor, ouro_integrity_verify_cbor):
+ * ouro_tpraos_verify_cbor, ouro_integrity_verify_cbor)
+ * and their multi-device forms (ouro_*_verify_cbor_multi; VERDICT r05 item
+ * 2: threads with id % 4 == 2 pass devices {0}, id % 4 == 3 devices {0, 0}):
  * THREADS pthreads each call both entries ROUNDS times on the same raw
  * headers -- as a node's ChainDB / storage threads would through the FFI --
  * and compare status, verdicts and both VRF outputs with the expectations the
@@ -56,11 +58,15 @@ static void *worker(void *arg) {
   long calls = 0;
   memcpy(my_ea, ea, 32 * n);
   memcpy(my_la, la, 32 * n);
+  static const int devs[2] = {0, 0};
+  const int multi = id % 4 >= 2, ndev = id % 4 == 3 ? 2 : 1;
   for (int r = 0; r < rounds; r++) {
     memset(v, 0xEE, n);
-    const int rc = ouro_tpraos_verify_cbor(raw, raw_bytes, off, len, n, spkp,
-                                           NULL, (id & 1) ? ea : my_ea, (id & 1) ? la : my_la,
-                                           st, v, be, bl, NULL);
+    const uint8_t *a = (id & 1) ? ea : my_ea, *b = (id & 1) ? la : my_la;
+    const int rc = multi ? ouro_tpraos_verify_cbor_multi(devs, ndev, raw, raw_bytes, off, len, n,
+                                                         spkp, NULL, a, b, st, v, be, bl, NULL)
+                         : ouro_tpraos_verify_cbor(raw, raw_bytes, off, len, n, spkp, NULL, a, b,
+                                                   st, v, be, bl, NULL);
     CHECK(rc == OURO_OK, "t%d tpraos rc %d (%s)\n", id, rc, ouro_last_error());
     for (uint64_t i = 0; i < n; i++) {
       CHECK(st[i] == w_st[i], "t%d status %llu\n", id, (unsigned long long)i);
@@ -74,7 +80,9 @@ static void *worker(void *arg) {
       }
     }
     memset(v, 0xEE, n);
-    const int ri = ouro_integrity_verify_cbor(raw, raw_bytes, off, len, n, spkp, st, v);
+    const int ri = multi ? ouro_integrity_verify_cbor_multi(devs, ndev, raw, raw_bytes, off, len,
+                                                            n, spkp, st, v)
+                         : ouro_integrity_verify_cbor(raw, raw_bytes, off, len, n, spkp, st, v);
     CHECK(ri == OURO_OK, "t%d integrity rc %d (%s)\n", id, ri, ouro_last_error());
     for (uint64_t i = 0; i < n; i++)
       CHECK(v[i] == w_int[i], "t%d integrity %llu\n", id, (unsigned long long)i);

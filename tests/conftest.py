@@ -110,3 +110,26 @@ def gpu_lib():
 
     lib = ona._native.load()
     return lib
+
+
+@pytest.fixture
+def small_chunks():
+    """The pipeline cut into many chunks: `set(CHUNK=..., SLOTS=..., RAMP=...)`
+    sets OURO_CBOR_* and has the library re-read its switches (knobs.h)."""
+    from ouroboros_network_amd import _native
+
+    saved = {k: os.environ.get(k) for k in ("OURO_CBOR_CHUNK", "OURO_CBOR_SLOTS",
+                                             "OURO_CBOR_RAMP")}
+
+    def set_(**kw):
+        for k, v in kw.items():
+            os.environ["OURO_CBOR_" + k] = str(v)
+        _native.reload_knobs()
+
+    yield set_
+    for k, v in saved.items():
+        if v is None:
+            os.environ.pop(k, None)
+        else:
+            os.environ[k] = v
+    _native.reload_knobs()

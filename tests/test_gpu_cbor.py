@@ -75,29 +75,6 @@ def _check(raws, spkp, ea=None, la=None, epoch_nonce=None, triple=None):
     return v, st
 
 
-@pytest.fixture
-def small_chunks():
-    """The pipeline cut into many chunks: `set(CHUNK=..., SLOTS=..., RAMP=...)`
-    sets OURO_CBOR_* and has the library re-read its switches (knobs.h)."""
-    from ouroboros_network_amd import _native
-
-    saved = {k: os.environ.get(k) for k in ("OURO_CBOR_CHUNK", "OURO_CBOR_SLOTS",
-                                             "OURO_CBOR_RAMP")}
-
-    def set_(**kw):
-        for k, v in kw.items():
-            os.environ["OURO_CBOR_" + k] = str(v)
-        _native.reload_knobs()
-
-    yield set_
-    for k, v in saved.items():
-        if v is None:
-            os.environ.pop(k, None)
-        else:
-            os.environ[k] = v
-    _native.reload_knobs()
-
-
 @pytest.mark.gpu
 def test_golden_corruptions_truncations(gpu_lib, kats):
     from ouroboros_network_amd import header as H
@@ -263,7 +240,8 @@ def test_device_error_recomputes_on_the_host_path(gpu_lib, kats, small_chunks):
 @pytest.mark.gpu
 def test_c_callers(gpu_lib, kats, tmp_path):
     """tests/c/cbor_callers.c: 8 pthreads call ouro_tpraos_verify_cbor and
-    ouro_integrity_verify_cbor through the C ABI on the golden cases (every
+    ouro_integrity_verify_cbor -- four of them the multi-device forms with
+    devices {0} and {0, 0} -- through the C ABI on the golden cases (every
     single-byte corruption and truncations), each result checked against the
     pinned host slicer + oracle."""
     import subprocess
