@@ -2928,6 +2928,8 @@ WorkerPool& worker_pool() {
   return *p;
 }
 
+// an idle worker of `dev`, or a new one; nullptr if no thread could be
+// started (no exception ever crosses the C ABI)
 Worker* borrow_worker(int dev) {
   WorkerPool& P = worker_pool();
   std::lock_guard<std::mutex> g(P.mu);
@@ -2937,9 +2939,16 @@ Worker* borrow_worker(int dev) {
     v.pop_back();
     return w;
   }
-  Worker* w = new Worker;
+  Worker* w = new (std::nothrow) Worker;
+  if (!w) return nullptr;
   w->dev = dev;
-  std::thread([w] { w->loop(); }).detach();
+  try {
+    P.all.reserve(P.all.size() + 1);
+    std::thread([w] { w->loop(); }).detach();
+  } catch (...) {
+    delete w;
+    return nullptr;
+  }
   P.all.push_back(w);
   return w;
 }
@@ -2972,12 +2981,22 @@ template <class Job>
 int run_multi(const std::vector<int>& devs, size_t n, Job&& job) {
   const size_t g = std::min<size_t>(devs.size(), n);
   const size_t per = (n + g - 1) / g;
+  // every shard's worker first, so a worker that cannot be started fails the
+  // call before any shard runs
   std::vector<Worker*> used;
-  for (size_t k = 0; k < g; k++) {
-    const size_t lo = k * per;
-    if (lo >= n) break;
-    const size_t m = std::min(per, n - lo);
+  for (size_t k = 0; k < g && k * per < n; k++) {
     Worker* w = borrow_worker(devs[k]);
+    if (!w) {
+      for (Worker* u : used) return_worker(u);
+      return fail(OURO_EDEVICE, "cannot start a worker thread for device " +
+                                    std::to_string(devs[k]));
+    }
+    used.push_back(w);
+  }
+  for (size_t k = 0; k < used.size(); k++) {
+    const size_t lo = k * per;
+    const size_t m = std::min(per, n - lo);
+    Worker* w = used[k];
     {
       std::lock_guard<std::mutex> lk(w->mu);
       w->job = [&job, lo, m] { return job(lo, m); };
@@ -2985,7 +3004,6 @@ int run_multi(const std::vector<int>& devs, size_t n, Job&& job) {
       w->has_job = true;
     }
     w->cv.notify_all();
-    used.push_back(w);
   }
   int rc = OURO_OK;
   for (Worker* w : used) {  // wait for every shard, errors included
