@@ -40,6 +40,7 @@ def main():
     import torch
 
     import bench
+    from ouroboros_network_amd import _native
     from ouroboros_network_amd.tpraos import HeaderPlan
 
     dev = torch.device("cuda", 0)
@@ -62,6 +63,7 @@ def main():
             kv = [c.split("=", 1) for c in combo.split("+")]
             for k, v in kv:
                 os.environ[k] = v
+            _native.reload_knobs()  # the library reads its switches once (knobs.h)
             plans[combo] = HeaderPlan(args.batch, body)
             for k, _ in kv:
                 del os.environ[k]
@@ -69,6 +71,7 @@ def main():
         values = args.values.split(",")
         for v in values:
             os.environ[args.var] = v
+            _native.reload_knobs()
             plans[v] = HeaderPlan(args.batch, body)
     lat = {k: [] for k in plans}
     outs = {}

@@ -62,6 +62,7 @@ def main():
         for kind, fn in (("hdr", hdr), ("kes", kes)):
             for ramp in ("1", "0", "1", "0"):
                 os.environ["OURO_CBOR_RAMP"] = ramp
+                _native.reload_knobs()  # the library reads its switches once (knobs.h)
                 assert fn() == 0, lib.ouro_last_error()
                 ts = []
                 for _ in range(reps):
@@ -79,6 +80,7 @@ def main():
             os.environ["OURO_CBOR_CHUNK"] = str(chunk)
             os.environ["OURO_CBOR_SLOTS"] = str(slots)
             os.environ["OURO_CBOR_COPY_THREADS"] = str(threads)
+            _native.reload_knobs()
             assert fn() == 0, lib.ouro_last_error()
             ts, ss = [], []
             for _ in range(reps):

@@ -25,6 +25,7 @@ def main():
     import torch
 
     import bench
+    from ouroboros_network_amd import _native
 
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(0)
@@ -34,8 +35,10 @@ def main():
     out = {}
     for v in args.values.split(","):
         os.environ[args.var] = v
+        _native.reload_knobs()  # the library reads its switches once (knobs.h)
         out[f"{args.var}={v}"] = bench._plan_phases(nb, args.iters, nonce=True)
         del os.environ[args.var]
+        _native.reload_knobs()
     print(json.dumps(out, indent=1))
 
 
