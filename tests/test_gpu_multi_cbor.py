@@ -204,3 +204,34 @@ def test_multi_rejects_bad_arguments(gpu_lib, kats):
         H.verify_integrity_cbor((buf, off, ln), SPKP, devices=[0, 0])
     with pytest.raises(_native.NativeUnavailable):
         H.verify_integrity_cbor(raws, SPKP, devices=[0, 99])
+
+
+@pytest.mark.device_error
+def test_multi_cbor_device_error_recomputes_on_the_host_path(gpu_lib, kats, small_chunks):
+    """OURO_TEST_DEVICE_ERROR (test build): every launch of every shard fails;
+    each shard is recomputed on the host path and the three multi entries
+    still return the oracle's verdicts (never an accept the device did not
+    make)."""
+    from ouroboros_network_amd import _native
+    from ouroboros_network_amd import byron as B
+    from ouroboros_network_amd import header as H
+
+    raws, ea, la = _golden_cases(kats, stride=13)
+    want = _expect(raws, SPKP, ea, la)
+    want_ok, want_st = H.verify_integrity_cbor(raws, SPKP, host=True)
+    braws, bwant, bwant_st = _byron_cases(kats)
+    with _native.knob_env(OURO_TEST_DEVICE_ERROR="1", OURO_CBOR_CHUNK="256"):
+        v, be, bl, st = H.verify_headers_cbor(raws, SPKP, eta_alpha=ea, leader_alpha=la,
+                                              devices=[0, 0])
+        np.testing.assert_array_equal(st, want[4])
+        np.testing.assert_array_equal(v, want[0])
+        ok, ist = H.verify_integrity_cbor(raws, SPKP, devices=[0, 0])
+        np.testing.assert_array_equal(ok, want_ok)
+        np.testing.assert_array_equal(ist, want_st)
+        got, bst = B.verify_byron_cbor(braws, B.HEADER_MAGIC, devices=[0, 0])
+        np.testing.assert_array_equal(got, bwant)
+        np.testing.assert_array_equal(bst, bwant_st)
+        got1, _ = B.verify_byron_cbor(braws, B.HEADER_MAGIC)
+        np.testing.assert_array_equal(got1, bwant)
+        msg = gpu_lib.ouro_last_error().decode()
+        assert "recomputed on the host path" in msg, msg
