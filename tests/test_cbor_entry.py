@@ -97,3 +97,47 @@ def test_python_mirror_checks_its_arguments(kats):
         H.verify_headers_cbor(raws, 100, eta_alpha=np.zeros((len(raws), 32), np.uint8))
     v, be, bl, st = H.verify_headers_cbor([], 100)
     assert v.size == 0 and st.size == 0
+
+
+def test_multi_entries_without_a_device(lib, kats):
+    """The multi-device raw entries check every span, the
+    period, the alpha pair, the protocol magic and the device list before any
+    shard starts (OURO_EINVAL), accept n = 0, and with no GPU return
+    OURO_ENODEV with the verdicts untouched."""
+    import torch
+
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is present")
+    buf, off, ln = _args(kats)
+    n = off.size
+    st = np.zeros(n, np.uint8)
+    v = np.full(n, 0xEE, np.uint8)
+    a = np.zeros((n, 32), np.uint8)
+    devs = np.array([0, 0], np.int32)
+    I = ctypes.c_int
+
+    def hdr(d, nd, o=off, spkp=100, ea=None, la=None, count=n):
+        return lib.ouro_tpraos_verify_cbor_multi(P(d), I(nd), P(buf), buf.size, P(o), P(ln), count,
+                                                 spkp, None, P(ea), P(la), P(st), P(v), None,
+                                                 None, None)
+
+    def kes(d, nd, o=off, spkp=100):
+        return lib.ouro_integrity_verify_cbor_multi(P(d), I(nd), P(buf), buf.size, P(o), P(ln),
+                                                    n, spkp, P(st), P(v))
+
+    def byron(d, nd, magic=-1, o=off):
+        return lib.ouro_byron_verify_cbor_multi(P(d), I(nd), P(buf), buf.size, P(o), P(ln), n,
+                                                magic, P(st), P(v))
+
+    bad = off.copy()
+    bad[-1] = buf.size - 3
+    for call in (lambda: hdr(devs, 2, o=bad), lambda: kes(devs, 2, o=bad),
+                 lambda: byron(devs, 2, o=bad), lambda: hdr(devs, 2, spkp=0),
+                 lambda: kes(devs, 2, spkp=0), lambda: hdr(devs, 2, ea=a),
+                 lambda: byron(devs, 2, magic=2**32), lambda: byron(devs, 2, magic=-2),
+                 lambda: hdr(devs, 0), lambda: kes(devs, -1), lambda: byron(devs, 65)):
+        assert call() == EINVAL, lib.ouro_last_error()
+    assert hdr(devs, 2, count=0) == 0
+    for call in (lambda: hdr(devs, 2), lambda: kes(None, 0), lambda: byron(devs, 1)):
+        assert call() == ENODEV
+    assert (v == 0xEE).all()
