@@ -1252,7 +1252,7 @@ def byron_leg(n: int, threads: int, reps: int = 3):
             "python_slicer_headers_per_s": round(m / tpy, 1),
             "note": "golden Byron headers repeated; pageable host memory in, verdicts out; "
                     "since round 6 on the raw-CBOR pipeline (pinned staging, device Byron "
-                    "slicer, ByronDSIGN kernel, 4 chunks in flight)"}
+                    "slicer, ByronDSIGN kernel, 5 chunks in flight)"}
 
 
 def _timed(fn) -> float:

@@ -419,7 +419,7 @@ int ouro_byron_verify_cbor(const uint8_t *raw, size_t raw_bytes, const uint64_t 
 /* (How ouro_byron_verify_cbor runs, since round 6: on the raw-CBOR pipeline
  * of ouro_tpraos_verify_cbor -- chunks gathered into pinned NUMA-local
  * staging, the device Byron slicer (the same cbor_byron.h parse as
- * ouro_byron_pack_cbor) and the ByronDSIGN Ed25519 kernel per chunk, 4
+ * ouro_byron_pack_cbor) and the ByronDSIGN Ed25519 kernel per chunk, 5
  * chunks in flight; a device error recomputes the batch on the host path.
  * OURO_EINVAL as for ouro_byron_pack_cbor.) */
 

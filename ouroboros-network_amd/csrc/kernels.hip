@@ -2019,8 +2019,11 @@ int raw_run(const RawCall& c, const std::vector<RawChunk>& chunks) {
   RawPipe& p = ctx_of(dev).raw;
   // chunks in flight: the header kernel wants ~3 grids of work queued (6 x
   // 64 K headers); the Sum6KES kernel is PCIe-bound, 4 suffice
-  // (profiles/r05a/cbor_sweep.jsonl), and so is Byron's Ed25519
-  const int S = (int)knob_size(ouro_knobs::get().cbor_slots, c.kind == kRawHdr ? 6 : 4, 1, kRawMaxSlots);
+  // (profiles/r05a/cbor_sweep.jsonl); Byron's Ed25519 runs best with 5
+  // (66.7--67.1 M headers/s against ~61 with 4 and 60--68 with 6, interleaved
+  // on one box: profiles/r06k/byron_ab.jsonl)
+  const int S = (int)knob_size(ouro_knobs::get().cbor_slots, c.kind == kRawHdr ? 6 : (c.kind == kRawByron ? 5 : 4), 1,
+                                kRawMaxSlots);
   for (int k = 0; k < S; k++) {
     RawSlot& s = p.s[k];
     if (!s.st) OURO_HIP(hipStreamCreateWithFlags(&s.st, hipStreamNonBlocking));
@@ -2171,8 +2174,8 @@ int ouro_tpraos_verify_cbor(const uint8_t* raw, size_t raw_bytes, const uint64_t
 // Integrity.hs:24-35) through the raw-CBOR pipeline above: chunks gathered
 // into pinned NUMA-local staging, the device Byron slicer (k_byron_pack, the
 // host slicer's cbor_byron.h parse), then the Ed25519 kernel with ByronDSIGN
-// acceptance.  An epoch-boundary header is 1 (status OURO_PACK_EBB); a
-// rejected one 0.
+// acceptance, five chunks in flight.  An epoch-boundary header is 1 (status
+// OURO_PACK_EBB); a rejected one 0.
 int ouro_byron_verify_cbor(const uint8_t* raw, size_t raw_bytes, const uint64_t* off,
                            const uint32_t* len, size_t n, int64_t protocol_magic,
                            uint8_t* status, uint8_t* verdict) {

@@ -30,6 +30,8 @@ def main():
     dev = torch.device("cuda", 0)
     lib = _native.load()
     lib.ouro_bind_thread_to_device(0)
+    if os.environ.get("CBOR_SWEEP_BYRON"):  # ouro_byron_verify_cbor (round 6)
+        return byron_sweep(lib, n, reps)
     eta0 = bytes(range(101, 133))
     raw, rl = bench.synth_raw_node_headers(n, 1024, dev, eta0)
     buf = raw.cpu().numpy()
@@ -75,8 +77,14 @@ def main():
                                   "M_per_s": round(n / min(ts) / 1e6, 3),
                                   "chunks": int(stats[3]), "all_valid": ok}), flush=True)
         return
-    for kind, fn in (("hdr", hdr), ("kes", kes)):
-        for chunk, slots, threads in grid[kind]:
+    if os.environ.get("CBOR_SWEEP_GRID"):  # "kind:chunk:slots:threads,..." in order
+        order = [g.split(":") for g in os.environ["CBOR_SWEEP_GRID"].split(",")]
+        plan = [(k, {"hdr": hdr, "kes": kes}[k], [(int(c), int(s_), int(t))])
+                for k, c, s_, t in order]
+    else:
+        plan = [(kind, fn, grid[kind]) for kind, fn in (("hdr", hdr), ("kes", kes))]
+    for kind, fn, configs in plan:
+        for chunk, slots, threads in configs:
             os.environ["OURO_CBOR_CHUNK"] = str(chunk)
             os.environ["OURO_CBOR_SLOTS"] = str(slots)
             os.environ["OURO_CBOR_COPY_THREADS"] = str(threads)
@@ -95,6 +103,42 @@ def main():
                               "ms": round(ts[k] * 1e3, 2), "M_per_s": round(n / ts[k] / 1e6, 3),
                               "gather_ms": round(ss[k][1], 2), "wait_ms": round(ss[k][2], 2),
                               "all_valid": ok}), flush=True)
+
+
+def byron_sweep(lib, n, reps):
+    """The golden Byron wire forms repeated to n (bench.py byron_leg), raw ->
+    verdicts over chunk x slots x gather threads."""
+    from ouroboros_network_amd import _native
+    from ouroboros_network_amd import byron as B
+
+    with open(os.path.join(ROOT, "tests", "golden", "reference_kats.json")) as f:
+        wires = [bytes.fromhex(w["raw"]) for w in json.load(f)["byron_wire"]]
+    raws = [wires[i % len(wires)] for i in range(n)]
+    ln = np.array([len(r) for r in raws], np.uint32)
+    off = np.zeros(n, np.uint64)
+    off[1:] = np.cumsum(ln[:-1], dtype=np.uint64)
+    arg = (np.frombuffer(b"".join(raws), np.uint8), off, ln)
+    stats = np.zeros(6)
+    grid = list(itertools.product((32768, 65536, 131072, 262144), (2, 4, 6, 8), (8, 16)))
+    if os.environ.get("CBOR_SWEEP_GRID"):  # "chunk:slots:threads,..." repeated in order
+        grid = [tuple(int(x) for x in g.split(":")) for g in
+                os.environ["CBOR_SWEEP_GRID"].split(",")]
+    for chunk, slots, threads in grid:
+        os.environ["OURO_CBOR_CHUNK"] = str(chunk)
+        os.environ["OURO_CBOR_SLOTS"] = str(slots)
+        os.environ["OURO_CBOR_COPY_THREADS"] = str(threads)
+        _native.reload_knobs()
+        v, st = B.verify_byron_cbor(arg, B.HEADER_MAGIC)
+        ts = []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            v, st = B.verify_byron_cbor(arg, B.HEADER_MAGIC)
+            ts.append(time.perf_counter() - t0)
+        lib.ouro_debug_cbor_stats(stats.ctypes.data)
+        print(json.dumps({"kind": "byron", "chunk": chunk, "slots": slots, "threads": threads,
+                          "ms": round(min(ts) * 1e3, 2), "M_per_s": round(n / min(ts) / 1e6, 3),
+                          "gather_ms": round(stats[1], 2), "wait_ms": round(stats[2], 2),
+                          "all_valid": bool(v.all())}), flush=True)
 
 
 if __name__ == "__main__":
