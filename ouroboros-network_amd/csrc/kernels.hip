@@ -2911,7 +2911,17 @@ struct Worker {
       std::function<int()> f = std::move(job);
       lk.unlock();
       int r = ouro_set_device(dev);
-      if (r == OURO_OK) r = f();
+      // nothing thrown in a shard (a host allocation, say) may end the
+      // process from this detached thread: it fails the shard instead
+      if (r == OURO_OK) {
+        try {
+          r = f();
+        } catch (const std::bad_alloc&) {
+          r = fail(OURO_EDEVICE, "out of host memory");
+        } catch (...) {
+          r = fail(OURO_EDEVICE, "shard failed with an exception");
+        }
+      }
       lk.lock();
       rc = r;
       err = r ? t_last_error : std::string();
