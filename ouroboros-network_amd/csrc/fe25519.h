@@ -258,9 +258,14 @@ OURO_FI uint32_t u32_x2(uint32_t v) {
   return 2u * v;
 #endif
 }
+// OURO_MAD_BARRIER=0 (A/B only): no barrier; LLVM then adds each column's
+// carry last and drops most s_nop (profiles/r06p)
+#ifndef OURO_MAD_BARRIER
+#define OURO_MAD_BARRIER 1
+#endif
 OURO_FI uint64_t mad_acc(uint32_t a, uint32_t b, uint64_t c) {
   uint64_t r = (uint64_t)a * b + c;
-#if defined(__HIP_DEVICE_COMPILE__)
+#if defined(__HIP_DEVICE_COMPILE__) && OURO_MAD_BARRIER
   asm("" : "+v"(r));
 #endif
   return r;
