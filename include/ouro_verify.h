@@ -423,6 +423,34 @@ int ouro_byron_verify_cbor(const uint8_t *raw, size_t raw_bytes, const uint64_t 
  * chunks in flight; a device error recomputes the batch on the host path.
  * OURO_EINVAL as for ouro_byron_pack_cbor.) */
 
+/* Byron heavyweight delegation certificates (the "Byron delegation" use of
+ * DSIGN in the north star): a certificate (epoch, issuer XPub, delegate XPub,
+ * signature) -- cardano-ledger-byron's Delegation.Certificate [ext], the
+ * reference's PBftDelegationCert (ouroboros-consensus-byron/src/Ouroboros/
+ * Consensus/Byron/Protocol.hs:30) and the mempool's ByronDlg payload
+ * (.../Byron/Ledger/Mempool.hs:90), whose signature the ledger checks under
+ * the issuer's key with the SignCertificate tag.  Signed bytes, pinned on the
+ * certificate inside the reference's golden Byron header
+ * (tests/test_byron_cert.py):
+ *   0x0a || CBOR(protocol_magic) || CBOR bytes("00" || delegate XPub || CBOR(epoch))
+ * Key = issuer XPub[0:32]; ByronDSIGN acceptance (ouro_byron_ed25519_verify).
+ * _message writes those bytes (at most OURO_BYRON_DLG_MSG_MAX) and returns
+ * their length (0 for NULL arguments); _verify is one certificate on the
+ * host path (0 / -1 / <= -2 as ouro_byron_ed25519_verify); _verify_batch
+ * builds the n messages and runs ouro_byron_ed25519_verify_batch
+ * (verdict[i] = 1 / 0). */
+#define OURO_BYRON_DLG_MSG_MAX 96
+size_t ouro_byron_dlg_cert_message(uint8_t *out, uint32_t protocol_magic,
+                                   const uint8_t *delegate_xpub /* 64 */, uint64_t epoch);
+int ouro_byron_dlg_cert_verify(uint32_t protocol_magic, const uint8_t *issuer_xpub /* 64 */,
+                               const uint8_t *delegate_xpub /* 64 */, uint64_t epoch,
+                               const uint8_t *sig /* 64 */);
+int ouro_byron_dlg_cert_verify_batch(size_t n, uint32_t protocol_magic,
+                                     const uint8_t *issuer_xpub /* n x 64 */,
+                                     const uint8_t *delegate_xpub /* n x 64 */,
+                                     const uint64_t *epoch, const uint8_t *sig /* n x 64 */,
+                                     uint8_t *verdict);
+
 /* The host-side UPDN fold (ledger-specs; the per-header step of
  * SL.updateChainDepState after the crypto): for i = 0..n-1
  *   eta_v <- eta_v (*) eta_nonce[i]

@@ -8,8 +8,8 @@ is the gfx950 library ``lib/libouro_verify.so`` behind the C ABI in
 """
 from . import _native
 from ._native import DeviceError, NativeUnavailable
-from .byron import (ByronDSIGN, pack_byron_cbor, parse_byron_header, verify_byron_cbor,
-                    verify_byron_headers)
+from .byron import (ByronDSIGN, dlg_cert_message, pack_byron_cbor, parse_byron_header,
+                    verify_byron_cbor, verify_byron_headers, verify_delegation_certs)
 from .dsign import Ed25519DSIGN
 from .header import verify_headers_cbor, verify_integrity_cbor
 from .kes import Sum6KES, kes_period
@@ -26,10 +26,12 @@ __all__ = [
     "Sum6KES",
     "first_invalid",
     "kes_period",
+    "dlg_cert_message",
     "pack_byron_cbor",
     "parse_byron_header",
     "verify_byron_cbor",
     "verify_byron_headers",
+    "verify_delegation_certs",
     "verify_headers",
     "verify_headers_cbor",
     "verify_headers_multi",

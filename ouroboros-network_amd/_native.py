@@ -101,6 +101,9 @@ SIGNATURES = {
     "ouro_sum6kes_verify": (_I, [_P, ctypes.c_uint, _P, _ULL, _P]),
     "ouro_ed25519_verify_batch": (_I, [_SZ, _P, _P, _P, _P, _P, _P]),
     "ouro_byron_ed25519_verify_batch": (_I, [_SZ, _P, _P, _P, _P, _P, _P]),
+    "ouro_byron_dlg_cert_message": (_SZ, [_P, ctypes.c_uint32, _P, ctypes.c_uint64]),
+    "ouro_byron_dlg_cert_verify": (_I, [ctypes.c_uint32, _P, _P, ctypes.c_uint64, _P]),
+    "ouro_byron_dlg_cert_verify_batch": (_I, [_SZ, ctypes.c_uint32, _P, _P, _P, _P, _P]),
     "ouro_vrf03_verify_batch": (_I, [_SZ, _P, _P, _P, _P, _P, _P, _P]),
     "ouro_vrf03_verify_batch_flags": (_I, [_SZ, _P, _P, _P, _P, _P, _P, _P, ctypes.c_uint32]),
     "ouro_vrf03_verify_batch_device_flags": (_I, [_P, _SZ, _P, _P, _P, _P, _P, _P, _P,

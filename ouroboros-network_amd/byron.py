@@ -55,6 +55,49 @@ def sign_tag_block(magic: int, gen_xpub: bytes) -> bytes:
     return b"01" + bytes(gen_xpub) + b"\x09" + cbor_uint(magic)
 
 
+# ---- delegation certificates ---------------------------------------------------
+# A heavyweight delegation certificate (epoch, issuer XPub, delegate XPub,
+# signature): cardano-ledger-byron's Delegation.Certificate [ext], the
+# reference's PBftDelegationCert
+# (ouroboros-consensus-byron/src/Ouroboros/Consensus/Byron/Protocol.hs:30) and
+# the mempool's ByronDlg payload (.../Byron/Ledger/Mempool.hs:90).  The ledger
+# verifies its signature under the issuer's key with the SignCertificate tag;
+# the signed bytes below are pinned on the certificate the reference's golden
+# Byron header carries (tests/test_byron_cert.py).  C ABI:
+# ouro_byron_dlg_cert_{message,verify,verify_batch} (csrc/byron_dlg.cpp).
+DLG_MSG_MAX = 96
+
+
+def dlg_cert_message(magic: int, delegate_xpub: bytes, epoch: int) -> bytes:
+    """0x0a || CBOR(magic) || CBOR bytes("00" || delegate XPub || CBOR(epoch))."""
+    if len(delegate_xpub) != SIZE_VERKEY:
+        raise ValueError("delegate key must be a 64-byte XPub")
+    inner = b"00" + bytes(delegate_xpub) + cbor_uint(epoch)
+    return b"\x0a" + cbor_uint(magic) + bytes([0x58, len(inner)]) + inner
+
+
+def verify_delegation_certs(issuer_xpubs, delegate_xpubs, epochs, sigs,
+                            protocol_magic: int) -> np.ndarray:
+    """The certificates' signatures (ByronDSIGN acceptance) under the node's
+    ProtocolMagicId, on the device (ouro_byron_dlg_cert_verify_batch); a
+    bool array."""
+    iss = as_rows(issuer_xpubs, SIZE_VERKEY, "issuer XPub")
+    dlg = as_rows(delegate_xpubs, SIZE_VERKEY, "delegate XPub")
+    sg = as_rows(sigs, SIZE_SIG, "sig")
+    ep = np.ascontiguousarray(np.asarray(epochs, dtype=np.uint64).reshape(-1))
+    n = iss.shape[0]
+    if dlg.shape[0] != n or sg.shape[0] != n or ep.shape[0] != n:
+        raise ValueError("certificate arrays differ in length")
+    if not 0 <= int(protocol_magic) <= WORD32_MAX:
+        raise ValueError("protocol magic outside Word32")
+    out = np.zeros(n, dtype=np.uint8)
+    if n:
+        rc = _native.load().ouro_byron_dlg_cert_verify_batch(n, int(protocol_magic), ptr(iss),
+                                                             ptr(dlg), ptr(ep), ptr(sg), ptr(out))
+        _native.check(rc, "ouro_byron_dlg_cert_verify_batch")
+    return out.astype(bool)
+
+
 class ByronDSIGN:
     """Verification half of ByronDSIGN (DSIGN.hs:63-120)."""
 
@@ -132,6 +175,8 @@ class ByronHeader:
     delegate_xpub: bytes  # signing (delegate) key
     sig: bytes            # 64-byte block signature
     slot_raw: bytes
+    cert_epoch: int = 0   # the delegation certificate's epoch
+    cert_sig: bytes = b""  # its signature (issuer key over dlg_cert_message)
 
     def message(self, protocol_magic: Union[int, str]) -> bytes:
         """signTag magic (SignBlock genKey) || signed bytes; magic = the node's
@@ -242,8 +287,20 @@ def _parse(raw: bytes) -> Optional[ByronHeader]:
     raw_of = lambda it: buf[it[0]:it[1]]  # noqa: E731
     to_sign = (b"\x85" + raw_of(f[1]) + raw_of(f[2]) + raw_of(cons[0]) + raw_of(cons[2])
                + raw_of(f[4]))
+    # the certificate's epoch and signature (not checked by PBFT's header
+    # validation; dlg_cert_message / verify_delegation_certs): kept when well
+    # formed, else left empty -- they never change the header's status
+    cert_epoch, cert_sig = 0, b""
+    try:
+        mt, ep, _ = _head(buf, cert[0][0])
+        mt2, ln, j2 = _head(buf, cert[3][0])
+        if mt == 0 and ep >= 0 and mt2 == 2 and ln == SIZE_SIG and j2 + ln <= len(buf):
+            cert_epoch, cert_sig = ep, bytes(buf[j2:j2 + ln])
+    except (CBORError, IndexError):
+        pass
     return ByronHeader(magic=magic, to_sign=to_sign, issuer_xpub=vals[0], delegate_xpub=vals[1],
-                       sig=vals[2], slot_raw=raw_of(cons[0]))
+                       sig=vals[2], slot_raw=raw_of(cons[0]), cert_epoch=cert_epoch,
+                       cert_sig=cert_sig)
 
 
 def byron_status(raw: bytes) -> Tuple[int, Optional[ByronHeader]]:

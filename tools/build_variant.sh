@@ -15,5 +15,5 @@ F="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wall -Wno-unused-function $*"
 /opt/rocm/bin/hipcc -O2 -std=c++17 -fPIC -c -o "$B/numa.o" csrc/numa.cpp &
 /opt/rocm/bin/hipcc -O2 -std=c++17 -fPIC -c -o "$B/task_pool.o" csrc/task_pool.cpp &
 wait
-/opt/rocm/bin/hipcc --hip-link -shared -fPIC -o "lib/variants/$NAME.so" "$B/kernels.o" "$B/kernels_lat.o" "$B/pack.o" "$B/host_path.o" "$B/numa.o" "$B/task_pool.o" build/knobs.o -lpthread
+/opt/rocm/bin/hipcc --hip-link -shared -fPIC -o "lib/variants/$NAME.so" "$B/kernels.o" "$B/kernels_lat.o" "$B/pack.o" "$B/host_path.o" "$B/numa.o" "$B/task_pool.o" build/knobs.o build/byron_dlg.o -lpthread
 echo "lib/variants/$NAME.so"
