@@ -1243,6 +1243,24 @@ def byron_leg(n: int, threads: int, reps: int = 3):
     for r in raws[:m]:
         B.byron_status(r)
     tpy = time.perf_counter() - t0
+    # delegation certificates: the golden regular header's own certificate
+    # repeated to n (ouro_byron_dlg_cert_verify_batch: messages built on the
+    # host, ByronDSIGN kernel), every eighth with one signature bit flipped
+    h = next(x for x in (B.byron_status(w)[1] for w in wires) if x is not None)
+    iss = np.tile(np.frombuffer(h.issuer_xpub, np.uint8), (n, 1))
+    dlg = np.tile(np.frombuffer(h.delegate_xpub, np.uint8), (n, 1))
+    sig = np.tile(np.frombuffer(h.cert_sig, np.uint8), (n, 1))
+    sig[::8, 5] ^= 0x20
+    ep = np.full(n, h.cert_epoch, np.uint64)
+    dv = B.verify_delegation_certs(iss, dlg, ep, sig, h.magic)  # warm
+    td = min(_timed(lambda: B.verify_delegation_certs(iss, dlg, ep, sig, h.magic))
+             for _ in range(reps))
+    bad = np.zeros(n, bool)
+    bad[::8] = True
+    dlg_out = {"certificates": n, "certs_per_s": round(n / td, 1),
+               "verdicts_as_expected": bool((dv == ~bad).all()),
+               "note": "golden certificate repeated, 1/8 with a flipped signature bit; host "
+                       "arrays in, verdicts out"}
     return {"headers": n, "all_valid": bool(v.all()),
             "boundary_headers": int((st == B.PACK_EBB).sum()),
             "pack_headers_per_s": round(n / tp, 1), "pack_threads": threads,
@@ -1250,6 +1268,7 @@ def byron_leg(n: int, threads: int, reps: int = 3):
             "verify_cbor_multi": {"devices": mdevs, "headers_per_s": round(n / tm, 1),
                                   "equals_one_device": bool((vm == v).all())},
             "python_slicer_headers_per_s": round(m / tpy, 1),
+            "delegation_certificates": dlg_out,
             "note": "golden Byron headers repeated; pageable host memory in, verdicts out; "
                     "since round 6 on the raw-CBOR pipeline (pinned staging, device Byron "
                     "slicer, ByronDSIGN kernel, 5 chunks in flight)"}

@@ -18,11 +18,13 @@
 //
 // Host code: the messages are built here and verified through the ByronDSIGN
 // batch (device kernel; host path for single items and after a device error).
+#include <algorithm>
 #include <cstring>
 #include <memory>
 #include <new>
 
 #include "../../include/ouro_verify.h"
+#include "task_pool.h"
 
 namespace {
 
@@ -37,6 +39,10 @@ size_t put_uint(uint8_t* o, uint64_t v, uint8_t major = 0) {
   o[0] = (uint8_t)(mt | (w == 1 ? 24 : w == 2 ? 25 : w == 4 ? 26 : 27));
   for (int i = 0; i < w; i++) o[1 + i] = (uint8_t)(v >> (8 * (w - 1 - i)));
   return 1 + (size_t)w;
+}
+
+size_t uint_len(uint64_t v) {
+  return v < 24 ? 1 : v < (1ull << 8) ? 2 : v < (1ull << 16) ? 3 : v < (1ull << 32) ? 5 : 9;
 }
 
 // the signed bytes of one certificate into o (at most OURO_BYRON_DLG_MSG_MAX)
@@ -86,14 +92,28 @@ int ouro_byron_dlg_cert_verify_batch(size_t n, uint32_t protocol_magic,
   std::unique_ptr<uint64_t[]> off(new (std::nothrow) uint64_t[n]);
   std::unique_ptr<uint32_t[]> len(new (std::nothrow) uint32_t[n]);
   if (!msg || !pk || !off || !len) return OURO_EDEVICE;  // out of host memory
+  // offsets first (a message's length is fixed by the magic and its epoch's
+  // CBOR size), then the messages and keys on the library's worker pool:
+  // with one thread the first touch of ~100 MB of fresh pages would
+  // dominate a 1M-certificate call
+  const size_t fixed = 1 + uint_len(protocol_magic) + 2 + 2 + 64;
   uint64_t at = 0;
   for (size_t i = 0; i < n; i++) {
     off[i] = at;
-    len[i] = (uint32_t)dlg_message(msg.get() + at, protocol_magic, delegate_xpub + 64 * i,
-                                   epoch[i]);
+    len[i] = (uint32_t)(fixed + uint_len(epoch[i]));
     at += len[i];
-    memcpy(pk.get() + 32 * i, issuer_xpub + 64 * i, 32);  // XPub[0:32]
   }
+  const size_t rows = 16384;
+  const size_t tasks = (n + rows - 1) / rows;
+  const int width = std::max(1, std::min(16, ouro_pool::usable_cpus()));
+  const int rc = ouro_pool::parallel_for(tasks, width, [&](size_t t) {
+    const size_t lo = t * rows, hi = std::min(n, lo + rows);
+    for (size_t i = lo; i < hi; i++) {
+      dlg_message(msg.get() + off[i], protocol_magic, delegate_xpub + 64 * i, epoch[i]);
+      memcpy(pk.get() + 32 * i, issuer_xpub + 64 * i, 32);  // XPub[0:32]
+    }
+  });
+  if (rc) return OURO_EDEVICE;
   return ouro_byron_ed25519_verify_batch(n, pk.get(), sig, msg.get(), off.get(), len.get(),
                                          verdict);
 }
