@@ -213,6 +213,18 @@ int dh_half_scalars(const uint8_t* h32, uint8_t* c0, uint8_t* c1, int* c0_neg) {
   *c0_neg = hs.c0_neg ? 1 : 0;
   return hs.bits;
 }
+// the round-1 reduction (lattice.h ed25519_half_scalars_v1), for the
+// equivalence test of the round-6 step
+int dh_half_scalars_v1(const uint8_t* h32, uint8_t* c0, uint8_t* c1, int* c0_neg) {
+  uint32_t h[8];
+  bytes_to_words8(h, h32);
+  HalfScalars hs;
+  ed25519_half_scalars_v1(hs, h);
+  memcpy(c0, hs.c0, 32);
+  memcpy(c1, hs.c1, 32);
+  *c0_neg = hs.c0_neg ? 1 : 0;
+  return hs.bits;
+}
 int dh_ed25519_verify(const uint8_t* sig, const uint8_t* m, uint32_t mlen, const uint8_t* pk) {
   uint32_t s[16], p[8];
   for (int i = 0; i < 16; i++) s[i] = ld_le32(sig + 4 * i);

@@ -153,91 +153,10 @@ struct HalfScalars {
   int bits;        // max(bitlen |c0|, bitlen c1)
 };
 
-// (c0, c1) for h < 2^253: c0 = c1 h (mod 8L), c1 odd, both short.
-OURO_HD inline void ed25519_half_scalars(HalfScalars& out, const uint32_t h[8]) {
-  i288 ru = i288_8L(), rv, tu, tv;
-#pragma unroll
-  for (int i = 0; i < 9; i++) {
-    rv.w[i] = i < 8 ? h[i] : 0u;
-    tu.w[i] = 0;
-    tv.w[i] = i == 0 ? 1u : 0u;
-  }
-  // invariant: ru >= rv >= 0, r = t h (mod 8L) for both rows
-#pragma unroll 1
-  for (int outer = 0; outer < 12; outer++) {
-    if (i288_bitlen(rv) <= 128) break;
-    const int len = i288_bitlen(ru);
-    const int sh = len > 64 ? len - 64 : 0;
-    uint64_t x = i288_bits64(ru, sh), y = i288_bits64(rv, sh);
-    // rows of the step matrix: u' = m00 u + m01 v, v' = m10 u + m11 v
-    int64_t m00 = 1, m01 = 0, m10 = 0, m11 = 1;
-    bool moved = false;
-    // stop when the leading bits are used up (y < 2^32) or when r_v crosses
-    // 2^128 (y < 2^(128 - sh)), so that u stays the last remainder above it
-    // (sh >= 65 here: r_u > r_v > 2^128)
-    const int ybits = 128 - sh > 32 ? 128 - sh : 32;
-#if OURO_LATTICE_QUOT
-#pragma unroll 1
-    for (int it = 0; it < 96; it++) {
-      if (y < (1ull << ybits)) break;
-      // q = floor(x / y) >= 1 (x >= y): the double quotient scaled down by
-      // 2^-48 never exceeds it (x, y rounded to 53 bits: relative error
-      // < 2^-51 in the ratio), and is at most 1 short -- fixed exactly below
-      uint64_t q = (uint64_t)((double)x / (double)y * (1.0 - 0x1p-48));
-      if (q == 0) q = 1;
-      uint64_t r = x - q * y;  // q y <= x: no wrap
-      if (r >= y) {
-        q++;
-        r -= y;
-      }
-      // keep |m| < 2^31: the modified row grows to |m0| + q |m1|
-      if (q >= (1ull << 31)) break;
-      const int64_t a10 = m10 < 0 ? -m10 : m10, a11 = m11 < 0 ? -m11 : m11;
-      const int64_t a00 = m00 < 0 ? -m00 : m00, a01 = m01 < 0 ? -m01 : m01;
-      if (a00 + (int64_t)q * a10 >= (1ll << 31) || a01 + (int64_t)q * a11 >= (1ll << 31)) break;
-      m00 -= (int64_t)q * m10;
-      m01 -= (int64_t)q * m11;
-      moved = true;
-      // r < y: swap the rows
-      x = y;
-      y = r;
-      int64_t t = m00; m00 = m10; m10 = t;
-      t = m01; m01 = m11; m11 = t;
-    }
-#else
-#pragma unroll 1
-    for (int it = 0; it < 96; it++) {
-      if (y < (1ull << ybits)) break;
-      int s = clz64(y) - clz64(x);
-      if ((y << s) > x) s--;
-      const int64_t a10 = m10 < 0 ? -m10 : m10, a11 = m11 < 0 ? -m11 : m11;
-      const int64_t a00 = m00 < 0 ? -m00 : m00, a01 = m01 < 0 ? -m01 : m01;
-      const int64_t big1 = a10 > a11 ? a10 : a11, big0 = a00 > a01 ? a00 : a01;
-      if ((big1 << s) + big0 >= (1ll << 31)) break;  // keep |m| < 2^31
-      x -= y << s;
-      m00 -= m10 * ((int64_t)1 << s);
-      m01 -= m11 * ((int64_t)1 << s);
-      moved = true;
-      if (x < y) {
-        const uint64_t tx = x; x = y; y = tx;
-        int64_t q = m00; m00 = m10; m10 = q;
-        q = m01; m01 = m11; m11 = q;
-      }
-    }
-#endif
-    if (!moved) break;
-    i288 nu = i288_add(i288_mul_s32(ru, (int32_t)m00), i288_mul_s32(rv, (int32_t)m01));
-    i288 nv = i288_add(i288_mul_s32(ru, (int32_t)m10), i288_mul_s32(rv, (int32_t)m11));
-    i288 ntu = i288_add(i288_mul_s32(tu, (int32_t)m00), i288_mul_s32(tv, (int32_t)m01));
-    i288 ntv = i288_add(i288_mul_s32(tu, (int32_t)m10), i288_mul_s32(tv, (int32_t)m11));
-    // the approximation may overshoot: (-r, -t) is the same lattice vector's negative
-    if (i288_is_neg(nu)) { i288_negate(nu); i288_negate(ntu); }
-    if (i288_is_neg(nv)) { i288_negate(nv); i288_negate(ntv); }
-    const bool sw = i288_lt(nu, nv);
-    i288_cswap(nu, nv, sw);
-    i288_cswap(ntu, ntv, sw);
-    ru = nu; rv = nv; tu = ntu; tv = ntv;
-  }
+// The common end of both reductions: from the rows (ru, tu), (rv, tv) with
+// ru > rv around 2^128, the shortest candidate with odd t, re-checked.
+OURO_HD inline void half_scalars_finish(HalfScalars& out, const uint32_t h[8], const i288& ru,
+                                        const i288& rv, const i288& tu, const i288& tv) {
   // one Euclid step past v: w = u - q v, q from the leading bits (any integer
   // q keeps w in the lattice; the right one makes it the next remainder)
   i288 rw = rv, tw = tv;
@@ -333,6 +252,205 @@ OURO_HD inline void ed25519_half_scalars(HalfScalars& out, const uint32_t h[8]) 
     best = i288_bitlen(hv);
   }
   out.bits = best;
+}
+
+
+// (c0, c1) for h < 2^253: c0 = c1 h (mod 8L), c1 odd, both short -- the
+// round-1 form (int64 cofactors, an IEEE division per step; A/B and the
+// equivalence test of tests/test_devcode_host.py).
+OURO_HD inline void ed25519_half_scalars_v1(HalfScalars& out, const uint32_t h[8]) {
+  i288 ru = i288_8L(), rv, tu, tv;
+#pragma unroll
+  for (int i = 0; i < 9; i++) {
+    rv.w[i] = i < 8 ? h[i] : 0u;
+    tu.w[i] = 0;
+    tv.w[i] = i == 0 ? 1u : 0u;
+  }
+  // invariant: ru >= rv >= 0, r = t h (mod 8L) for both rows
+#pragma unroll 1
+  for (int outer = 0; outer < 12; outer++) {
+    if (i288_bitlen(rv) <= 128) break;
+    const int len = i288_bitlen(ru);
+    const int sh = len > 64 ? len - 64 : 0;
+    uint64_t x = i288_bits64(ru, sh), y = i288_bits64(rv, sh);
+    // rows of the step matrix: u' = m00 u + m01 v, v' = m10 u + m11 v
+    int64_t m00 = 1, m01 = 0, m10 = 0, m11 = 1;
+    bool moved = false;
+    // stop when the leading bits are used up (y < 2^32) or when r_v crosses
+    // 2^128 (y < 2^(128 - sh)), so that u stays the last remainder above it
+    // (sh >= 65 here: r_u > r_v > 2^128)
+    const int ybits = 128 - sh > 32 ? 128 - sh : 32;
+#if OURO_LATTICE_QUOT
+#pragma unroll 1
+    for (int it = 0; it < 96; it++) {
+      if (y < (1ull << ybits)) break;
+      // q = floor(x / y) >= 1 (x >= y): the double quotient scaled down by
+      // 2^-48 never exceeds it (x, y rounded to 53 bits: relative error
+      // < 2^-51 in the ratio), and is at most 1 short -- fixed exactly below
+      uint64_t q = (uint64_t)((double)x / (double)y * (1.0 - 0x1p-48));
+      if (q == 0) q = 1;
+      uint64_t r = x - q * y;  // q y <= x: no wrap
+      if (r >= y) {
+        q++;
+        r -= y;
+      }
+      // keep |m| < 2^31: the modified row grows to |m0| + q |m1|
+      if (q >= (1ull << 31)) break;
+      const int64_t a10 = m10 < 0 ? -m10 : m10, a11 = m11 < 0 ? -m11 : m11;
+      const int64_t a00 = m00 < 0 ? -m00 : m00, a01 = m01 < 0 ? -m01 : m01;
+      if (a00 + (int64_t)q * a10 >= (1ll << 31) || a01 + (int64_t)q * a11 >= (1ll << 31)) break;
+      m00 -= (int64_t)q * m10;
+      m01 -= (int64_t)q * m11;
+      moved = true;
+      // r < y: swap the rows
+      x = y;
+      y = r;
+      int64_t t = m00; m00 = m10; m10 = t;
+      t = m01; m01 = m11; m11 = t;
+    }
+#else
+#pragma unroll 1
+    for (int it = 0; it < 96; it++) {
+      if (y < (1ull << ybits)) break;
+      int s = clz64(y) - clz64(x);
+      if ((y << s) > x) s--;
+      const int64_t a10 = m10 < 0 ? -m10 : m10, a11 = m11 < 0 ? -m11 : m11;
+      const int64_t a00 = m00 < 0 ? -m00 : m00, a01 = m01 < 0 ? -m01 : m01;
+      const int64_t big1 = a10 > a11 ? a10 : a11, big0 = a00 > a01 ? a00 : a01;
+      if ((big1 << s) + big0 >= (1ll << 31)) break;  // keep |m| < 2^31
+      x -= y << s;
+      m00 -= m10 * ((int64_t)1 << s);
+      m01 -= m11 * ((int64_t)1 << s);
+      moved = true;
+      if (x < y) {
+        const uint64_t tx = x; x = y; y = tx;
+        int64_t q = m00; m00 = m10; m10 = q;
+        q = m01; m01 = m11; m11 = q;
+      }
+    }
+#endif
+    if (!moved) break;
+    i288 nu = i288_add(i288_mul_s32(ru, (int32_t)m00), i288_mul_s32(rv, (int32_t)m01));
+    i288 nv = i288_add(i288_mul_s32(ru, (int32_t)m10), i288_mul_s32(rv, (int32_t)m11));
+    i288 ntu = i288_add(i288_mul_s32(tu, (int32_t)m00), i288_mul_s32(tv, (int32_t)m01));
+    i288 ntv = i288_add(i288_mul_s32(tu, (int32_t)m10), i288_mul_s32(tv, (int32_t)m11));
+    // the approximation may overshoot: (-r, -t) is the same lattice vector's negative
+    if (i288_is_neg(nu)) { i288_negate(nu); i288_negate(ntu); }
+    if (i288_is_neg(nv)) { i288_negate(nv); i288_negate(ntv); }
+    const bool sw = i288_lt(nu, nv);
+    i288_cswap(nu, nv, sw);
+    i288_cswap(ntu, ntv, sw);
+    ru = nu; rv = nv; tu = ntu; tv = ntv;
+  }
+  half_scalars_finish(out, h, ru, rv, tu, tv);
+}
+
+// a * x mod 2^288 for 0 <= a < 2^32 (two's complement x: the signed product)
+OURO_FI i288 i288_mul_u32(const i288& x, uint32_t a) {
+  i288 r;
+  uint64_t carry = 0;
+#pragma unroll
+  for (int i = 0; i < 9; i++) {
+    const uint64_t t = (uint64_t)x.w[i] * a + carry;
+    r.w[i] = (uint32_t)t;
+    carry = t >> 32;
+  }
+  return r;
+}
+OURO_FI double u64_to_f64(uint64_t v) {
+  return (double)(uint32_t)(v >> 32) * 0x1p32 + (double)(uint32_t)v;
+}
+// 1 / d for 1 <= d < 2^64: the hardware reciprocal refined by two Newton
+// steps (the refinement LLVM's f64 division uses before its final rounding
+// fix-up, which the quotient estimate below does not need)
+OURO_FI double recip_f64(double d) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  double r = __builtin_amdgcn_rcp(d);
+  double e = __builtin_fma(-d, r, 1.0);
+  r = __builtin_fma(r, e, r);
+  e = __builtin_fma(-d, r, 1.0);
+  return __builtin_fma(r, e, r);
+#else
+  return 1.0 / d;
+#endif
+}
+
+// The same reduction with a leaner Lehmer step (round 6): the inner loop
+// keeps the cofactor rows as 32-bit MAGNITUDES -- an exact Euclid step's
+// cofactors alternate in sign, so |m0'| = |m0| + q |m1| and the bound check
+// is the update itself --, estimates q from a Newton-refined reciprocal
+// instead of an IEEE division, converts only the new remainder, and applies
+// the rows as a * r - b * r' (the overall sign is the one the normalisation
+// below fixes anyway).  Same quotients, same breaks, so the same rows and
+// the same (c0, c1) as ed25519_half_scalars_v1 bit for bit
+// (tests/test_devcode_host.py::test_half_scalars_v2_equals_v1).
+OURO_HD inline void ed25519_half_scalars_v2(HalfScalars& out, const uint32_t h[8]) {
+  i288 ru = i288_8L(), rv, tu, tv;
+#pragma unroll
+  for (int i = 0; i < 9; i++) {
+    rv.w[i] = i < 8 ? h[i] : 0u;
+    tu.w[i] = 0;
+    tv.w[i] = i == 0 ? 1u : 0u;
+  }
+#pragma unroll 1
+  for (int outer = 0; outer < 12; outer++) {
+    if (i288_bitlen(rv) <= 128) break;
+    const int len = i288_bitlen(ru);
+    const int sh = len > 64 ? len - 64 : 0;
+    uint64_t x = i288_bits64(ru, sh), y = i288_bits64(rv, sh);
+    // |m00|, |m01| (row 0) and |m10|, |m11| (row 1), all < 2^31
+    uint32_t a0 = 1, b0 = 0, a1 = 0, b1 = 1;
+    bool moved = false;
+    const int ybits = 128 - sh > 32 ? 128 - sh : 32;
+    double xd = u64_to_f64(x), yd = u64_to_f64(y);
+#pragma unroll 1
+    for (int it = 0; it < 96; it++) {
+      if (y < (1ull << ybits)) break;
+      // q = floor(x / y) >= 1: the estimate never exceeds it (relative error
+      // < 2^-51, scaled down by 2^-48) and is at most 1 short
+      const double qd = xd * recip_f64(yd) * (1.0 - 0x1p-48);
+      if (qd >= 0x1p31) break;  // a cofactor would reach 2^31
+      uint32_t q = (uint32_t)qd;
+      q = q ? q : 1u;
+      uint64_t r = x - (uint64_t)q * y;
+      if (r >= y) {
+        q++;
+        r -= y;
+      }
+      const uint64_t na = (uint64_t)q * a1 + a0, nb = (uint64_t)q * b1 + b0;
+      if ((na | nb) >> 31) break;
+      a0 = a1;
+      b0 = b1;
+      a1 = (uint32_t)na;
+      b1 = (uint32_t)nb;
+      moved = true;
+      x = y;
+      y = r;
+      xd = yd;
+      yd = u64_to_f64(r);
+    }
+    if (!moved) break;
+    // u' = +-(a0 u - b0 v), v' = +-(b1 v - a1 u); the sign: the normalisation
+    i288 nu = i288_sub(i288_mul_u32(ru, a0), i288_mul_u32(rv, b0));
+    i288 ntu = i288_sub(i288_mul_u32(tu, a0), i288_mul_u32(tv, b0));
+    i288 nv = i288_sub(i288_mul_u32(rv, b1), i288_mul_u32(ru, a1));
+    i288 ntv = i288_sub(i288_mul_u32(tv, b1), i288_mul_u32(tu, a1));
+    if (i288_is_neg(nu)) { i288_negate(nu); i288_negate(ntu); }
+    if (i288_is_neg(nv)) { i288_negate(nv); i288_negate(ntv); }
+    const bool sw = i288_lt(nu, nv);
+    i288_cswap(nu, nv, sw);
+    i288_cswap(ntu, ntv, sw);
+    ru = nu; rv = nv; tu = ntu; tv = ntv;
+  }
+  half_scalars_finish(out, h, ru, rv, tu, tv);
+}
+
+#ifndef OURO_LATTICE_V2
+#define OURO_LATTICE_V2 1  // 0: the round-1 step (A/B)
+#endif
+OURO_HD inline void ed25519_half_scalars(HalfScalars& out, const uint32_t h[8]) {
+  if constexpr (OURO_LATTICE_V2) ed25519_half_scalars_v2(out, h);
+  else ed25519_half_scalars_v1(out, h);
 }
 
 }  // namespace ouro
