@@ -919,8 +919,13 @@ OURO_FI void fe_mul_xn(fe* h, const fe* f, const fe* g) {
   }
 }
 // N independent squarings in lockstep; element e is scaled by kScale[e]
-// (1: f^2, 2: 2 f^2), one chain each as fe_sq_scan
-template <int N>
+// (1: f^2, 2: 2 f^2), one chain each as fe_sq_scan.  kComp (device only):
+// the elements whose bit is set are returned COMPLEMENTED, limb k as
+// mask_k - h_k -- the same single instruction per limb as the mask
+// ((~t) & mask), limb 1 with its carry subtracted instead of added -- so a
+// caller's Y - h becomes Y + (mask - h) + (2p - mask): one three-input add per
+// limb instead of an add and a subtract (ge25519.h ge_dbl_lockstep).
+template <int N, unsigned kComp = 0>
 OURO_FI void fe_sq_xn(fe* h, const fe* f, const int (&scale)[N]) {
   uint32_t fs[N][10], f2s[N][10], f4s[N][10], f19[N][10];
 #pragma unroll
@@ -961,14 +966,31 @@ OURO_FI void fe_sq_xn(fe* h, const fe* f, const int (&scale)[N]) {
       }
 #pragma unroll
     for (int e = 0; e < N; e++) {
-      hv[e][k] = (uint32_t)t[e] & limb_mask(k);
+      // (limb 0 stays plain: scan_finish adds the wrap to it first)
+      const bool comp = ((kComp >> e) & 1u) && k > 0;
+      hv[e][k] = comp ? ~(uint32_t)t[e] & limb_mask(k) : (uint32_t)t[e] & limb_mask(k);
       c[e] = t[e] >> limb_bits(k);
     }
   }
 #pragma unroll
   for (int e = 0; e < N; e++) {
     OURO_COUNT_SQ();
-    h[e] = scan_finish(hv[e], c[e]);
+    if ((kComp >> e) & 1u) {
+      // scan_finish with the complement: limb 0 = mask_0 - (t0 & mask_0),
+      // limb 1 = (mask_1 - h_1) - (t0 >> 26)
+      const uint64_t t0 = (uint64_t)hv[e][0] + 19ull * c[e];
+      hv[e][0] = ~(uint32_t)t0 & limb_mask(0);
+      hv[e][1] -= (uint32_t)(t0 >> 26);
+#pragma unroll
+      for (int i = 0; i < 10; i++) {
+        h[e].v[i] = hv[e][i];
+#if defined(__HIP_DEVICE_COMPILE__)
+        asm("" : "+v"(h[e].v[i]));  // hide the limb ranges (see fe_carry64)
+#endif
+      }
+    } else {
+      h[e] = scan_finish(hv[e], c[e]);
+    }
     OURO_TRK(trk_sq_scan(h[e], f[e], (unsigned)scale[e], 1));
   }
 }

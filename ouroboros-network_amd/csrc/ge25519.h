@@ -76,6 +76,15 @@ OURO_FI ge_p1p1 ge_p3_dbl(const ge_p3& p) { return ge_p2_dbl(ge_p3_to_p2(p)); }
 // order, so the same bounds, scheduled so no multiply-add waits on the one
 // before it (round 4: 29.3 -> 25.9 ps per chip-wide doubling at two waves per
 // SIMD, profiles/r04/occupancy_lockstep.json).
+// OURO_DBL_COMP (device, the default since round 6): the doubling returns
+// (X, Z) negated -- X = Y' - S, Z = A - B, the same point -- so that S, used
+// only there, comes out of its squaring complemented (fe_sq_xn kComp) and
+// X = Y' + (mask - S) + (2p - mask) is one three-input add per limb: the
+// limbs are exactly fe_sub(Y', S)'s, ~10 VALU fewer per doubling.  The host
+// build (and OURO_DBL_COMP=0) computes the same limbs with fe_sub.
+#ifndef OURO_DBL_COMP
+#define OURO_DBL_COMP 1
+#endif
 OURO_FI ge_p1p1 ge_dbl_lockstep(const ge_p1p1& t) {
   const fe f[3] = {t.T, t.Z, t.T}, g[3] = {t.X, t.Y, t.Z};
   fe p[3];
@@ -83,11 +92,23 @@ OURO_FI ge_p1p1 ge_dbl_lockstep(const ge_p1p1& t) {
   const fe in[4] = {p[0], p[1], p[2], fe_add(p[0], p[1])};
   constexpr int kScale[4] = {1, 1, 2, 1};  // A = X^2, B = Y^2, C = 2 Z^2, S = (X + Y)^2
   fe o[4];
-  fe_sq_xn<4>(o, in, kScale);
   ge_p1p1 r;
+#if defined(__HIP_DEVICE_COMPILE__)
+  if constexpr (OURO_DBL_COMP) {
+    fe_sq_xn<4, 8u>(o, in, kScale);  // o[3] = mask - S
+    r.Y = fe_carry(fe_add(o[1], o[0]));
+    r.Z = fe_sub(o[0], o[1]);
+#pragma unroll
+    for (int i = 0; i < 10; i++)
+      r.X.v[i] = r.Y.v[i] + o[3].v[i] + (kp_limb(2, i) - limb_mask(i));
+    r.T = fe_sub(fe_add(o[2], o[0]), o[1]);
+    return r;
+  }
+#endif
+  fe_sq_xn<4>(o, in, kScale);
   r.Y = fe_carry(fe_add(o[1], o[0]));
-  r.Z = fe_sub(o[1], o[0]);
-  r.X = fe_sub(o[3], r.Y);
+  r.Z = OURO_DBL_COMP ? fe_sub(o[0], o[1]) : fe_sub(o[1], o[0]);
+  r.X = OURO_DBL_COMP ? fe_sub(r.Y, o[3]) : fe_sub(o[3], r.Y);
   r.T = fe_sub(fe_add(o[2], o[0]), o[1]);
   return r;
 }
